@@ -1,0 +1,217 @@
+#!/usr/bin/env python
+"""Benchmark: k-point FFT-ISDF build + get_jk (BASELINE.json metric) on MI355X.
+
+A "step" is one full ISDF build (selection, x4, y, per-q fit + FFT Coulomb, W_s) plus
+one get_jk on a synthetic diamond gth-dzvp-shaped cell, 4x4x4 k-mesh, nip = 600,
+36^3 FFT mesh.  AO values (PySCF's job in the reference)
+are evaluated once on the host and are resident in HBM before the timed region.
+
+  python bench.py [--gpus N --steps K --warmup W] [--config c3|c2|c1] [--no-cpu-baseline]
+
+For N > 1 launch with torch.distributed.run; k-points are sharded over ranks (RCCL
+all-reduce of W_s + broadcast of W_0), rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "fft-isdf-scratch_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+CONFIGS = {
+    # name: (basis, mesh, kmesh, m0, nip)
+    "c3": ("gth-dzvp", (36, 36, 36), (4, 4, 4), (15, 15, 15), 600),
+    "c2": ("gth-dzvp", (36, 36, 36), (2, 2, 2), (15, 15, 15), 300),
+    "c1": ("gth-szv", (8, 8, 8), (1, 1, 1), (15, 15, 15), 160),
+}
+DESC = {
+    "c3": "diamond gth-dzvp-shaped, 4x4x4 k-mesh, nip 600, mesh 36^3 (C3)",
+    "c2": "diamond gth-dzvp-shaped, 2x2x2 k-mesh, nip 300, mesh 36^3 (C2)",
+    "c1": "diamond gth-szv-shaped, Gamma, nip 160, mesh 8^3 (C1)",
+}
+PEAK_FP64_TFLOPS = 78.6  # MI355X FP64 matrix (= vector) dense peak, MI355X_MICROARCH / BASELINE.md
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-q", type=int, default=2, help="q-points timed in the CPU sample")
+    return p.parse_args()
+
+
+def setup(cfg):
+    from fisdf import cell as C
+    basis, mesh, kmesh, m0, nip = CONFIGS[cfg]
+    cell = C.diamond_cell(basis=basis, mesh=mesh)
+    nao = cell.nao_nr()
+    c0 = (nip + 0.5) / nao                                    # int(nao*c0) == nip
+    x0 = C.eval_ao_kpts(cell, cell.gen_uniform_grids(m0), kmesh)
+    chi = C.eval_ao_kpts(cell, cell.gen_uniform_grids(mesh), kmesh)
+    dm = C.make_dm(nao, kmesh, cell, seed=1234)
+    return cell, kmesh, m0, c0, x0, chi, dm
+
+
+def cpu_baseline(cell, kmesh, m0, c0, x0, chi, dm, nq):
+    """Oracle (NumPy/SciPy restatement of fftisdf.py) on a bounded sample of the same job,
+    extrapolated to the whole job: selection + x4 + y for a grid slice + fit/FFT/W for nq
+    q-points + get_jk, scaled by ngrid/slice and nk/nq."""
+    from oracle import isdf_ref as R
+    import scipy
+    nk = chi.shape[0]
+    ngrid = chi.shape[1]
+    t = {}
+    t0 = time.perf_counter()
+    perm, rank, nip, _ = R.select_interpolation_points(x0, cell.nao_nr(), c0)
+    t["select"] = time.perf_counter() - t0
+    xip = x0[:, perm]
+    kpts = R.get_kpts(cell.a, kmesh)
+    phase = R.get_phase(cell.a, kpts, kmesh)
+    t0 = time.perf_counter()
+    x4 = R.build_x4(xip, phase)
+    t["x4"] = time.perf_counter() - t0
+    blk = min(ngrid, 4000)
+    t0 = time.perf_counter()
+    yb = R.build_y(chi[:, :blk], xip, phase)
+    t["y"] = (time.perf_counter() - t0) * ngrid / blk
+    del yb
+    # fit + Coulomb for nq q-points on the full grid (needs y_q for all g: build per q)
+    coords = cell.gen_uniform_grids(cell.mesh)
+    Gv = R.get_Gv(cell.a, cell.mesh)
+    tq = 0.0
+    for q in range(nq):
+        # y_q over the whole grid (excluded from the fit timing: counted in t["y"])
+        yq = np.empty((ngrid, nip), complex)
+        for g0 in range(0, ngrid, 8000):
+            g1 = min(g0 + 8000, ngrid)
+            fx = np.asarray([f.conj() @ x.T for f, x in zip(chi[:, g0:g1], xip)])
+            fs = (phase @ fx.reshape(nk, -1)).real ** 2
+            yq[g0:g1] = (phase[:, q] @ fs.reshape(nk, -1)).reshape(g1 - g0, nip)
+        t0 = time.perf_counter()
+        R.fit_and_coulomb(x4[q], yq, kpts[q], coords, cell.a, cell.mesh, cell.vol, Gv)
+        tq += time.perf_counter() - t0
+    t["fit"] = tq * nk / nq
+    dms = dm[None]
+    t0 = time.perf_counter()
+    wq = np.zeros((nk, nip, nip), complex)  # timing only: get_jk cost is independent of values
+    R.get_k_kpts(xip, wq, dms, phase)
+    R.get_j_kpts(xip, wq[0], dms)
+    t["get_jk"] = time.perf_counter() - t0
+    total = sum(t.values())
+    cores = os.cpu_count()
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max(i.get("num_threads", 1) for i in threadpool_info()) or cores
+    except Exception:
+        pass
+    return dict(value=nk / total, unit="k-points/s", cores=int(cores), kind="port",
+                sample=(f"oracle (NumPy/SciPy gelsy restatement of fftisdf.py) timed on "
+                        f"selection + x4 + y on {blk}/{ngrid} grid points + fit/FFT/W for "
+                        f"{nq}/{nk} q + get_jk, extrapolated to the full job "
+                        f"(est. {total:.1f} s/job)"),
+                stages_s={k: round(v, 3) for k, v in t.items()})
+
+
+def main():
+    args = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    comm = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        comm = dist.group.WORLD
+
+    from fisdf import ISDF
+    from fisdf import _lib
+    cell, kmesh, m0, c0, x0, chi, dm = setup(args.config)
+    nk = int(np.prod(kmesh))
+    df = ISDF(cell, cell.get_kpts(kmesh), m0=list(m0), c0=c0, comm=comm)
+    d = df.device
+    df._kmesh()
+    df._ao_parent = d.to_dev(x0)
+    df._ao_grid = d.to_dev(chi)
+    del chi
+
+    def step():
+        df._dev_state = None
+        df.build()
+        df.get_jk(dm)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if comm is not None:
+            torch.distributed.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    d.ctx.call("fisdf_set_timing", 1)
+    d.ctx.timings()  # reset
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    dt = time.perf_counter() - t0
+    stages = d.ctx.timings()
+    d.ctx.call("fisdf_set_timing", 0)
+    if comm is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device=d.dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms_per_step = dt / args.steps * 1e3
+    value = nk / (dt / args.steps)
+
+    # roofline of the dominant kernel: the Coulomb HERK W_q = Zhat Zhat^H (one launch per q)
+    ngrid = int(np.prod(cell.mesh))
+    ranks = np.asarray(df.ranks, dtype=np.int64)
+    herk_ms, herk_calls = stages["herk"]
+    herk_flop = 4.0 * float(np.sum(ranks.astype(np.float64) ** 2)) * ngrid * args.steps
+    achieved = herk_flop / (herk_ms * 1e-3) / 1e12 if herk_ms > 0 else 0.0
+    roof = {"bound": "mfma", "kernel": "zgemm_kernel<0,3,true> (HERK W_q, split-K) + reduce",
+            "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP64_TFLOPS, 4), "traffic": None,
+            "flop_per_launch": 4.0 * float(np.mean(ranks.astype(np.float64) ** 2)) * ngrid,
+            "avg_launch_ms": herk_ms / max(herk_calls, 1)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        chi = __import__("fisdf").cell.eval_ao_kpts(cell, cell.gen_uniform_grids(cell.mesh), kmesh)
+        cpu = cpu_baseline(cell, kmesh, m0, c0, x0, chi, dm, args.cpu_q)
+        del chi
+
+    if rank == 0:
+        out = {
+            "metric": "ISDF build + get_jk k-points/s, diamond gth-dzvp 4x4x4"
+            if args.config == "c3" else f"ISDF build + get_jk k-points/s ({args.config})",
+            "value": round(value, 4), "unit": "k-points/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f64 (complex128)", "data": "synthetic (gth-dzvp-shaped contracted Gaussians)",
+            "config": {"workload": DESC[args.config], "nk": nk, "nao": cell.nao_nr(),
+                       "nip": int(df.nip), "ngrid": ngrid, "fit": "pivoted-Cholesky factored",
+                       "parallelism": f"k-shard x{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "stages_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()},
+            "ranks": [int(ranks.min()), int(ranks.max())],
+        }
+        print(json.dumps(out))
+    if comm is not None:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

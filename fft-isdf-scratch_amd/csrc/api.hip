@@ -1,0 +1,728 @@
+// C-ABI of libfisdf.so (include/fisdf.h): orchestration of the HIP kernels that
+// replace the reference's fftisdf.py hot path.  Each entry cites the reference lines
+// it stands in for.
+#include "../../include/fisdf.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <vector>
+
+#include "common.h"
+#include "linalg.h"
+
+namespace fisdf {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+}  // namespace fisdf
+
+using namespace fisdf;
+
+struct fisdf_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  // grow-only scratch arena (sequential use on `stream`)
+  void* arena = nullptr;
+  size_t arena_size = 0;
+  // phase matrices Phi (nimg x nk) keyed by kmesh + lattice
+  std::map<std::vector<double>, cplx*> phase_cache;
+  // per-q factors of x4_q (fisdf_factor_x4)
+  int f_q0 = 0, f_nk = 0, f_nip = 0, f_nb = 64;  // shard [f_q0, f_q0+f_nk)
+  cplx* f_L = nullptr;      // (nk, nip, nip) raw left-looking factor (row order)
+  cplx* f_Lp = nullptr;     // (nk, nip*nip) pivot-order factor, ld = rank_q
+  cplx* f_Linv = nullptr;   // (nk, nblk*nb*nb)
+  int* f_piv = nullptr;     // (nk, nip)
+  std::vector<int> f_rank;  // host copy
+  // reality-invariant monitors
+  unsigned long long* maximag = nullptr;  // 3 slots
+  // timing
+  bool timing = false;
+  struct Ev { int stage; hipEvent_t a, b; };
+  std::vector<Ev> events;
+};
+
+namespace {
+
+int arena_get(fisdf_ctx* c, size_t bytes, void** out) {
+  bytes = std::max<size_t>(bytes, 256);
+  if (bytes > c->arena_size) {
+    FISDF_HIP(hipStreamSynchronize(c->stream));
+    if (c->arena) FISDF_HIP(hipFree(c->arena));
+    c->arena = nullptr;
+    size_t sz = bytes + bytes / 8;
+    FISDF_HIP(hipMalloc(&c->arena, sz));
+    c->arena_size = sz;
+  }
+  *out = c->arena;
+  return 0;
+}
+
+// carve aligned sub-buffers from one arena request
+struct Carver {
+  size_t off = 0;
+  size_t take(size_t bytes) {
+    size_t o = off;
+    off += (bytes + 255) / 256 * 256;
+    return o;
+  }
+};
+
+struct StageTimer {
+  fisdf_ctx* c;
+  int stage;
+  hipEvent_t a = nullptr, b = nullptr;
+  StageTimer(fisdf_ctx* c_, int st) : c(c_), stage(st) {
+    if (c->timing) {
+      (void)hipEventCreate(&a);
+      (void)hipEventCreate(&b);
+      (void)hipEventRecord(a, c->stream);
+    }
+  }
+  ~StageTimer() {
+    if (c->timing) {
+      (void)hipEventRecord(b, c->stream);
+      c->events.push_back({stage, a, b});
+    }
+  }
+};
+
+void lattice(const double a[9], CellGeom& g) {
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) g.a[i][j] = a[3 * i + j];
+  // b = 2 pi inv(a)^T
+  const double(*A)[3] = g.a;
+  double det = A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) -
+               A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
+               A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
+  double inv[3][3];
+  inv[0][0] = (A[1][1] * A[2][2] - A[1][2] * A[2][1]) / det;
+  inv[0][1] = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) / det;
+  inv[0][2] = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) / det;
+  inv[1][0] = (A[1][2] * A[2][0] - A[1][0] * A[2][2]) / det;
+  inv[1][1] = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) / det;
+  inv[1][2] = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) / det;
+  inv[2][0] = (A[1][0] * A[2][1] - A[1][1] * A[2][0]) / det;
+  inv[2][1] = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) / det;
+  inv[2][2] = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) / det;
+  const double twopi = 6.283185307179586;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) g.b[i][j] = twopi * inv[j][i];
+}
+
+double cell_volume(const double a[9]) {
+  return std::fabs(a[0] * (a[4] * a[8] - a[5] * a[7]) - a[1] * (a[3] * a[8] - a[5] * a[6]) +
+                   a[2] * (a[3] * a[7] - a[4] * a[6]));
+}
+
+// k-point q of the mesh (get_kpts order, wrap_around=False): k = (i/n) . b
+void kpoint(const int kmesh[3], const CellGeom& g, int q, double k[3]) {
+  int i2 = q % kmesh[2], i1 = (q / kmesh[2]) % kmesh[1], i0 = q / (kmesh[1] * kmesh[2]);
+  double f[3] = {(double)i0 / kmesh[0], (double)i1 / kmesh[1], (double)i2 / kmesh[2]};
+  for (int c = 0; c < 3; ++c) k[c] = f[0] * g.b[0][c] + f[1] * g.b[1][c] + f[2] * g.b[2][c];
+}
+
+// Phi[R,k] = exp(i T_R . k)/sqrt(nk)  (k2gamma.get_phase, wrap_around=False)
+int get_phase(fisdf_ctx* c, const int kmesh[3], const double a[9], const cplx** out) {
+  std::vector<double> key = {(double)kmesh[0], (double)kmesh[1], (double)kmesh[2]};
+  for (int i = 0; i < 9; ++i) key.push_back(a[i]);
+  auto it = c->phase_cache.find(key);
+  if (it != c->phase_cache.end()) { *out = it->second; return 0; }
+  CellGeom g;
+  lattice(a, g);
+  int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  std::vector<cplx> h((size_t)nk * nk);
+  for (int R = 0; R < nk; ++R) {
+    int r2 = R % kmesh[2], r1 = (R / kmesh[2]) % kmesh[1], r0 = R / (kmesh[1] * kmesh[2]);
+    double T[3];
+    for (int cc = 0; cc < 3; ++cc) T[cc] = r0 * g.a[0][cc] + r1 * g.a[1][cc] + r2 * g.a[2][cc];
+    for (int q = 0; q < nk; ++q) {
+      double k[3];
+      kpoint(kmesh, g, q, k);
+      double th = T[0] * k[0] + T[1] * k[1] + T[2] * k[2];
+      h[(size_t)R * nk + q] = cmk(std::cos(th) / std::sqrt((double)nk), std::sin(th) / std::sqrt((double)nk));
+    }
+  }
+  cplx* d = nullptr;
+  FISDF_HIP(hipMalloc(&d, sizeof(cplx) * h.size()));
+  FISDF_HIP(hipMemcpy(d, h.data(), sizeof(cplx) * h.size(), hipMemcpyHostToDevice));
+  c->phase_cache[key] = d;
+  *out = d;
+  return 0;
+}
+
+int device_guard(fisdf_ctx* c) {
+  FISDF_CHECK(c != nullptr, "null context");
+  FISDF_HIP(hipSetDevice(c->device));
+  return 0;
+}
+
+const cplx ONE = {1.0, 0.0}, ZERO = {0.0, 0.0};
+
+int free_factors(fisdf_ctx* c) {
+  if (c->f_L) FISDF_HIP(hipFree(c->f_L));
+  if (c->f_Lp) FISDF_HIP(hipFree(c->f_Lp));
+  if (c->f_Linv) FISDF_HIP(hipFree(c->f_Linv));
+  if (c->f_piv) FISDF_HIP(hipFree(c->f_piv));
+  c->f_L = c->f_Lp = c->f_Linv = nullptr;
+  c->f_piv = nullptr;
+  c->f_rank.clear();
+  c->f_nk = c->f_nip = 0;
+  return 0;
+}
+
+int pick_ksplit(int M, int N, int K) {
+  long tiles = (long)((M + 63) / 64) * ((N + 63) / 64);
+  int ks = 1;
+  while (tiles * ks < 1024 && K / (ks * 2) >= 512) ks *= 2;
+  return ks;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int fisdf_abi_version(void) { return FISDF_ABI_VERSION; }
+
+const char* fisdf_last_error(void) { return g_last_error.c_str(); }
+
+int fisdf_create(int device, void* stream, fisdf_ctx** out) {
+  FISDF_CHECK(out != nullptr, "out is null");
+  int ndev = 0;
+  FISDF_HIP(hipGetDeviceCount(&ndev));
+  FISDF_CHECK(device >= 0 && device < ndev, "device id out of range (no GPU visible?)");
+  FISDF_HIP(hipSetDevice(device));
+  fisdf_ctx* c = new fisdf_ctx();
+  c->device = device;
+  if (stream) {
+    c->stream = (hipStream_t)stream;
+  } else {
+    FISDF_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->own_stream = true;
+  }
+  FISDF_HIP(hipMalloc(&c->maximag, 4 * sizeof(unsigned long long)));
+  FISDF_HIP(hipMemsetAsync(c->maximag, 0, 4 * sizeof(unsigned long long), c->stream));
+  *out = c;
+  return 0;
+}
+
+int fisdf_destroy(fisdf_ctx* c) {
+  if (!c) return 0;
+  FISDF_HIP(hipSetDevice(c->device));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  for (auto& e : c->events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+  for (auto& kv : c->phase_cache) (void)hipFree(kv.second);
+  free_factors(c);
+  if (c->arena) (void)hipFree(c->arena);
+  if (c->maximag) (void)hipFree(c->maximag);
+  if (c->own_stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return 0;
+}
+
+int fisdf_sync(fisdf_ctx* c) {
+  FISDF_TRY(device_guard(c));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int fisdf_malloc(fisdf_ctx* c, size_t bytes, void** p) {
+  FISDF_TRY(device_guard(c));
+  FISDF_HIP(hipMalloc(p, std::max<size_t>(bytes, 1)));
+  return 0;
+}
+
+int fisdf_free(fisdf_ctx* c, void* p) {
+  FISDF_TRY(device_guard(c));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  FISDF_HIP(hipFree(p));
+  return 0;
+}
+
+int fisdf_memcpy_htod(fisdf_ctx* c, void* d, const void* h, size_t bytes) {
+  FISDF_TRY(device_guard(c));
+  FISDF_HIP(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, c->stream));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int fisdf_memcpy_dtoh(fisdf_ctx* c, void* h, const void* d, size_t bytes) {
+  FISDF_TRY(device_guard(c));
+  FISDF_HIP(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int fisdf_set_timing(fisdf_ctx* c, int enable) {
+  FISDF_TRY(device_guard(c));
+  c->timing = enable != 0;
+  return 0;
+}
+
+int fisdf_timings(fisdf_ctx* c, double* ms, int* calls) {
+  FISDF_TRY(device_guard(c));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  for (int i = 0; i < FISDF_NSTAGES; ++i) {
+    if (ms) ms[i] = 0;
+    if (calls) calls[i] = 0;
+  }
+  for (auto& e : c->events) {
+    float t = 0;
+    FISDF_HIP(hipEventElapsedTime(&t, e.a, e.b));
+    if (ms) ms[e.stage] += t;
+    if (calls) calls[e.stage] += 1;
+    (void)hipEventDestroy(e.a);
+    (void)hipEventDestroy(e.b);
+  }
+  c->events.clear();
+  return 0;
+}
+
+int fisdf_max_imag(fisdf_ctx* c, double* out) {
+  FISDF_TRY(device_guard(c));
+  unsigned long long h[4];
+  FISDF_HIP(hipMemcpyAsync(h, c->maximag, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  for (int i = 0; i < 3; ++i) {
+    double v;
+    std::memcpy(&v, &h[i], sizeof(double));
+    out[i] = v;
+  }
+  FISDF_HIP(hipMemsetAsync(c->maximag, 0, 4 * sizeof(unsigned long long), c->stream));
+  return 0;
+}
+
+// ---- building blocks -------------------------------------------------------
+int fisdf_zgemm(fisdf_ctx* c, int opA, int opB, int M, int N, int K, const double alpha[2],
+                const void* A, long lda, long sA, const void* B, long ldb, long sB,
+                const double beta[2], void* C, long ldc, long sC, int batch, int ksplit) {
+  FISDF_TRY(device_guard(c));
+  cplx* work = nullptr;
+  if (ksplit > 1) {
+    void* w;
+    FISDF_TRY(arena_get(c, sizeof(cplx) * (size_t)ksplit * M * N * batch, &w));
+    work = (cplx*)w;
+  }
+  return zgemm(c->stream, opA, opB, M, N, K, cmk(alpha[0], alpha[1]), (const cplx*)A, lda, sA,
+               (const cplx*)B, ldb, sB, cmk(beta[0], beta[1]), (cplx*)C, ldc, sC, batch,
+               ksplit, work);
+}
+
+int fisdf_herk(fisdf_ctx* c, int n, int K, double alpha, const void* A, long lda, void* Cm,
+               long ldc, int ksplit) {
+  FISDF_TRY(device_guard(c));
+  cplx* work = nullptr;
+  if (ksplit > 1) {
+    void* w;
+    FISDF_TRY(arena_get(c, sizeof(cplx) * (size_t)ksplit * n * n, &w));
+    work = (cplx*)w;
+  }
+  return herk(c->stream, n, K, alpha, (const cplx*)A, lda, (cplx*)Cm, ldc, ksplit, work);
+}
+
+int fisdf_fft3d(fisdf_ctx* c, const void* in, void* out, int rows, const int mesh[3]) {
+  FISDF_TRY(device_guard(c));
+  long ng = (long)mesh[0] * mesh[1] * mesh[2];
+  return fft3d(c->stream, (const cplx*)in, ng, nullptr, (cplx*)out, ng, rows, mesh[0], mesh[1],
+               mesh[2], nullptr, nullptr, nullptr);
+}
+
+int fisdf_coulg(fisdf_ctx* c, const int mesh[3], const double a[9], const double k[3],
+                double scale, int take_sqrt, double* w) {
+  FISDF_TRY(device_guard(c));
+  CellGeom g;
+  lattice(a, g);
+  return coulg_weight(c->stream, mesh, g, k, scale, take_sqrt, w);
+}
+
+int fisdf_pivoted_cholesky(fisdf_ctx* c, const void* A, int n, int batch, int rmax,
+                           double tol_rel, int* h_piv, int* h_rank) {
+  FISDF_TRY(device_guard(c));
+  Carver cv;
+  size_t oL = cv.take(sizeof(cplx) * (size_t)batch * n * rmax);
+  size_t oP = cv.take(sizeof(int) * (size_t)batch * rmax);
+  size_t oR = cv.take(sizeof(int) * batch);
+  size_t oD = cv.take(sizeof(double) * (size_t)batch * n);
+  size_t oF = cv.take(sizeof(int) * batch);
+  size_t oW = cv.take(sizeof(double) * (size_t)batch * (1 + rmax));
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  char* b = (char*)base;
+  FISDF_TRY(pchol(c->stream, (const cplx*)A, n, (long)n * n, n, batch, rmax, tol_rel, 0.0,
+                  (cplx*)(b + oL), (int*)(b + oP), (int*)(b + oR), (double*)(b + oD),
+                  (int*)(b + oF), (double*)(b + oW)));
+  FISDF_HIP(hipMemcpyAsync(h_piv, b + oP, sizeof(int) * (size_t)batch * rmax,
+                           hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipMemcpyAsync(h_rank, b + oR, sizeof(int) * batch, hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// ---- A1 ---------------------------------------------------------------------
+int fisdf_select_points(fisdf_ctx* c, const void* x0v, int nk, int ng0, int nao, int nip_max,
+                        double tol, int* h_perm, int* h_npiv, int* h_full_rank) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(nk > 0 && ng0 > 0 && nao > 0 && nip_max > 0, "select_points: bad sizes");
+  nip_max = std::min(nip_max, ng0);
+  StageTimer tm(c, FISDF_ST_SELECT);
+  const cplx* x0 = (const cplx*)x0v;
+  Carver cv;
+  size_t oX2 = cv.take(sizeof(cplx) * (size_t)ng0 * ng0);
+  size_t oX4 = cv.take(sizeof(cplx) * (size_t)ng0 * ng0);
+  size_t oL = cv.take(sizeof(cplx) * (size_t)ng0 * nip_max);
+  size_t oP = cv.take(sizeof(int) * nip_max);
+  size_t oR = cv.take(sizeof(int) * 4);
+  size_t oD = cv.take(sizeof(double) * ng0);
+  size_t oF = cv.take(sizeof(int) * 4);
+  size_t oW = cv.take(sizeof(double) * (1 + nip_max));
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  char* b = (char*)base;
+  cplx* X2 = (cplx*)(b + oX2);
+  cplx* X4 = (cplx*)(b + oX4);
+  // x2 = sum_q conj(x0_q) x0_q^T   (fftisdf.py:376-378; real part taken below)
+  for (int q = 0; q < nk; ++q) {
+    const cplx* xq = x0 + (size_t)q * ng0 * nao;
+    FISDF_TRY(zgemm(c->stream, OP_R, OP_T, ng0, ng0, nao, ONE, xq, nao, 0, xq, nao, 0,
+                    q ? ONE : ZERO, X2, ng0, 0, 1));
+  }
+  // x4 = Re(x2)^2 / nk  (:379)
+  FISDF_TRY(square_scale(c->stream, X2, 1.0 / nk, X4, (long)ng0 * ng0));
+  // greedy pivoted Cholesky (:381-384), first nip_max pivots
+  FISDF_TRY(pchol(c->stream, X4, ng0, 0, ng0, 1, nip_max, tol, 0.0, (cplx*)(b + oL),
+                  (int*)(b + oP), (int*)(b + oR), (double*)(b + oD), (int*)(b + oF),
+                  (double*)(b + oW)));
+  int rank = 0;
+  FISDF_HIP(hipMemcpyAsync(&rank, b + oR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipMemcpyAsync(h_perm, b + oP, sizeof(int) * nip_max, hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  *h_npiv = rank;
+  if (h_full_rank) *h_full_rank = rank < nip_max ? 1 : 0;
+  return 0;
+}
+
+int fisdf_gather_points(fisdf_ctx* c, const void* x0, int nk, int ng0, int nao, const int* h_perm,
+                        int nip, void* X) {
+  FISDF_TRY(device_guard(c));
+  void* base;
+  FISDF_TRY(arena_get(c, sizeof(int) * (size_t)nip, &base));
+  for (int i = 0; i < nip; ++i) FISDF_CHECK(h_perm[i] >= 0 && h_perm[i] < ng0, "perm out of range");
+  FISDF_HIP(hipMemcpyAsync(base, h_perm, sizeof(int) * nip, hipMemcpyHostToDevice, c->stream));
+  FISDF_TRY(gather_points(c->stream, (const cplx*)x0, nk, ng0, nao, (const int*)base, nip, (cplx*)X));
+  FISDF_HIP(hipStreamSynchronize(c->stream));  // h_perm staging is reused
+  return 0;
+}
+
+// ---- A2 ---------------------------------------------------------------------
+int fisdf_build_x4(fisdf_ctx* c, const void* Xv, int nip, int nao, const int kmesh[3],
+                   const double a[9], void* x4v) {
+  FISDF_TRY(device_guard(c));
+  StageTimer tm(c, FISDF_ST_X4);
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  const cplx* phase;
+  FISDF_TRY(get_phase(c, kmesh, a, &phase));
+  const cplx* X = (const cplx*)Xv;
+  const long nn = (long)nip * nip;
+  Carver cv;
+  size_t o1 = cv.take(sizeof(cplx) * nk * nn);
+  size_t o2 = cv.take(sizeof(cplx) * nk * nn);
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  cplx* X2k = (cplx*)((char*)base + o1);
+  cplx* X2s = (cplx*)((char*)base + o2);
+  // x2_k = X_k^* X_k^T  (:38)
+  FISDF_TRY(zgemm(c->stream, OP_R, OP_T, nip, nip, nao, ONE, X, nao, (long)nip * nao, X, nao,
+                  (long)nip * nao, ZERO, X2k, nip, nn, nk));
+  // x2_s = Phi x2_k  (:41), must be real (:43)
+  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nn, nk, ONE, phase, nk, 0, X2k, nn, 0, ZERO, X2s, nn,
+                  0, 1));
+  // x4_s = x2_s * x2_s (:45); records max|Im x2_s|
+  FISDF_TRY(csquare(c->stream, X2s, nk * nn, c->maximag + 0));
+  // x4_k = Phi^H x4_s (:46)
+  FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nk, nn, nk, ONE, phase, nk, 0, X2s, nn, 0, ZERO,
+                  (cplx*)x4v, nn, 0, 1));
+  return 0;
+}
+
+// ---- A3 ---------------------------------------------------------------------
+int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk, int ngrid,
+                  const void* Xv, int nip, int nao, const int kmesh[3], const double a[9],
+                  int q0, int q1, void* yTv) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(g0 >= 0 && nblk >= 0 && g0 + nblk <= ngrid, "build_y: block out of range");
+  StageTimer tm(c, FISDF_ST_Y);
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  FISDF_CHECK(0 <= q0 && q0 < q1 && q1 <= nk, "build_y: bad q range");
+  const cplx* phase;
+  FISDF_TRY(get_phase(c, kmesh, a, &phase));
+  const cplx* f = (const cplx*)fv;
+  const cplx* X = (const cplx*)Xv;
+  cplx* yT = (cplx*)yTv;
+  // sub-block so that the temporaries stay ~<= 2 GB
+  const long per_g = (long)nk * nip * sizeof(cplx);
+  int gb = (int)std::max(64L, std::min<long>(nblk, (1L << 30) / std::max(per_g, 1L)));
+  gb = std::min(gb, std::max(nblk, 1));
+  Carver cv;
+  size_t o1 = cv.take((size_t)per_g * gb);
+  size_t o2 = cv.take((size_t)per_g * gb);
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  cplx* FX = (cplx*)((char*)base + o1);
+  cplx* FS = (cplx*)((char*)base + o2);
+  for (int s0 = 0; s0 < nblk; s0 += gb) {
+    const int m = std::min(gb, nblk - s0);
+    const long nm = (long)nip * m;
+    // fx_k^T = X_k f_k^H  -> FX[k][I][g]   (:76, transposed layout)
+    FISDF_TRY(zgemm(c->stream, OP_N, OP_C, nip, m, nao, ONE, X, nao, (long)nip * nao,
+                    f + (long)s0 * nao, nao, f_kstride, ZERO, FX, m, nm, nk));
+    // fx_s = Phi fx_k  (:79), real (:81)
+    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nm, nk, ONE, phase, nk, 0, FX, nm, 0, ZERO, FS, nm,
+                    0, 1));
+    // y_s = fx_s^2 (:83)
+    FISDF_TRY(square_real(c->stream, FS, FX, (long)nk * nm, c->maximag + 1));
+    // y_k = Phi^T y_s (:84) for the shard's k rows, scattered into yT[k-q0][I][g0+s0+g] (:85)
+    FISDF_TRY(zgemm(c->stream, OP_T, OP_N, q1 - q0, m, nk, ONE, phase + q0, nk, 0, FX, nm, m,
+                    ZERO, yT + g0 + s0, (long)nip * ngrid, ngrid, nip));
+  }
+  return 0;
+}
+
+// ---- A4 ---------------------------------------------------------------------
+int fisdf_factor_x4(fisdf_ctx* c, const void* x4v, int q0, int q1, int nip, double tol_rel,
+                    int* h_ranks) {
+  FISDF_TRY(device_guard(c));
+  const int nk = q1 - q0;
+  FISDF_CHECK(q0 >= 0 && nk > 0 && nip > 0, "factor_x4: bad sizes");
+  x4v = (const cplx*)x4v + (long)q0 * nip * nip;
+  StageTimer tm(c, FISDF_ST_FACTOR);
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  FISDF_TRY(free_factors(c));
+  const int nb = c->f_nb;
+  const int nblk = (nip + nb - 1) / nb;
+  const long nn = (long)nip * nip;
+  FISDF_HIP(hipMalloc(&c->f_L, sizeof(cplx) * nk * nn));
+  FISDF_HIP(hipMalloc(&c->f_Lp, sizeof(cplx) * nk * nn));
+  FISDF_HIP(hipMalloc(&c->f_Linv, sizeof(cplx) * (size_t)nk * nblk * nb * nb));
+  FISDF_HIP(hipMalloc(&c->f_piv, sizeof(int) * (size_t)nk * nip));
+  c->f_q0 = q0;
+  c->f_nk = nk;
+  c->f_nip = nip;
+  Carver cv;
+  size_t oR = cv.take(sizeof(int) * nk);
+  size_t oD = cv.take(sizeof(double) * (size_t)nk * nip);
+  size_t oF = cv.take(sizeof(int) * nk);
+  size_t oW = cv.take(sizeof(double) * (size_t)nk * (1 + nip));
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  char* b = (char*)base;
+  FISDF_TRY(pchol(c->stream, (const cplx*)x4v, nip, nn, nip, nk, nip, tol_rel, 0.0, c->f_L,
+                  c->f_piv, (int*)(b + oR), (double*)(b + oD), (int*)(b + oF), (double*)(b + oW)));
+  c->f_rank.assign(nk, 0);
+  FISDF_HIP(hipMemcpyAsync(c->f_rank.data(), b + oR, sizeof(int) * nk, hipMemcpyDeviceToHost,
+                           c->stream));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  for (int q = 0; q < nk; ++q) {
+    const int r = c->f_rank[q];
+    if (h_ranks) h_ranks[q] = r;
+    if (r == 0) continue;
+    cplx* Lp = c->f_Lp + (long)q * nn;
+    FISDF_TRY(gather_lp(c->stream, c->f_L + (long)q * nn, nip, c->f_piv + (long)q * nip, r, r, Lp));
+    FISDF_TRY(trinv_blocks(c->stream, Lp, r, nb, c->f_Linv + (long)q * nblk * nb * nb));
+  }
+  return 0;
+}
+
+// ---- A4 + A5 ------------------------------------------------------------------
+int fisdf_fit_coulomb(fisdf_ctx* c, int q0, int q1, const void* yTv, int nip, const int mesh[3],
+                      const int kmesh[3], const double a[9], void* Wqv) {
+  FISDF_TRY(device_guard(c));
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  FISDF_CHECK(c->f_q0 == q0 && c->f_nk == q1 - q0 && c->f_nip == nip,
+              "fit_coulomb: call fisdf_factor_x4 on the same q range first");
+  FISDF_CHECK(0 <= q0 && q0 <= q1 && q1 <= nk, "fit_coulomb: bad q range");
+  const long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
+  const long nn = (long)nip * nip;
+  const int nb = c->f_nb;
+  const int nblk = (nip + nb - 1) / nb;
+  CellGeom g;
+  lattice(a, g);
+  const double vol = cell_volume(a);
+  const cplx* yT = (const cplx*)yTv;
+  cplx* Wq = (cplx*)Wqv;
+  int rmax = 0;
+  for (int q = q0; q < q1; ++q) rmax = std::max(rmax, c->f_rank[q - q0]);
+  const int ks = pick_ksplit(rmax, rmax, (int)ngrid);
+  Carver cv;
+  size_t oY = cv.take(sizeof(cplx) * rmax * ngrid);
+  size_t oU = cv.take(sizeof(cplx) * rmax * ngrid);
+  size_t oWt = cv.take(sizeof(double) * ngrid);
+  size_t oG = cv.take(sizeof(cplx) * nn);
+  size_t oT = cv.take(sizeof(cplx) * nn);
+  size_t oS = cv.take(sizeof(cplx) * nn);
+  size_t oK = cv.take(sizeof(cplx) * (size_t)ks * rmax * rmax);
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  char* b = (char*)base;
+  cplx* Yh = (cplx*)(b + oY);
+  cplx* U = (cplx*)(b + oU);
+  double* wt = (double*)(b + oWt);
+  cplx* G = (cplx*)(b + oG);
+  cplx* T = (cplx*)(b + oT);
+  cplx* S = (cplx*)(b + oS);
+  cplx* kw = (cplx*)(b + oK);
+  for (int q = q0; q < q1; ++q) {
+    const int lq = q - q0;
+    const int r = c->f_rank[lq];
+    cplx* Wout = Wq + (long)lq * nn;
+    if (r == 0) {
+      FISDF_HIP(hipMemsetAsync(Wout, 0, sizeof(cplx) * nn, c->stream));
+      continue;
+    }
+    const int* piv = c->f_piv + (long)lq * nip;
+    const cplx* Lp = c->f_Lp + (long)lq * nn;
+    const cplx* Linv = c->f_Linv + (long)lq * nblk * nb * nb;
+    double kq[3], kd[3];
+    kpoint(kmesh, g, q, kq);
+    for (int i = 0; i < 3; ++i) kd[i] = g.a[i][0] * kq[0] + g.a[i][1] * kq[1] + g.a[i][2] * kq[2];
+    {
+      StageTimer tm(c, FISDF_ST_FFT);
+      // sqrt(coulG(k_q+G) vol/N^2)  (:114-115 and the Parseval 1/N of :118)
+      FISDF_TRY(coulg_weight(c->stream, mesh, g, kq, vol / ((double)ngrid * ngrid), 1, wt));
+      // Yh = FFT(y_q[:, piv] * f_q) * w   (:99, :113; rows in pivot order)
+      FISDF_TRY(fft3d(c->stream, yT + (long)lq * nip * ngrid, ngrid, piv, Yh, ngrid, r, mesh[0],
+                      mesh[1], mesh[2], kd, wt, nullptr));
+    }
+    {
+      StageTimer tm(c, FISDF_ST_TRSM);
+      // U = L^{-1} Yh   (fit, factored order; (x4_q)_PP = L L^H)
+      FISDF_TRY(trsm_blocked(c->stream, 1, Lp, r, Linv, nb, Yh, ngrid, U, ngrid, (int)ngrid));
+    }
+    {
+      StageTimer tm(c, FISDF_ST_HERK);
+      // G = U U^H  (:121 by Parseval)
+      FISDF_TRY(herk(c->stream, r, (int)ngrid, 1.0, U, ngrid, G, r, ks, kw));
+    }
+    {
+      StageTimer tm(c, FISDF_ST_SMALL);
+      // W_PP = L^{-H} G L^{-1}:  T = L^{-H} G ; S = L^{-H} T^H ; W_PP = S^H
+      FISDF_TRY(trsm_blocked(c->stream, 0, Lp, r, Linv, nb, G, r, T, r, r));
+      FISDF_TRY(conj_transpose(c->stream, T, r, G));
+      FISDF_TRY(trsm_blocked(c->stream, 0, Lp, r, Linv, nb, G, r, S, r, r));
+      FISDF_TRY(conj_transpose(c->stream, S, r, T));
+      FISDF_TRY(scatter_w(c->stream, T, r, piv, Wout, nip));
+    }
+  }
+  return 0;
+}
+
+// ---- A8 prep ------------------------------------------------------------------
+int fisdf_build_ws(fisdf_ctx* c, const void* Wqv, int q0, int q1, int nip, const int kmesh[3],
+                   const double a[9], void* Wsv) {
+  FISDF_TRY(device_guard(c));
+  StageTimer tm(c, FISDF_ST_WS);
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  FISDF_CHECK(0 <= q0 && q0 <= q1 && q1 <= nk, "build_ws: bad q range");
+  const cplx* phase;
+  FISDF_TRY(get_phase(c, kmesh, a, &phase));
+  const long nn = (long)nip * nip;
+  void* base;
+  FISDF_TRY(arena_get(c, sizeof(cplx) * nk * nn, &base));
+  cplx* tmp = (cplx*)base;
+  if (q1 == q0) {
+    FISDF_HIP(hipMemsetAsync(Wsv, 0, sizeof(cplx) * nk * nn, c->stream));
+    return 0;
+  }
+  // ws = Phi W (:205), real part * sqrt(nk) (:207)
+  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nn, q1 - q0, ONE, phase + q0, nk, 0,
+                  (const cplx*)Wqv, nn, 0, ZERO, tmp, nn, 0, 1));
+  FISDF_TRY(real_part(c->stream, tmp, std::sqrt((double)nk), (cplx*)Wsv, nk * nn, nullptr));
+  return 0;
+}
+
+// ---- A7 -----------------------------------------------------------------------
+int fisdf_get_j(fisdf_ctx* c, const void* Xv, const void* W0, const void* dmsv, int nset, int nk,
+                int nip, int nao, void* vjv) {
+  FISDF_TRY(device_guard(c));
+  StageTimer tm(c, FISDF_ST_J);
+  const cplx* X = (const cplx*)Xv;
+  const cplx* dms = (const cplx*)dmsv;
+  cplx* vj = (cplx*)vjv;
+  const long xs = (long)nip * nao, ds = (long)nao * nao;
+  Carver cv;
+  size_t oT = cv.take(sizeof(cplx) * nset * nk * xs);
+  size_t oR = cv.take(sizeof(cplx) * nset * nip);
+  size_t oV = cv.take(sizeof(cplx) * nset * nip);
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  cplx* T = (cplx*)((char*)base + oT);
+  cplx* rho = (cplx*)((char*)base + oR);
+  cplx* v = (cplx*)((char*)base + oV);
+  // T = X_k D_k
+  for (int x = 0; x < nset; ++x)
+    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nip, nao, nao, ONE, X, nao, xs, dms + (long)x * nk * ds,
+                    nao, ds, ZERO, T + (long)x * nk * xs, nao, xs, nk));
+  // rho_I = sum_k X_k[I,m] D_k[m,n] X_k*[I,n] / nk  (:155-156)
+  FISDF_TRY(rho_diag(c->stream, T, X, nset, nk, nip, nao, 1.0 / nk, rho));
+  // v = W0 rho  (:159)
+  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nip, 1, nip, ONE, (const cplx*)W0, nip, 0, rho, 1, nip,
+                  ZERO, v, 1, nip, nset));
+  // J_k = X_k^H diag(v) X_k  (:166)
+  FISDF_TRY(scale_rows(c->stream, X, v, nset, nk, nip, nao, T));
+  for (int x = 0; x < nset; ++x)
+    FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nao, nao, nip, ONE, X, nao, xs, T + (long)x * nk * xs,
+                    nao, xs, ZERO, vj + (long)x * nk * ds, nao, ds, nk));
+  return 0;
+}
+
+// ---- A8 -----------------------------------------------------------------------
+int fisdf_get_k(fisdf_ctx* c, const void* Xv, const void* Wsv, const void* dmsv, int nset, int nip,
+                int nao, const int kmesh[3], const double a[9], void* vkv) {
+  FISDF_TRY(device_guard(c));
+  StageTimer tm(c, FISDF_ST_K);
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  const cplx* phase;
+  FISDF_TRY(get_phase(c, kmesh, a, &phase));
+  const cplx* X = (const cplx*)Xv;
+  const cplx* Ws = (const cplx*)Wsv;
+  const cplx* dms = (const cplx*)dmsv;
+  cplx* vk = (cplx*)vkv;
+  const long xs = (long)nip * nao, ds = (long)nao * nao, nn = (long)nip * nip;
+  Carver cv;
+  size_t oT = cv.take(sizeof(cplx) * nk * xs);
+  size_t o1 = cv.take(sizeof(cplx) * nk * nn);
+  size_t o2 = cv.take(sizeof(cplx) * nk * nn);
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  cplx* T = (cplx*)((char*)base + oT);
+  cplx* B1 = (cplx*)((char*)base + o1);
+  cplx* B2 = (cplx*)((char*)base + o2);
+  for (int x = 0; x < nset; ++x) {
+    const cplx* dm = dms + (long)x * nk * ds;
+    // rho_k = X_k D_k X_k^H / nk  (:211-212)
+    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nip, nao, nao, ONE, X, nao, xs, dm, nao, ds, ZERO, T,
+                    nao, xs, nk));
+    FISDF_TRY(zgemm(c->stream, OP_N, OP_C, nip, nip, nao, cmk(1.0 / nk, 0), T, nao, xs, X, nao, xs,
+                    ZERO, B1, nip, nn, nk));
+    // rho_s = Phi rho_k (:215), real (:216)
+    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nn, nk, ONE, phase, nk, 0, B1, nn, 0, ZERO, B2, nn,
+                    0, 1));
+    FISDF_TRY(real_part(c->stream, B2, 1.0, B2, nk * nn, c->maximag + 2));
+    // V_s = W_s * rho_s^T (:219)
+    FISDF_TRY(ws_times_rhoT(c->stream, Ws, B2, nk, nip, B1));
+    // V_k = Phi^T V_s (:222)
+    FISDF_TRY(zgemm(c->stream, OP_T, OP_N, nk, nn, nk, ONE, phase, nk, 0, B1, nn, 0, ZERO, B2, nn,
+                    0, 1));
+    // K_k = X_k^H V_k X_k (:225)
+    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nip, nao, nip, ONE, B2, nip, nn, X, nao, xs, ZERO, T,
+                    nao, xs, nk));
+    FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nao, nao, nip, ONE, X, nao, xs, T, nao, xs, ZERO,
+                    vk + (long)x * nk * ds, nao, ds, nk));
+  }
+  return 0;
+}
+
+}  // extern "C"

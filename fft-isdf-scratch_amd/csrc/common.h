@@ -1,0 +1,76 @@
+// fisdf — MI355X-native FFT-ISDF kernels: shared device/host helpers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+namespace fisdf {
+
+typedef double2 cplx;  // interleaved complex128 (matches NumPy complex128)
+typedef __attribute__((ext_vector_type(4))) double f64x4;
+
+// ---- error plumbing (C-ABI returns 0 / negative code, message via fisdf_last_error)
+void set_error(const std::string& msg);
+
+#define FISDF_HIP(call)                                                              \
+  do {                                                                               \
+    hipError_t _e = (call);                                                          \
+    if (_e != hipSuccess) {                                                          \
+      ::fisdf::set_error(std::string("HIP error '") + hipGetErrorString(_e) +        \
+                         "' at " __FILE__ ":" + std::to_string(__LINE__) + " in " #call); \
+      return -2;                                                                     \
+    }                                                                                \
+  } while (0)
+
+#define FISDF_CHECK(cond, msg)                                                       \
+  do {                                                                               \
+    if (!(cond)) {                                                                   \
+      ::fisdf::set_error(std::string("fisdf: ") + (msg) + " [" #cond "] at " __FILE__ ":" + \
+                         std::to_string(__LINE__));                                  \
+      return -1;                                                                     \
+    }                                                                                \
+  } while (0)
+
+#define FISDF_TRY(call)        \
+  do {                         \
+    int _r = (call);           \
+    if (_r != 0) return _r;    \
+  } while (0)
+
+// ---- complex helpers (device + host)
+__host__ __device__ inline cplx cmk(double r, double i) { cplx c; c.x = r; c.y = i; return c; }
+__host__ __device__ inline cplx cadd(cplx a, cplx b) { return cmk(a.x + b.x, a.y + b.y); }
+__host__ __device__ inline cplx csub(cplx a, cplx b) { return cmk(a.x - b.x, a.y - b.y); }
+__host__ __device__ inline cplx cmul(cplx a, cplx b) { return cmk(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+__host__ __device__ inline cplx cconj(cplx a) { return cmk(a.x, -a.y); }
+__host__ __device__ inline cplx cscale(cplx a, double s) { return cmk(a.x * s, a.y * s); }
+
+// ---- GEMM op codes: bit0 = transpose, bit1 = conjugate
+enum Op { OP_N = 0, OP_T = 1, OP_R = 2 /*conj only*/, OP_C = 3 /*conj-transpose*/ };
+
+// ---- kernels (launchers return 0 or negative; all asynchronous on `stream`)
+// C[b] = alpha * op(A[b]) * op(B[b]) + beta * C[b]; lda/ldb/ldc in complex elements,
+// strides sA/sB/sC per batch in complex elements. ksplit>1 uses `work` (ksplit*M*N cplx).
+int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha,
+          const cplx* A, long lda, long sA, const cplx* B, long ldb, long sB, cplx beta,
+          cplx* C, long ldc, long sC, int batch, int ksplit = 1, cplx* work = nullptr);
+
+// C = alpha A A^H (Hermitian rank-K update; lower tiles computed, upper mirrored)
+int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cplx* C, long ldc,
+         int ksplit = 1, cplx* work = nullptr);
+
+// batched pivoted Cholesky of Hermitian PSD matrices (fftisdf.py:381-382, A4 factorisation)
+int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int rmax,
+          double tol_rel, double tol_abs, cplx* L /*batch, n, rmax*/, int* piv /*batch, rmax*/,
+          int* rank /*batch, device*/, double* d /*batch,n*/, int* flags /*batch*/,
+          double* work /*batch*(1+rmax)*/);
+
+// 3-D FFT (unnormalised forward, numpy.fft.fftn sign) over `rows` rows of length n0*n1*n2.
+// in-row gather `rowidx` (may be null), pre-multiply by exp(-i (f.kd)) where f are the
+// fftfreq fractions (if kd != null), post-multiply by weight[G] (if weight != null).
+int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* out, long out_ld,
+          int rows, int n0, int n1, int n2, const double* kd /*3 or null*/,
+          const double* weight /*ngrid or null*/, cplx* work);
+
+}  // namespace fisdf

@@ -1,0 +1,283 @@
+// Batched 3-D complex FFT over the plane-wave mesh (forward, unnormalised, numpy sign).
+//
+// Replaces pbctools.fft(z_q * fq, mesh) of fftisdf.py:113 (and the fq = exp(-i k_q.r)
+// of :99, the coulG weight of :114-115).  Only the FORWARD transform is needed: the
+// inverse FFT + zeta z^H of :118-121 is folded into a Coulomb-weighted HERK by
+// Parseval, so `weight` carries sqrt(coulG(k_q+G) * vol/ngrid^2).
+//
+// One kernel per axis.  A workgroup stages a tile of TL lines x n points
+// (n = mesh[axis] <= 64) in LDS with coalesced loads (the TL lines are the
+// contiguous inner index for the strided axes), runs a mixed-radix Stockham FFT
+// (radix 4/2/3/5/7/11/13, twiddles from an n-th-root table in LDS) ping-ponging
+// between two LDS buffers, and writes the tile back.  The first pass (axis 2)
+// fuses the row gather (interpolation-point pivots) and the exp(-i k.r) phase,
+// the last pass (axis 0) fuses the Coulomb weight.
+#include "common.h"
+
+#include <map>
+#include <mutex>
+#include <vector>
+#include <cmath>
+
+namespace fisdf {
+
+namespace {
+
+constexpr int MAXN = 64;
+constexpr int MAXST = 8;
+
+struct Stages {
+  int nst;
+  int radix[MAXST];
+};
+
+template <int R>
+__device__ __forceinline__ void dft_small(cplx* v, const cplx* __restrict__ tw, int n) {
+  // out[k] = sum_r v[r] * exp(-2 pi i r k / R);  exp(-2 pi i x / R) = tw[x * n / R]
+  if constexpr (R == 2) {
+    cplx a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+  } else if constexpr (R == 4) {
+    cplx a0 = cadd(v[0], v[2]), a1 = csub(v[0], v[2]);
+    cplx b0 = cadd(v[1], v[3]), b1 = csub(v[1], v[3]);
+    // b1 * (-i)
+    cplx b1m = cmk(b1.y, -b1.x);
+    v[0] = cadd(a0, b0);
+    v[2] = csub(a0, b0);
+    v[1] = cadd(a1, b1m);
+    v[3] = csub(a1, b1m);
+  } else {
+    cplx o[R];
+    const int step = n / R;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      cplx acc = v[0];
+#pragma unroll
+      for (int r = 1; r < R; ++r) acc = cadd(acc, cmul(v[r], tw[((r * k) % R) * step]));
+      o[k] = acc;
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) v[k] = o[k];
+  }
+}
+
+template <int R>
+__device__ __forceinline__ void stockham_stage(const cplx* __restrict__ src, cplx* __restrict__ dst,
+                                               const cplx* __restrict__ tw, int n, int Ns, int TL,
+                                               int tid, int nthr) {
+  const int nb = n / R;
+  const int total = nb * TL;
+  const int twstep = n / (Ns * R);
+  for (int bf = tid; bf < total; bf += nthr) {
+    const int l = bf % TL, j = bf / TL;
+    cplx v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = src[(j + r * nb) * TL + l];
+    const int k = j % Ns;
+    if (Ns > 1) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[(k * r * twstep) % n]);
+    }
+    dft_small<R>(v, tw, n);
+    const int idx = (j / Ns) * Ns * R + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) dst[(idx + r * Ns) * TL + l] = v[r];
+  }
+}
+
+__device__ __forceinline__ double fftfreq(int i, int n) {
+  return (double)(i < (n + 1) / 2 ? i : i - n) / (double)n;
+}
+
+// axis pass. contiguous=1: lines are `n` contiguous elements (axis 2); tiles = TL consecutive lines.
+// contiguous=0: element p of line (o, ii) at o*n*inner + p*inner + ii; tile = TL consecutive ii.
+__global__ __launch_bounds__(256) void fft_axis_kernel(
+    const cplx* __restrict__ in, long in_ld, const int* __restrict__ rowidx, cplx* out, long out_ld,
+    int rows, int n, int inner, int outer, int TL, int contiguous, Stages st,
+    const cplx* __restrict__ twg, int n0, int n1, int n2, double kd0, double kd1, double kd2,
+    int use_phase, const double* __restrict__ weight) {
+  extern __shared__ cplx smem[];
+  cplx* tw = smem;                 // n roots
+  cplx* buf0 = smem + MAXN;        // TL*n
+  cplx* buf1 = buf0 + TL * n;      // TL*n
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  for (int t = tid; t < n; t += nthr) tw[t] = twg[t];
+
+  // tile -> (row, line block)
+  long tile = blockIdx.x;
+  int tiles_per_row = contiguous ? (outer + TL - 1) / TL : outer * (inner / TL);
+  int row = (int)(tile / tiles_per_row);
+  int trow = (int)(tile % tiles_per_row);
+  if (row >= rows) return;
+  const cplx* src = in + (long)(rowidx ? rowidx[row] : row) * in_ld;
+  cplx* dstp = out + (long)row * out_ld;
+  const int ngrid = n0 * n1 * n2;
+
+  long base;       // element offset of (line 0, p 0) of the tile inside the row
+  int nlines = TL;
+  if (contiguous) {
+    int o0 = trow * TL;
+    nlines = min(TL, outer - o0);
+    base = (long)o0 * n;
+  } else {
+    int o = trow / (inner / TL), ib = trow % (inner / TL);
+    base = (long)o * n * inner + (long)ib * TL;
+  }
+  auto gidx = [&](int l, int p) -> long {
+    return contiguous ? base + (long)l * n + p : base + (long)p * inner + l;
+  };
+
+  const int tot = TL * n;
+  __syncthreads();
+  for (int e = tid; e < tot; e += nthr) {
+    int l, p;
+    if (contiguous) { l = e / n; p = e % n; } else { l = e % TL; p = e / TL; }
+    cplx v = cmk(0, 0);
+    if (l < nlines) {
+      long g = gidx(l, p);
+      v = src[g];
+      if (use_phase) {
+        int i2 = (int)(g % n2);
+        int i1 = (int)((g / n2) % n1);
+        int i0 = (int)(g / ((long)n1 * n2));
+        double th = -(fftfreq(i0, n0) * kd0 + fftfreq(i1, n1) * kd1 + fftfreq(i2, n2) * kd2);
+        double s, c;
+        sincos(th, &s, &c);
+        v = cmul(v, cmk(c, s));
+      }
+    }
+    buf0[p * TL + l] = v;
+  }
+  __syncthreads();
+  cplx* a = buf0;
+  cplx* b = buf1;
+  int Ns = 1;
+  for (int s = 0; s < st.nst; ++s) {
+    int R = st.radix[s];
+    switch (R) {
+      case 2: stockham_stage<2>(a, b, tw, n, Ns, TL, tid, nthr); break;
+      case 3: stockham_stage<3>(a, b, tw, n, Ns, TL, tid, nthr); break;
+      case 4: stockham_stage<4>(a, b, tw, n, Ns, TL, tid, nthr); break;
+      case 5: stockham_stage<5>(a, b, tw, n, Ns, TL, tid, nthr); break;
+      case 7: stockham_stage<7>(a, b, tw, n, Ns, TL, tid, nthr); break;
+      case 11: stockham_stage<11>(a, b, tw, n, Ns, TL, tid, nthr); break;
+      case 13: stockham_stage<13>(a, b, tw, n, Ns, TL, tid, nthr); break;
+    }
+    Ns *= R;
+    __syncthreads();
+    cplx* t = a; a = b; b = t;
+  }
+  for (int e = tid; e < tot; e += nthr) {
+    int l, p;
+    if (contiguous) { l = e / n; p = e % n; } else { l = e % TL; p = e / TL; }
+    if (l < nlines) {
+      long g = gidx(l, p);
+      cplx v = a[p * TL + l];
+      if (weight) v = cscale(v, weight[g % ngrid]);
+      dstp[g] = v;
+    }
+  }
+}
+
+bool factorize(int n, Stages& st) {
+  st.nst = 0;
+  const int rs[] = {4, 2, 3, 5, 7, 11, 13};
+  for (int r : rs)
+    while (n % r == 0) {
+      if (st.nst >= MAXST) return false;
+      st.radix[st.nst++] = r;
+      n /= r;
+    }
+  return n == 1;
+}
+
+struct TwTable {
+  cplx* dev = nullptr;
+};
+std::mutex g_tw_mu;
+std::map<std::pair<int, int>, TwTable> g_tw;  // (device, n) -> roots
+
+int get_twiddles(int n, const cplx** out) {
+  int dev = 0;
+  FISDF_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_tw_mu);
+  auto key = std::make_pair(dev, n);
+  auto it = g_tw.find(key);
+  if (it == g_tw.end()) {
+    std::vector<cplx> h(n);
+    for (int t = 0; t < n; ++t) {
+      // exp(-2 pi i t / n), exact for the quarter points
+      long double ang = -2.0L * 3.14159265358979323846264338327950288L * t / n;
+      h[t] = cmk((double)cosl(ang), (double)sinl(ang));
+      if ((4 * t) % n == 0) {
+        int q = (4 * t) / n;
+        const double re[4] = {1, 0, -1, 0}, im[4] = {0, -1, 0, 1};
+        h[t] = cmk(re[q], im[q]);
+      }
+    }
+    TwTable tt;
+    FISDF_HIP(hipMalloc(&tt.dev, sizeof(cplx) * n));
+    FISDF_HIP(hipMemcpy(tt.dev, h.data(), sizeof(cplx) * n, hipMemcpyHostToDevice));
+    it = g_tw.emplace(key, tt).first;
+  }
+  *out = it->second.dev;
+  return 0;
+}
+
+int largest_divisor_le(int x, int cap) {
+  for (int d = std::min(x, cap); d >= 1; --d)
+    if (x % d == 0) return d;
+  return 1;
+}
+
+int axis_pass(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* out, long out_ld,
+              int rows, int axis, int n0, int n1, int n2, const double* kd, const double* weight) {
+  const int dims[3] = {n0, n1, n2};
+  const int n = dims[axis];
+  Stages st;
+  FISDF_CHECK(n >= 1 && n <= MAXN, "fft: mesh dimension must be in [1, 64]");
+  FISDF_CHECK(factorize(n, st), "fft: mesh dimension must factor into 2,3,5,7,11,13");
+  const cplx* tw = nullptr;
+  FISDF_TRY(get_twiddles(n, &tw));
+  int inner = 1, outer = 1;
+  for (int a = axis + 1; a < 3; ++a) inner *= dims[a];
+  for (int a = 0; a < axis; ++a) outer *= dims[a];
+  int contiguous = (axis == 2);
+  int TL;
+  long tiles;
+  if (contiguous) {
+    TL = std::max(1, std::min(64, 2048 / n));
+    tiles = (long)rows * ((outer + TL - 1) / TL);
+  } else {
+    TL = largest_divisor_le(inner, 64);
+    if (TL < 16 && inner > 64) TL = largest_divisor_le(inner, 128);  // keep tiles wide
+    FISDF_CHECK(TL <= 128, "fft: tile too wide");
+    tiles = (long)rows * outer * (inner / TL);
+  }
+  FISDF_CHECK(tiles < (1L << 31), "fft: too many tiles");
+  size_t lds = sizeof(cplx) * (MAXN + 2 * (size_t)TL * n);
+  FISDF_CHECK(lds <= 160 * 1024, "fft: LDS tile too large");
+  double k0 = 0, k1 = 0, k2 = 0;
+  int use_phase = kd != nullptr;
+  if (kd) { k0 = kd[0]; k1 = kd[1]; k2 = kd[2]; }
+  hipLaunchKernelGGL(fft_axis_kernel, dim3((unsigned)tiles), dim3(256), lds, s, in, in_ld, rowidx,
+                     out, out_ld, rows, n, inner, outer, TL, contiguous, st, tw, n0, n1, n2, k0, k1,
+                     k2, use_phase, weight);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace
+
+int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* out, long out_ld,
+          int rows, int n0, int n1, int n2, const double* kd, const double* weight, cplx* /*work*/) {
+  if (rows == 0) return 0;
+  FISDF_CHECK(in != out || rowidx == nullptr, "fft: in-place pass cannot gather rows");
+  FISDF_TRY(axis_pass(s, in, in_ld, rowidx, out, out_ld, rows, 2, n0, n1, n2, kd, nullptr));
+  FISDF_TRY(axis_pass(s, out, out_ld, nullptr, out, out_ld, rows, 1, n0, n1, n2, nullptr, nullptr));
+  FISDF_TRY(axis_pass(s, out, out_ld, nullptr, out, out_ld, rows, 0, n0, n1, n2, nullptr, weight));
+  return 0;
+}
+
+}  // namespace fisdf

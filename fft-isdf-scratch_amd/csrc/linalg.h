@@ -1,0 +1,32 @@
+#pragma once
+#include "common.h"
+
+namespace fisdf {
+
+struct CellGeom {
+  double a[3][3];  // lattice vectors (rows), bohr
+  double b[3][3];  // reciprocal vectors (rows), 2*pi*inv(a)^T
+};
+
+int gather_lp(hipStream_t s, const cplx* L, int rmax, const int* piv, int r, int rpad, cplx* Lp);
+int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int nb, cplx* Linv);
+int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, int r, const cplx* Linv, int nb,
+                 cplx* B, long ldb, cplx* X, long ldx, int ncol);
+int scatter_w(hipStream_t s, const cplx* Wpp, int r, const int* piv, cplx* W, int nip);
+int conj_transpose(hipStream_t s, const cplx* A, int n, cplx* B);
+int coulg_weight(hipStream_t s, const int mesh[3], const CellGeom& g, const double k[3],
+                 double scale, int take_sqrt, double* w);
+int square_real(hipStream_t s, const cplx* in, cplx* out, long n, unsigned long long* maximag);
+int real_part(hipStream_t s, const cplx* in, double scale, cplx* out, long n,
+              unsigned long long* maximag);
+int csquare(hipStream_t s, cplx* a, long n, unsigned long long* maximag);
+int ws_times_rhoT(hipStream_t s, const cplx* ws, const cplx* rho, int nimg, int nip, cplx* V);
+int rho_diag(hipStream_t s, const cplx* T, const cplx* X, int nset, int nk, int nip, int nao,
+             double scale, cplx* rho);
+int scale_rows(hipStream_t s, const cplx* X, const cplx* v, int nset, int nk, int nip, int nao,
+               cplx* Xv);
+int gather_points(hipStream_t s, const cplx* x0, int nk, int ng0, int nao, const int* perm,
+                  int nip, cplx* X);
+int square_scale(hipStream_t s, const cplx* in, double sc, cplx* out, long n);
+
+}  // namespace fisdf

@@ -1,0 +1,372 @@
+// Small device kernels around the GEMM / FFT / Cholesky engines:
+// pivot-order factor gather, diagonal-block triangular inverses, blocked TRSM driver,
+// Coulomb weights, the y-build square, scatter/gather and J/K element-wise steps.
+#include "common.h"
+#include "linalg.h"
+
+#include <cmath>
+
+namespace fisdf {
+
+namespace {
+
+// Lp[s][t] = L[piv[s]][t] (t <= s < r), zero above the diagonal; identity beyond rank.
+__global__ void gather_lp_kernel(const cplx* __restrict__ L, int rmax, const int* __restrict__ piv,
+                                 int r, int rpad, cplx* __restrict__ Lp) {
+  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= (long)rpad * rpad) return;
+  int s = (int)(e / rpad), t = (int)(e % rpad);
+  cplx v = cmk(0, 0);
+  if (s < r && t < r) {
+    if (t <= s) v = L[(long)piv[s] * rmax + t];
+  } else if (s == t) {
+    v = cmk(1, 0);
+  }
+  Lp[e] = v;
+}
+
+// inverse of each nb x nb lower-triangular diagonal block of Lp (r x r, ld = r)
+__global__ __launch_bounds__(64) void trinv_blocks_kernel(const cplx* __restrict__ Lp, int r,
+                                                          int nb, cplx* __restrict__ Linv) {
+  __shared__ cplx Ls[64][65];
+  __shared__ cplx Xs[64][65];
+  const int blk = blockIdx.x;
+  const int b0 = blk * nb;
+  const int m = min(nb, r - b0);
+  const int j = threadIdx.x;
+  for (int i = 0; i < m; ++i)
+    if (j < m) Ls[i][j] = Lp[(long)(b0 + i) * r + b0 + j];
+  __syncthreads();
+  if (j < m) {
+    for (int i = 0; i < m; ++i) {
+      cplx s = cmk(i == j ? 1.0 : 0.0, 0.0);
+      for (int t = j; t < i; ++t) s = csub(s, cmul(Ls[i][t], Xs[t][j]));
+      // divide by L_ii
+      cplx d = Ls[i][i];
+      double den = d.x * d.x + d.y * d.y;
+      Xs[i][j] = i < j ? cmk(0, 0) : cmk((s.x * d.x + s.y * d.y) / den, (s.y * d.x - s.x * d.y) / den);
+    }
+  }
+  __syncthreads();
+  cplx* out = Linv + (long)blk * nb * nb;
+  for (int i = 0; i < nb; ++i)
+    if (j < nb) out[i * nb + j] = (i < m && j < m) ? Xs[i][j] : cmk(i == j ? 1.0 : 0.0, 0.0);
+}
+
+// W[piv[s]][piv[t]] = Wpp[s][t]   (W zeroed beforehand)
+__global__ void scatter_w_kernel(const cplx* __restrict__ Wpp, int r, const int* __restrict__ piv,
+                                 cplx* __restrict__ W, int nip) {
+  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= (long)r * r) return;
+  int s = (int)(e / r), t = (int)(e % r);
+  W[(long)piv[s] * nip + piv[t]] = Wpp[e];
+}
+
+__global__ void conj_transpose_kernel(const cplx* __restrict__ A, int n, cplx* __restrict__ B) {
+  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= (long)n * n) return;
+  int i = (int)(e / n), j = (int)(e % n);
+  B[(long)j * n + i] = cconj(A[e]);
+}
+
+// sqrt(coulG(k+G) * scale); PySCF get_coulG (exxdiv=None, wrap_around=True) restated
+__global__ void coulg_weight_kernel(int n0, int n1, int n2, CellGeom g, double kx, double ky,
+                                    double kz, double scale, int take_sqrt,
+                                    double* __restrict__ w) {
+  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  long ngrid = (long)n0 * n1 * n2;
+  if (e >= ngrid) return;
+  int i2 = (int)(e % n2), i1 = (int)((e / n2) % n1), i0 = (int)(e / ((long)n1 * n2));
+  int ns[3] = {n0, n1, n2};
+  int is[3] = {i0, i1, i2};
+  double G[3] = {0, 0, 0};
+  for (int a = 0; a < 3; ++a) {
+    int m = is[a] < (ns[a] + 1) / 2 ? is[a] : is[a] - ns[a];
+    for (int c = 0; c < 3; ++c) G[c] += m * g.b[a][c];
+  }
+  double k[3] = {kx, ky, kz};
+  bool nonzero_k = fabs(kx) + fabs(ky) + fabs(kz) > 1e-9;
+  double kG[3];
+  for (int c = 0; c < 3; ++c) kG[c] = nonzero_k ? k[c] + G[c] : G[c];
+  bool boundary = false;
+  if (nonzero_k) {
+    const double twopi = 6.283185307179586;
+    double red[3];
+    int edge[3];
+    for (int a = 0; a < 3; ++a) {
+      double h = (double)(ns[a] / 2) + 0.5;
+      double r = (kG[0] * g.a[a][0] + kG[1] * g.a[a][1] + kG[2] * g.a[a][2]) / (twopi * h);
+      r = rint(r * 1e9) / 1e9;
+      red[a] = r;
+      edge[a] = (int)r;  // truncation, as numpy astype(int)
+    }
+    for (int a = 0; a < 3; ++a) {
+      if (red[a] == 1.0 || red[a] == -1.0) boundary = true;
+      double h = (double)(ns[a] / 2) + 0.5;
+      for (int c = 0; c < 3; ++c) {
+        if (edge[a] == 1) kG[c] -= 2 * h * g.b[a][c];
+        if (edge[a] == -1) kG[c] += 2 * h * g.b[a][c];
+      }
+    }
+  }
+  double g2 = kG[0] * kG[0] + kG[1] * kG[1] + kG[2] * kG[2];
+  double cg = (g2 == 0.0 || boundary) ? 0.0 : 4.0 * 3.141592653589793 / g2;
+  double v = cg * scale;
+  w[e] = take_sqrt ? sqrt(v) : v;
+}
+
+// out[e] = (Re in[e])^2 + 0i ; records max |Im in| (bit pattern of a non-negative double)
+__global__ void square_real_kernel(const cplx* __restrict__ in, cplx* __restrict__ out, long n,
+                                   unsigned long long* __restrict__ maximag) {
+  double mi = 0.0;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    cplx v = in[e];
+    out[e] = cmk(v.x * v.x, 0.0);
+    mi = fmax(mi, fabs(v.y));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mi = fmax(mi, __shfl_xor(mi, o, 64));
+  if ((threadIdx.x & 63) == 0 && maximag) atomicMax(maximag, (unsigned long long)__double_as_longlong(mi));
+}
+
+// out[R,I,J] = scale * Re(in[R,I,J]) (+0i);  records max |Im|
+__global__ void real_part_kernel(const cplx* __restrict__ in, double scale, cplx* __restrict__ out,
+                                 long n, unsigned long long* __restrict__ maximag) {
+  double mi = 0.0;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    cplx v = in[e];
+    out[e] = cmk(v.x * scale, 0.0);
+    mi = fmax(mi, fabs(v.y));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mi = fmax(mi, __shfl_xor(mi, o, 64));
+  if ((threadIdx.x & 63) == 0 && maximag) atomicMax(maximag, (unsigned long long)__double_as_longlong(mi));
+}
+
+// V[R,I,J] = Ws[R,I,J] * Re(rho[R,J,I])   (fftisdf.py:219)
+__global__ void ws_times_rhoT_kernel(const cplx* __restrict__ ws, const cplx* __restrict__ rho,
+                                     int nimg, int nip, cplx* __restrict__ V) {
+  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  long tot = (long)nimg * nip * nip;
+  if (e >= tot) return;
+  long R = e / ((long)nip * nip);
+  int I = (int)((e / nip) % nip), J = (int)(e % nip);
+  double r = rho[R * nip * nip + (long)J * nip + I].x;
+  V[e] = cmk(ws[e].x * r, 0.0);
+}
+
+// rho[x,I] = scale * sum_k sum_n T[x,k,I,n] conj(X[k,I,n])
+__global__ void rho_diag_kernel(const cplx* __restrict__ T, const cplx* __restrict__ X, int nset,
+                                int nk, int nip, int nao, double scale, cplx* __restrict__ rho) {
+  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= (long)nset * nip) return;
+  int x = (int)(e / nip), I = (int)(e % nip);
+  double sr = 0, si = 0;
+  for (int k = 0; k < nk; ++k) {
+    const cplx* t = T + (((long)x * nk + k) * nip + I) * nao;
+    const cplx* xr = X + ((long)k * nip + I) * nao;
+    for (int n = 0; n < nao; ++n) {
+      cplx a = t[n], b = xr[n];
+      sr += a.x * b.x + a.y * b.y;
+      si += a.y * b.x - a.x * b.y;
+    }
+  }
+  rho[e] = cmk(sr * scale, si * scale);
+}
+
+// Xv[x,k,I,n] = v[x,I] * X[k,I,n]
+__global__ void scale_rows_kernel(const cplx* __restrict__ X, const cplx* __restrict__ v, int nset,
+                                  int nk, int nip, int nao, cplx* __restrict__ Xv) {
+  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  long per = (long)nk * nip * nao;
+  if (e >= (long)nset * per) return;
+  int x = (int)(e / per);
+  long r = e % per;
+  int I = (int)((r / nao) % nip);
+  Xv[e] = cmul(v[(long)x * nip + I], X[r]);
+}
+
+// X[k,I,:] = x0[k, perm[I], :]
+__global__ void gather_points_kernel(const cplx* __restrict__ x0, int nk, int ng0, int nao,
+                                     const int* __restrict__ perm, int nip, cplx* __restrict__ X) {
+  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= (long)nk * nip * nao) return;
+  int m = (int)(e % nao);
+  int I = (int)((e / nao) % nip);
+  int k = (int)(e / ((long)nao * nip));
+  X[e] = x0[((long)k * ng0 + perm[I]) * nao + m];
+}
+
+// x4[i,j] = Re(x2[i,j])^2 / nk  (fftisdf.py:379)  — stored as complex (+0i) for pchol
+__global__ void square_scale_kernel(const cplx* __restrict__ in, double s, cplx* __restrict__ out,
+                                    long n) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    double r = in[e].x;
+    out[e] = cmk(r * r * s, 0.0);
+  }
+}
+
+// y_s element-wise square in place, complex: x2_s -> x4_s (complex square, fftisdf.py:45)
+__global__ void csquare_kernel(cplx* __restrict__ a, long n, unsigned long long* __restrict__ maximag) {
+  double mi = 0.0;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    cplx v = a[e];
+    mi = fmax(mi, fabs(v.y));
+    a[e] = cmul(v, v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mi = fmax(mi, __shfl_xor(mi, o, 64));
+  if ((threadIdx.x & 63) == 0 && maximag) atomicMax(maximag, (unsigned long long)__double_as_longlong(mi));
+}
+
+inline int nblocks(long n, int bs = 256, long cap = 1L << 20) {
+  long b = (n + bs - 1) / bs;
+  return (int)std::max(1L, std::min(b, cap));
+}
+
+}  // namespace
+
+int gather_lp(hipStream_t s, const cplx* L, int rmax, const int* piv, int r, int rpad, cplx* Lp) {
+  long n = (long)rpad * rpad;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(gather_lp_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, L, rmax,
+                     piv, r, rpad, Lp);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int nb, cplx* Linv) {
+  FISDF_CHECK(nb >= 1 && nb <= 64, "trinv_blocks: nb must be <= 64");
+  int nblk = (r + nb - 1) / nb;
+  if (nblk == 0) return 0;
+  hipLaunchKernelGGL(trinv_blocks_kernel, dim3(nblk), dim3(64), 0, s, Lp, r, nb, Linv);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+// X = L^{-1} B  (lower=1) or X = L^{-H} B (lower=0, backward with L^H); B is overwritten.
+// L: r x r lower (ld = r); Linv: diagonal-block inverses; B, X: r x ncol (ld given).
+int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, int r, const cplx* Linv, int nb,
+                 cplx* B, long ldb, cplx* X, long ldx, int ncol) {
+  const cplx one = cmk(1, 0), mone = cmk(-1, 0), zero = cmk(0, 0);
+  int nblk = (r + nb - 1) / nb;
+  for (int bi = 0; bi < nblk; ++bi) {
+    int blk = lower ? bi : nblk - 1 - bi;
+    int b0 = blk * nb, b1 = std::min(r, b0 + nb), m = b1 - b0;
+    if (lower) {
+      if (b0 > 0)  // B_b -= L[b, :b] X[:b]
+        FISDF_TRY(zgemm(s, OP_N, OP_N, m, ncol, b0, mone, Lp + (long)b0 * r, r, 0, X, ldx, 0,
+                        one, B + (long)b0 * ldb, ldb, 0, 1));
+      FISDF_TRY(zgemm(s, OP_N, OP_N, m, ncol, m, one, Linv + (long)blk * nb * nb, nb, 0,
+                      B + (long)b0 * ldb, ldb, 0, zero, X + (long)b0 * ldx, ldx, 0, 1));
+    } else {
+      if (b1 < r)  // B_b -= (L^H)[b, >b] X[>b] = conj(L[>b, b])^T X[>b]
+        FISDF_TRY(zgemm(s, OP_C, OP_N, m, ncol, r - b1, mone, Lp + (long)b1 * r + b0, r, 0,
+                        X + (long)b1 * ldx, ldx, 0, one, B + (long)b0 * ldb, ldb, 0, 1));
+      FISDF_TRY(zgemm(s, OP_C, OP_N, m, ncol, m, one, Linv + (long)blk * nb * nb, nb, 0,
+                      B + (long)b0 * ldb, ldb, 0, zero, X + (long)b0 * ldx, ldx, 0, 1));
+    }
+  }
+  return 0;
+}
+
+int scatter_w(hipStream_t s, const cplx* Wpp, int r, const int* piv, cplx* W, int nip) {
+  FISDF_HIP(hipMemsetAsync(W, 0, sizeof(cplx) * (size_t)nip * nip, s));
+  long n = (long)r * r;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(scatter_w_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, Wpp, r,
+                     piv, W, nip);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int conj_transpose(hipStream_t s, const cplx* A, int n, cplx* B) {
+  long e = (long)n * n;
+  if (e == 0) return 0;
+  hipLaunchKernelGGL(conj_transpose_kernel, dim3(nblocks(e, 256, 1L << 30)), dim3(256), 0, s, A,
+                     n, B);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int coulg_weight(hipStream_t s, const int mesh[3], const CellGeom& g, const double k[3],
+                 double scale, int take_sqrt, double* w) {
+  long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
+  hipLaunchKernelGGL(coulg_weight_kernel, dim3(nblocks(ngrid, 256, 1L << 30)), dim3(256), 0, s,
+                     mesh[0], mesh[1], mesh[2], g, k[0], k[1], k[2], scale, take_sqrt, w);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int square_real(hipStream_t s, const cplx* in, cplx* out, long n, unsigned long long* maximag) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(square_real_kernel, dim3(nblocks(n, 256, 8192)), dim3(256), 0, s, in, out, n,
+                     maximag);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int real_part(hipStream_t s, const cplx* in, double scale, cplx* out, long n,
+              unsigned long long* maximag) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(real_part_kernel, dim3(nblocks(n, 256, 8192)), dim3(256), 0, s, in, scale,
+                     out, n, maximag);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int csquare(hipStream_t s, cplx* a, long n, unsigned long long* maximag) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(csquare_kernel, dim3(nblocks(n, 256, 8192)), dim3(256), 0, s, a, n, maximag);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int ws_times_rhoT(hipStream_t s, const cplx* ws, const cplx* rho, int nimg, int nip, cplx* V) {
+  long n = (long)nimg * nip * nip;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ws_times_rhoT_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, ws,
+                     rho, nimg, nip, V);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int rho_diag(hipStream_t s, const cplx* T, const cplx* X, int nset, int nk, int nip, int nao,
+             double scale, cplx* rho) {
+  long n = (long)nset * nip;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(rho_diag_kernel, dim3(nblocks(n, 64, 1L << 30)), dim3(64), 0, s, T, X, nset,
+                     nk, nip, nao, scale, rho);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int scale_rows(hipStream_t s, const cplx* X, const cplx* v, int nset, int nk, int nip, int nao,
+               cplx* Xv) {
+  long n = (long)nset * nk * nip * nao;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(scale_rows_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, X, v,
+                     nset, nk, nip, nao, Xv);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int gather_points(hipStream_t s, const cplx* x0, int nk, int ng0, int nao, const int* perm,
+                  int nip, cplx* X) {
+  long n = (long)nk * nip * nao;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(gather_points_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, x0,
+                     nk, ng0, nao, perm, nip, X);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int square_scale(hipStream_t s, const cplx* in, double sc, cplx* out, long n) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(square_scale_kernel, dim3(nblocks(n, 256, 8192)), dim3(256), 0, s, in, sc,
+                     out, n);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace fisdf

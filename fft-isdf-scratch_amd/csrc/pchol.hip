@@ -1,0 +1,190 @@
+// Batched greedy (full-pivot) Cholesky of Hermitian PSD matrices.
+//
+// Serves two call sites of the reference:
+//  * interpolation-point selection: LAPACK dpstrf on the real parent-grid Gram x4
+//    (fftisdf.py:381-384 via pyscf.lib.scipy_helper.pivoted_cholesky); only the first
+//    nip = min(nao*c0, rank) pivots are produced, rank is detected by the same
+//    relative tolerance LAPACK uses (tol <= 0 -> n*eps*max(diag)).
+//  * the per-q factorisation of x4_q that replaces zgelsy's rank-revealing QRCP
+//    (fftisdf.py:108): rank cut at tol_rel * max(diag) (SURVEY.md A3 — applied in
+//    factored order downstream, never as an explicit inverse).
+//
+// Left-looking, one pivot per step: step j computes column j of L for every row
+// (one wave per row, dot product over the j previous columns with a wave reduction),
+// updates the residual diagonal d, then a per-matrix arg-max picks pivot j+1
+// (first index on ties, as LAPACK's MAXLOC).  Chosen rows are marked d = -1.
+#include "common.h"
+
+namespace fisdf {
+
+namespace {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// d <- Re(diag A); choose pivot 0.
+__global__ void pchol_init(const cplx* __restrict__ A, long lda, long sA, int n, int rmax,
+                           double tol_rel, double tol_abs, int* __restrict__ piv,
+                           double* __restrict__ pval, int* __restrict__ rank,
+                           double* __restrict__ d, int* __restrict__ flags,
+                           double* __restrict__ dmax0) {
+  const int b = blockIdx.x;
+  A += (long)b * sA;
+  d += (long)b * n;
+  __shared__ double sv[1024];
+  __shared__ int si[1024];
+  double best = -1.0;
+  int bi = 0x7fffffff;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    double v = A[(long)i * lda + i].x;
+    d[i] = v;
+    if (v > best || (v == best && i < bi)) { best = v; bi = i; }
+  }
+  sv[threadIdx.x] = best;
+  si[threadIdx.x] = bi;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      double o = sv[threadIdx.x + s];
+      int oi = si[threadIdx.x + s];
+      if (o > sv[threadIdx.x] || (o == sv[threadIdx.x] && oi < si[threadIdx.x])) {
+        sv[threadIdx.x] = o;
+        si[threadIdx.x] = oi;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double m = sv[0];
+    double tol = tol_rel > 0 ? tol_rel * m : (double)n * 2.220446049250313e-16 * m;
+    if (tol_abs > tol) tol = tol_abs;
+    dmax0[b] = tol;  // store the absolute stopping threshold
+    if (!(m > tol) || rmax <= 0) {
+      flags[b] = 1;
+      rank[b] = 0;
+    } else {
+      flags[b] = 0;
+      rank[b] = 0;
+      piv[(long)b * rmax] = si[0];
+      pval[(long)b * rmax] = m;
+    }
+  }
+}
+
+// column j of L for all rows; one wave per row
+__global__ __launch_bounds__(256) void pchol_step(const cplx* __restrict__ A, long lda, long sA,
+                                                  int n, int rmax, int j,
+                                                  const int* __restrict__ piv,
+                                                  const double* __restrict__ pval,
+                                                  cplx* __restrict__ L, double* __restrict__ d,
+                                                  const int* __restrict__ flags) {
+  const int b = blockIdx.y;
+  if (flags[b]) return;
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (i >= n) return;
+  A += (long)b * sA;
+  L += (long)b * n * rmax;
+  d += (long)b * n;
+  const int p = piv[(long)b * rmax + j];
+  const double dp = pval[(long)b * rmax + j];
+  const double di = d[i];
+  if (di <= -1e299 && i != p) {  // already a pivot row
+    if (lane == 0) L[(long)i * rmax + j] = cmk(0, 0);
+    return;
+  }
+  // s = sum_{t<j} L[i,t] * conj(L[p,t])
+  double sr = 0, si = 0;
+  const cplx* Li = L + (long)i * rmax;
+  const cplx* Lp = L + (long)p * rmax;
+  for (int t = lane; t < j; t += 64) {
+    cplx a = Li[t], c = Lp[t];
+    sr += a.x * c.x + a.y * c.y;
+    si += a.y * c.x - a.x * c.y;
+  }
+  sr = wave_sum(sr);
+  si = wave_sum(si);
+  if (lane == 0) {
+    const double sq = sqrt(dp);
+    if (i == p) {
+      L[(long)i * rmax + j] = cmk(sq, 0.0);
+      d[i] = -1e300;
+    } else {
+      cplx aip = A[(long)i * lda + p];
+      cplx l = cmk((aip.x - sr) / sq, (aip.y - si) / sq);
+      L[(long)i * rmax + j] = l;
+      d[i] = di - (l.x * l.x + l.y * l.y);
+    }
+  }
+}
+
+// arg-max of the residual diagonal -> pivot j+1, or stop
+__global__ void pchol_pick(int n, int rmax, int j, int* __restrict__ piv, double* __restrict__ pval,
+                           int* __restrict__ rank, const double* __restrict__ d,
+                           int* __restrict__ flags, const double* __restrict__ thr) {
+  const int b = blockIdx.x;
+  if (flags[b]) return;
+  d += (long)b * n;
+  __shared__ double sv[1024];
+  __shared__ int si[1024];
+  double best = -1.0;
+  int bi = 0x7fffffff;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    double v = d[i];
+    if (v > best || (v == best && i < bi)) { best = v; bi = i; }
+  }
+  sv[threadIdx.x] = best;
+  si[threadIdx.x] = bi;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      double o = sv[threadIdx.x + s];
+      int oi = si[threadIdx.x + s];
+      if (o > sv[threadIdx.x] || (o == sv[threadIdx.x] && oi < si[threadIdx.x])) {
+        sv[threadIdx.x] = o;
+        si[threadIdx.x] = oi;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    rank[b] = j + 1;
+    if (j + 1 >= rmax || !(sv[0] > thr[b])) {
+      flags[b] = 1;
+    } else {
+      piv[(long)b * rmax + j + 1] = si[0];
+      pval[(long)b * rmax + j + 1] = sv[0];
+    }
+  }
+}
+
+}  // namespace
+
+// pivot values are kept in `dmax0 + batch` (caller allocates 2*batch + batch*rmax doubles: see api)
+int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int rmax,
+          double tol_rel, double tol_abs, cplx* L, int* piv, int* rank, double* d, int* flags,
+          double* work) {
+  FISDF_CHECK(n > 0 && batch > 0 && rmax > 0 && rmax <= n, "pchol: bad sizes");
+  FISDF_CHECK(batch < 65536, "pchol: batch too large");
+  double* thr = work;                  // batch
+  double* pval = work + batch;         // batch * rmax
+  const int nt = 1024;
+  hipLaunchKernelGGL(pchol_init, dim3(batch), dim3(nt), 0, s, A, lda, sA, n, rmax, tol_rel,
+                     tol_abs, piv, pval, rank, d, flags, thr);
+  FISDF_HIP(hipGetLastError());
+  const int rows_per_block = 4;
+  dim3 g((n + rows_per_block - 1) / rows_per_block, batch);
+  for (int j = 0; j < rmax; ++j) {
+    hipLaunchKernelGGL(pchol_step, g, dim3(64 * rows_per_block), 0, s, A, lda, sA, n, rmax, j,
+                       piv, pval, L, d, flags);
+    hipLaunchKernelGGL(pchol_pick, dim3(batch), dim3(nt), 0, s, n, rmax, j, piv, pval, rank, d,
+                       flags, thr);
+  }
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace fisdf

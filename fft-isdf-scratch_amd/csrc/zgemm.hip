@@ -1,0 +1,271 @@
+// Batched complex128 GEMM on CDNA4 FP64 matrix cores (v_mfma_f64_16x16x4_f64).
+//
+// Replaces every BLAS zgemm the reference issues through NumPy `@` on the hot path
+// (fftisdf.py:38,41,46,76,79,84,121,205,211,215,222,225; einsums :155,159,166).
+//
+// Tile: 64x64 complex per 256-thread workgroup (4 waves, each 32x32 = 2x2 MFMA
+// blocks of 16x16), BK = 16 complex.  A and B tiles are staged global -> registers
+// -> LDS as split real/imag planes (double), so each MFMA operand is one f64 per
+// lane; the next K-tile is prefetched into registers while the current one is
+// consumed.  Complex product = 4 real MFMAs per 16x16x4 block:
+//   Cr += Ar*Br - Ai*Bi ;  Ci += Ar*Bi + Ai*Br
+// f64 MFMA fragment maps (cdna_hip_programming.md §3):
+//   A: lane l holds A[i=l&15][k=l>>4];  B: B[k=l>>4][j=l&15]
+//   C/D: 4 f64 per lane, col = l&15, row = (l>>4) + 4*r.
+#include "common.h"
+
+namespace fisdf {
+
+namespace {
+
+constexpr int BM = 64, BN = 64, BK = 16;
+constexpr int LDP = BM + 16;  // padded LDS row: k-rows 160 dwords apart -> conflict-free fragment reads
+
+template <int OP>
+__device__ __forceinline__ cplx load_op(const cplx* __restrict__ P, long ld, int r, int c, int R, int Ccols) {
+  // element (r, c) of op(P) where op(P) is R x Ccols
+  cplx v = cmk(0.0, 0.0);
+  if (r < R && c < Ccols) {
+    v = (OP & 1) ? P[(long)c * ld + r] : P[(long)r * ld + c];
+    if (OP & 2) v.y = -v.y;
+  }
+  return v;
+}
+
+// HERK=true: C = alpha A A^H (OPA = N, OPB = C, B == A, M == N); only lower-triangle tiles
+// (ti >= tj) are launched, blockIdx.x enumerates them, and the epilogue mirrors the
+// conjugate into the upper triangle — half the MFMA work of the GEMM (fftisdf.py:121).
+template <int OPA, int OPB, bool HERK>
+__global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx alpha,
+                                                    const cplx* __restrict__ A, long lda, long sA,
+                                                    const cplx* __restrict__ B, long ldb, long sB,
+                                                    cplx beta, cplx* __restrict__ C, long ldc, long sC,
+                                                    int ksplit, int kchunk, cplx* __restrict__ work) {
+  __shared__ double As[2][BK][LDP];
+  __shared__ double Bs[2][BK][LDP];
+
+  const int split = blockIdx.z % ksplit;
+  const int bz = blockIdx.z / ksplit;
+  A += (long)bz * sA;
+  B += (long)bz * sB;
+  int ti = blockIdx.y, tj = blockIdx.x;
+  if (HERK) {  // t = ti*(ti+1)/2 + tj, tj <= ti
+    const int t = blockIdx.x;
+    ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+    while (ti * (ti + 1) / 2 > t) --ti;
+    tj = t - ti * (ti + 1) / 2;
+  }
+  const int m0 = ti * BM, n0 = tj * BN;
+  const int kbeg = split * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+
+  f64x4 accR[2][2], accI[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      accR[i][j] = f64x4{0, 0, 0, 0};
+      accI[i][j] = f64x4{0, 0, 0, 0};
+    }
+
+  // per-thread element coordinates of the 4 loads per operand tile (64x16 = 1024 elements)
+  // A tile is op(A)[m0:m0+64, k:k+16]; B tile is op(B)[k:k+16, n0:n0+64]
+  cplx ra[4], rb[4];
+  auto a_coord = [&](int j, int& m, int& k) {
+    int e = tid + 256 * j;
+    if (OPA & 1) { m = e & 63; k = e >> 6; }   // memory [k][m]: m contiguous
+    else { m = e >> 4; k = e & 15; }           // memory [m][k]: k contiguous
+  };
+  auto b_coord = [&](int j, int& k, int& n) {
+    int e = tid + 256 * j;
+    if (OPB & 1) { n = e >> 4; k = e & 15; }   // memory [n][k]
+    else { n = e & 63; k = e >> 6; }           // memory [k][n]
+  };
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int m, k;
+      a_coord(j, m, k);
+      int gk = k0 + k;
+      ra[j] = load_op<OPA>(A, lda, m0 + m, gk, M, gk < kend ? K : 0);
+      int kk, n;
+      b_coord(j, kk, n);
+      int gk2 = k0 + kk;
+      rb[j] = load_op<OPB>(B, ldb, gk2, n0 + n, gk2 < kend ? K : 0, N);
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int m, k;
+      a_coord(j, m, k);
+      As[0][k][m] = ra[j].x;
+      As[1][k][m] = ra[j].y;
+      int kk, n;
+      b_coord(j, kk, n);
+      Bs[0][kk][n] = rb[j].x;
+      Bs[1][kk][n] = rb[j].y;
+    }
+  };
+
+  if (kbeg < kend) gload(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();
+    lstore();
+    __syncthreads();
+    if (k0 + BK < kend) gload(k0 + BK);  // prefetch next tile into registers
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      const int ka = kk + (lane >> 4), i = lane & 15;
+      double ar[2], ai[2], br[2], bi[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        ar[t] = As[0][ka][wm + t * 16 + i];
+        ai[t] = As[1][ka][wm + t * 16 + i];
+        br[t] = Bs[0][ka][wn + t * 16 + i];
+        bi[t] = Bs[1][ka][wn + t * 16 + i];
+      }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], accR[mi][ni], 0, 0, 0);
+          accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], bi[ni], accI[mi][ni], 0, 0, 0);
+          accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ai[mi], bi[ni], accR[mi][ni], 0, 0, 0);
+          accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], br[ni], accI[mi][ni], 0, 0, 0);
+        }
+    }
+  }
+
+  // epilogue
+  if (ksplit > 1) {
+    cplx* Wp = work + ((long)bz * ksplit + split) * (long)M * N;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
+          int col = n0 + wn + ni * 16 + (lane & 15);
+          if (row < M && col < N) {
+            Wp[(long)row * N + col] = cmk(accR[mi][ni][r], accI[mi][ni][r]);
+            if (HERK && ti != tj) Wp[(long)col * N + row] = cmk(accR[mi][ni][r], -accI[mi][ni][r]);
+          }
+        }
+    return;
+  }
+  C += (long)bz * sC;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
+        int col = n0 + wn + ni * 16 + (lane & 15);
+        if (row < M && col < N) {
+          cplx v = cmul(alpha, cmk(accR[mi][ni][r], accI[mi][ni][r]));
+          cplx* cp = C + (long)row * ldc + col;
+          if (beta.x != 0.0 || beta.y != 0.0) v = cadd(v, cmul(beta, *cp));
+          *cp = v;
+          if (HERK && ti != tj) C[(long)col * ldc + row] = cconj(v);
+        }
+      }
+}
+
+// C = alpha * sum_s work[s] + beta * C  (deterministic split-K reduction)
+__global__ void ksplit_reduce(int M, int N, int ksplit, const cplx* __restrict__ work, cplx alpha,
+                              cplx beta, cplx* __restrict__ C, long ldc, long sC) {
+  const int bz = blockIdx.y;
+  const long MN = (long)M * N;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < MN; e += (long)gridDim.x * blockDim.x) {
+    cplx acc = cmk(0, 0);
+    for (int s = 0; s < ksplit; ++s) acc = cadd(acc, work[((long)bz * ksplit + s) * MN + e]);
+    int row = (int)(e / N), col = (int)(e % N);
+    cplx* cp = C + (long)bz * sC + (long)row * ldc + col;
+    cplx v = cmul(alpha, acc);
+    if (beta.x != 0.0 || beta.y != 0.0) v = cadd(v, cmul(beta, *cp));
+    *cp = v;
+  }
+}
+
+template <int OPA, int OPB, bool HERK = false>
+void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cplx* A, long lda,
+            long sA, const cplx* B, long ldb, long sB, cplx beta, cplx* C, long ldc, long sC,
+            int ksplit, int kchunk, cplx* work) {
+  hipLaunchKernelGGL((zgemm_kernel<OPA, OPB, HERK>), grid, dim3(256), 0, s, M, N, K, alpha, A, lda, sA,
+                     B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work);
+}
+
+}  // namespace
+
+int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, const cplx* A,
+          long lda, long sA, const cplx* B, long ldb, long sB, cplx beta, cplx* C, long ldc,
+          long sC, int batch, int ksplit, cplx* work) {
+  FISDF_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 0, "zgemm: negative size");
+  FISDF_CHECK(opA >= 0 && opA < 4 && opB >= 0 && opB < 4, "zgemm: bad op");
+  if (M == 0 || N == 0 || batch == 0) return 0;
+  if (ksplit < 1) ksplit = 1;
+  if (ksplit > 1) FISDF_CHECK(work != nullptr, "zgemm: split-K needs a workspace");
+  int kchunk = (K + ksplit - 1) / ksplit;
+  kchunk = ((kchunk + BK - 1) / BK) * BK;
+  if (kchunk == 0) kchunk = BK;
+  ksplit = std::max(1, (K + kchunk - 1) / kchunk);
+  FISDF_CHECK((long)batch * ksplit < 65536, "zgemm: batch*ksplit exceeds grid.z");
+  dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch * ksplit);
+  FISDF_CHECK(grid.y < 65536, "zgemm: M too large");
+  if (K == 0) ksplit = 1;
+#define FISDF_CASE(a, b)                                                                      \
+  case a * 4 + b:                                                                             \
+    launch<a, b>(s, grid, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit,   \
+                 kchunk, work);                                                               \
+    break;
+  switch (opA * 4 + opB) {
+    FISDF_CASE(0, 0) FISDF_CASE(0, 1) FISDF_CASE(0, 2) FISDF_CASE(0, 3)
+    FISDF_CASE(1, 0) FISDF_CASE(1, 1) FISDF_CASE(1, 2) FISDF_CASE(1, 3)
+    FISDF_CASE(2, 0) FISDF_CASE(2, 1) FISDF_CASE(2, 2) FISDF_CASE(2, 3)
+    FISDF_CASE(3, 0) FISDF_CASE(3, 1) FISDF_CASE(3, 2) FISDF_CASE(3, 3)
+  }
+#undef FISDF_CASE
+  FISDF_HIP(hipGetLastError());
+  if (ksplit > 1) {
+    long MN = (long)M * N;
+    int blocks = (int)std::min<long>((MN + 255) / 256, 4096);
+    hipLaunchKernelGGL(ksplit_reduce, dim3(blocks, batch), dim3(256), 0, s, M, N, ksplit, work,
+                       alpha, beta, C, ldc, sC);
+    FISDF_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+// C = alpha A A^H, A: n x K (row-major, lda), C: n x n (ldc) Hermitian, lower tiles + mirror.
+int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cplx* C, long ldc,
+         int ksplit, cplx* work) {
+  FISDF_CHECK(n >= 0 && K >= 0, "herk: negative size");
+  if (n == 0) return 0;
+  if (ksplit < 1) ksplit = 1;
+  if (ksplit > 1) FISDF_CHECK(work != nullptr, "herk: split-K needs a workspace");
+  int kchunk = (K + ksplit - 1) / ksplit;
+  kchunk = std::max(BK, ((kchunk + BK - 1) / BK) * BK);
+  ksplit = std::max(1, (K + kchunk - 1) / kchunk);
+  const int nt = (n + BM - 1) / BM;
+  dim3 grid(nt * (nt + 1) / 2, 1, ksplit);
+  launch<OP_N, OP_C, true>(s, grid, n, n, K, cmk(alpha, 0), A, lda, 0, A, lda, 0, cmk(0, 0), C,
+                           ldc, 0, ksplit, kchunk, work);
+  FISDF_HIP(hipGetLastError());
+  if (ksplit > 1) {
+    long MN = (long)n * n;
+    int blocks = (int)std::min<long>((MN + 255) / 256, 4096);
+    hipLaunchKernelGGL(ksplit_reduce, dim3(blocks, 1), dim3(256), 0, s, n, n, ksplit, work,
+                       cmk(alpha, 0), cmk(0, 0), C, ldc, 0L);
+    FISDF_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+}  // namespace fisdf

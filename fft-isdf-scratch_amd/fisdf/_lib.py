@@ -1,0 +1,139 @@
+"""ctypes binding of libfisdf.so (the C-ABI of include/fisdf.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU is
+visible, ``load()`` / ``Context()`` raise.  Device memory is handed over as raw
+pointers (``torch.Tensor.data_ptr()`` of CUDA/HIP tensors or ``fisdf_malloc``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfisdf.so")
+
+STAGES = ["select", "x4", "y", "factor", "fft", "trsm", "herk", "small", "get_j", "get_k", "ws"]
+
+_lib = None
+
+_vp = C.c_void_p
+_i = C.c_int
+_l = C.c_long
+_d = C.c_double
+_ip = C.POINTER(C.c_int)
+_dp = C.POINTER(C.c_double)
+
+_SIGS = {
+    "fisdf_abi_version": ([], _i),
+    "fisdf_create": ([_i, _vp, C.POINTER(_vp)], _i),
+    "fisdf_destroy": ([_vp], _i),
+    "fisdf_last_error": ([], C.c_char_p),
+    "fisdf_sync": ([_vp], _i),
+    "fisdf_malloc": ([_vp, C.c_size_t, C.POINTER(_vp)], _i),
+    "fisdf_free": ([_vp, _vp], _i),
+    "fisdf_memcpy_htod": ([_vp, _vp, _vp, C.c_size_t], _i),
+    "fisdf_memcpy_dtoh": ([_vp, _vp, _vp, C.c_size_t], _i),
+    "fisdf_set_timing": ([_vp, _i], _i),
+    "fisdf_timings": ([_vp, _dp, _ip], _i),
+    "fisdf_max_imag": ([_vp, _dp], _i),
+    "fisdf_select_points": ([_vp, _vp, _i, _i, _i, _i, _d, _ip, _ip, _ip], _i),
+    "fisdf_gather_points": ([_vp, _vp, _i, _i, _i, _ip, _i, _vp], _i),
+    "fisdf_build_x4": ([_vp, _vp, _i, _i, _ip, _dp, _vp], _i),
+    "fisdf_build_y": ([_vp, _vp, _l, _i, _i, _i, _vp, _i, _i, _ip, _dp, _i, _i, _vp], _i),
+    "fisdf_factor_x4": ([_vp, _vp, _i, _i, _i, _d, _ip], _i),
+    "fisdf_fit_coulomb": ([_vp, _i, _i, _vp, _i, _ip, _ip, _dp, _vp], _i),
+    "fisdf_build_ws": ([_vp, _vp, _i, _i, _i, _ip, _dp, _vp], _i),
+    "fisdf_get_j": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp], _i),
+    "fisdf_get_k": ([_vp, _vp, _vp, _vp, _i, _i, _i, _ip, _dp, _vp], _i),
+    "fisdf_zgemm": ([_vp, _i, _i, _i, _i, _i, _dp, _vp, _l, _l, _vp, _l, _l, _dp, _vp, _l, _l,
+                     _i, _i], _i),
+    "fisdf_herk": ([_vp, _i, _i, _d, _vp, _l, _vp, _l, _i], _i),
+    "fisdf_fft3d": ([_vp, _vp, _vp, _i, _ip], _i),
+    "fisdf_coulg": ([_vp, _ip, _dp, _dp, _d, _i, _vp], _i),
+    "fisdf_pivoted_cholesky": ([_vp, _vp, _i, _i, _i, _d, _ip, _ip], _i),
+}
+
+
+class FisdfError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load libfisdf.so and declare every exported symbol (fails loudly if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FisdfError(
+            f"{path} not found: build the HIP extension first (python -c "
+            f"'import __graft_entry__ as g; g.build()')")
+    lib = C.CDLL(path)
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        raise FisdfError(load().fisdf_last_error().decode())
+
+
+def iarr(x):
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.int32))
+    return a, a.ctypes.data_as(_ip)
+
+
+def darr(x):
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    return a, a.ctypes.data_as(_dp)
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (must be contiguous and on the GPU)."""
+    if not t.is_cuda:
+        raise FisdfError("fisdf expects device tensors")
+    if not t.is_contiguous():
+        raise FisdfError("fisdf expects contiguous tensors")
+    return _vp(t.data_ptr())
+
+
+class Context:
+    """One fisdf context per process/device, bound to torch's current HIP stream."""
+
+    def __init__(self, device: int = 0, stream=None):
+        lib = load()
+        out = _vp()
+        check(lib.fisdf_create(int(device), _vp(stream) if stream else None, C.byref(out)))
+        self.lib = lib
+        self.h = out
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.fisdf_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def call(self, name, *args):
+        check(getattr(self.lib, name)(self.h, *args))
+
+    def timings(self):
+        ms = (C.c_double * len(STAGES))()
+        calls = (C.c_int * len(STAGES))()
+        self.call("fisdf_timings", ms, calls)
+        return {s: (ms[i], calls[i]) for i, s in enumerate(STAGES)}
+
+    def max_imag(self):
+        out = (C.c_double * 3)()
+        self.call("fisdf_max_imag", out)
+        return list(out)

@@ -1,0 +1,360 @@
+"""PySCF-style ISDF density-fitting object on MI355X (mirror of fftisdf.py).
+
+Drop-in for ``InterpolativeSeparableDensityFitting`` / ``ISDF`` of the reference
+(/root/reference/fftisdf.py:296-410): same constructor, attributes (``c0``, ``m0``,
+``blksize``, ``_x``, ``_w0``, ``_wq``), ``build()``, ``aoR_loop()``,
+``select_interpolation_points()``, ``get_jk()`` and the module functions ``build``,
+``get_j_kpts`` and ``get_k_kpts`` — with every numerical stage executed by the HIP
+kernels of libfisdf.so (no CPU fallback: missing library or GPU raises).
+
+Differences from the reference, all deliberate:
+* the zgelsy fit (fftisdf.py:108) is replaced by a pivoted-Cholesky factorisation of
+  x4_q applied in factored order (tolerance ``fit_tol``); J/K agree with
+  the gelsy oracle to < 1e-8 but W_q differs in the null space of x4_q;
+* ``y`` stays resident in HBM (no HDF5 scratch, fftisdf.py:60-63);
+* the bug of fftisdf.py:322 (global ``cell``) is not reproduced;
+* optional k-point sharding over ranks of a torch.distributed group (``comm``).
+"""
+from __future__ import annotations
+
+import logging
+import time
+
+import numpy as np
+
+from . import _lib
+from .cell import eval_ao_kpts, make_kpts
+
+log = logging.getLogger("fisdf")
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def kpts_to_kmesh(cell, kpts):
+    """[pyscf] k2gamma.kpts_to_kmesh: number of distinct scaled coordinates per axis."""
+    kpts = np.asarray(kpts, float).reshape(-1, 3)
+    scaled = kpts @ cell.lattice_vectors().T / (2 * np.pi)
+    kmesh = [len(np.unique(np.round(scaled[:, i], 6))) for i in range(3)]
+    return np.asarray(kmesh)
+
+
+def _format_dms(dm_kpts, nkpts):
+    """[pyscf] df_jk._format_dms -> (nset, nk, nao, nao)."""
+    dm = np.asarray(dm_kpts)
+    nao = dm.shape[-1]
+    return dm.reshape(-1, nkpts, nao, nao)
+
+
+def _format_jks(v, dm_kpts):
+    """[pyscf] df_jk._format_jks: result shaped like the input dm."""
+    return v.reshape(np.shape(dm_kpts))
+
+
+class _Device:
+    """Per-process device state: torch device, fisdf context, k-point shard."""
+
+    def __init__(self, device=None, comm=None):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise _lib.FisdfError("fisdf: no GPU visible (the HIP path has no CPU fallback)")
+        if device is None:
+            device = torch.cuda.current_device()
+        self.torch = torch
+        self.dev = torch.device("cuda", int(device))
+        self.stream = torch.cuda.current_stream(self.dev)
+        self.ctx = _lib.Context(int(device), self.stream.cuda_stream)
+        self.comm = comm
+        if comm is not None:
+            import torch.distributed as dist
+            self.rank = dist.get_rank(comm)
+            self.size = dist.get_world_size(comm)
+        else:
+            self.rank, self.size = 0, 1
+
+    def shard(self, nk):
+        """Contiguous q-range of this rank."""
+        base, rem = divmod(nk, self.size)
+        q0 = self.rank * base + min(self.rank, rem)
+        q1 = q0 + base + (1 if self.rank < rem else 0)
+        return q0, q1
+
+    def empty(self, shape, dtype="c128"):
+        t = self.torch
+        dt = {"c128": t.complex128, "f64": t.float64, "i32": t.int32}[dtype]
+        return t.empty(tuple(int(s) for s in shape), dtype=dt, device=self.dev)
+
+    def to_dev(self, arr):
+        t = self.torch
+        a = np.ascontiguousarray(arr)
+        return t.from_numpy(a).to(self.dev, non_blocking=False)
+
+
+class InterpolativeSeparableDensityFitting:
+    """ISDF(cell, kpts, m0=None, c0=20.0) — fftisdf.py:296-306."""
+
+    _x = None
+    _w0 = None
+    _wq = None
+    blksize = 8000          # fftisdf.py:300
+    fit_tol = 1e-14         # relative pivot cut of the x4_q factorisation
+    select_tol = -1.0       # dpstrf default tolerance (ng0*eps*max diag)
+
+    def __init__(self, cell, kpts, m0=None, c0=20.0, device=None, comm=None):
+        self.cell = cell
+        self.kpts = np.asarray(kpts, float).reshape(-1, 3)
+        self.m0 = m0 if m0 is not None else [15, 15, 15]
+        self.c0 = c0
+        self.mesh = tuple(cell.mesh)
+        self.verbose = getattr(cell, "verbose", 0)
+        self.kmesh = None
+        self._device_id = device
+        self._comm = comm
+        self._d = None
+        self._ao_grid = None      # device (nk, ngrid, nao) Bloch AOs on the FFT grid (cached)
+        self._ao_parent = None    # device (nk, ng0, nao) Bloch AOs on the parent grid (cached)
+        self._dev_state = None
+        self.timings = {}
+        self.nip = None
+        self.ranks = None
+
+    # ---- device plumbing --------------------------------------------------
+    @property
+    def device(self):
+        if self._d is None:
+            self._d = _Device(self._device_id, self._comm)
+        return self._d
+
+    def grids_coords(self):
+        return self.cell.gen_uniform_grids(self.mesh)
+
+    def preload_ao(self):
+        """Evaluate and upload the AO inputs (PySCF's job in the reference) before build."""
+        kmesh = self._kmesh()
+        d = self.device
+        if self._ao_parent is None:
+            x0 = eval_ao_kpts(self.cell, self.cell.gen_uniform_grids(self.m0), kmesh)
+            self._ao_parent = d.to_dev(x0)
+        if self._ao_grid is None:
+            f = eval_ao_kpts(self.cell, self.grids_coords(), kmesh)
+            self._ao_grid = d.to_dev(f)
+        return self
+
+    def _kmesh(self):
+        if self.kmesh is None:
+            self.kmesh = kpts_to_kmesh(self.cell, self.kpts)
+            self.kpts = make_kpts(self.cell, self.kmesh)        # fftisdf.py:317-322 (self.cell)
+        return self.kmesh
+
+    # ---- reference surface ----------------------------------------------
+    def build(self):
+        """fftisdf.py:308-325."""
+        self._kmesh()
+        return build(self)
+
+    def aoR_loop(self, grids=None, kpts=None, deriv=0, blksize=None):
+        """fftisdf.py:327-355: yields ((ao_k,), g0, g1) over blocks of the FFT grid (host)."""
+        assert deriv == 0
+        coords = self.grids_coords() if grids is None else np.asarray(getattr(grids, "coords", grids))
+        blksize = self.blksize if blksize is None else blksize
+        kmesh = self._kmesh()
+        for g0 in range(0, coords.shape[0], blksize):
+            g1 = min(g0 + blksize, coords.shape[0])
+            yield (eval_ao_kpts(self.cell, coords[g0:g1], kmesh),), g0, g1
+
+    def select_interpolation_points(self, x0=None, phase=None):
+        """fftisdf.py:357-388 on the GPU; returns X = x0[:, perm[:nip], :] as a host array."""
+        self._select()
+        return self._dev_state["X"].cpu().numpy()
+
+    def _select(self):
+        d = self.device
+        kmesh = self._kmesh()
+        nk = int(np.prod(kmesh))
+        nao = self.cell.nao_nr()
+        if self._ao_parent is None:
+            x0 = eval_ao_kpts(self.cell, self.cell.gen_uniform_grids(self.m0), kmesh)
+            self._ao_parent = d.to_dev(x0)
+        x0 = self._ao_parent
+        ng0 = x0.shape[1]
+        nip_max = min(int(nao * self.c0), ng0)
+        perm = np.zeros(nip_max, np.int32)
+        npiv = C_int()
+        full = C_int()
+        d.ctx.call("fisdf_select_points", _lib.ptr(x0), nk, ng0, nao, nip_max,
+                   float(self.select_tol), perm.ctypes.data_as(_lib._ip), byref(npiv), byref(full))
+        nip = min(nip_max, npiv.value)                                  # fftisdf.py:383
+        self.perm = perm[:nip].copy()
+        X = d.empty((nk, nip, nao))
+        d.ctx.call("fisdf_gather_points", _lib.ptr(x0), nk, ng0, nao,
+                   self.perm.ctypes.data_as(_lib._ip), nip, _lib.ptr(X))
+        log.info("Pivoted Cholesky: nip = %d (rank %s)", nip, "reached" if full.value else ">= nip")
+        self._dev_state = dict(X=X)
+        self.nip = nip
+        return X
+
+    def set_interpolation_points(self, perm):
+        """Inject a selection (e.g. the oracle's pivots, SURVEY.md §7 hard part (b))."""
+        d = self.device
+        kmesh = self._kmesh()
+        nk = int(np.prod(kmesh))
+        nao = self.cell.nao_nr()
+        if self._ao_parent is None:
+            x0 = eval_ao_kpts(self.cell, self.cell.gen_uniform_grids(self.m0), kmesh)
+            self._ao_parent = d.to_dev(x0)
+        x0 = self._ao_parent
+        self.perm = np.ascontiguousarray(perm, dtype=np.int32)
+        nip = len(self.perm)
+        X = d.empty((nk, nip, nao))
+        d.ctx.call("fisdf_gather_points", _lib.ptr(x0), nk, x0.shape[1], nao,
+                   self.perm.ctypes.data_as(_lib._ip), nip, _lib.ptr(X))
+        self._dev_state = dict(X=X)
+        self.nip = nip
+
+    def get_jk(self, dm, hermi=1, kpts=None, kpts_band=None, with_j=True, with_k=True,
+               omega=None, exxdiv=None):
+        """fftisdf.py:390-408."""
+        if omega is not None:
+            raise NotImplementedError
+        if exxdiv is not None:
+            raise NotImplementedError
+        kpts = self.kpts if kpts is None else np.asarray(kpts)
+        if kpts.ndim == 1:                                            # _check_kpts single kpt
+            raise NotImplementedError
+        vj = vk = None
+        if with_k:
+            vk = get_k_kpts(self, dm, hermi, kpts, kpts_band, exxdiv)
+        if with_j:
+            vj = get_j_kpts(self, dm, hermi, kpts, kpts_band)
+        return vj, vk
+
+    # reference attributes, materialised on demand from HBM
+    def __getattribute__(self, name):
+        if name in ("_x", "_w0", "_wq"):
+            st = object.__getattribute__(self, "_dev_state")
+            if st is not None and "W0" in st:
+                if name == "_x":
+                    return st["X"].cpu().numpy()
+                if name == "_w0":
+                    return st["W0"].cpu().numpy()
+                return object.__getattribute__(self, "_gather_wq")()
+        return object.__getattribute__(self, name)
+
+    def _gather_wq(self):
+        st = self._dev_state
+        d = self.device
+        if d.size == 1:
+            return st["Wq"].cpu().numpy()
+        import torch.distributed as dist
+        nk = int(np.prod(self.kmesh))
+        parts = [None] * d.size
+        dist.all_gather_object(parts, (d.shard(nk), st["Wq"].cpu().numpy()), group=d.comm)
+        out = np.zeros((nk, self.nip, self.nip), complex)
+        for (q0, q1), w in parts:
+            out[q0:q1] = w
+        return out
+
+
+ISDF = InterpolativeSeparableDensityFitting
+
+from ctypes import c_int as C_int, byref  # noqa: E402
+
+
+def build(df_obj):
+    """fftisdf.py:22-128 on the GPU.  Leaves X, W_q (own shard), W_0, W_s resident."""
+    t0 = time.perf_counter()
+    d = df_obj.device
+    torch = d.torch
+    cell = df_obj.cell
+    kmesh = np.asarray(df_obj._kmesh(), dtype=np.int32)
+    nk = int(np.prod(kmesh))
+    nao = cell.nao_nr()
+    a = np.ascontiguousarray(cell.lattice_vectors(), dtype=np.float64)
+    km_c, km_p = _lib.iarr(kmesh)
+    a_c, a_p = _lib.darr(a.ravel())
+    mesh_c, mesh_p = _lib.iarr(df_obj.mesh)
+    ngrid = int(np.prod(df_obj.mesh))
+
+    if df_obj._dev_state is None or "X" not in df_obj._dev_state:
+        df_obj._select()                                                 # fftisdf.py:33
+    X = df_obj._dev_state["X"]
+    nip = X.shape[1]
+
+    x4 = d.empty((nk, nip, nip))
+    d.ctx.call("fisdf_build_x4", _lib.ptr(X), nip, nao, km_p, a_p, _lib.ptr(x4))   # :38-48
+
+    q0, q1 = d.shard(nk)
+    if df_obj._ao_grid is None:
+        df_obj._ao_grid = d.to_dev(eval_ao_kpts(cell, df_obj.grids_coords(), kmesh))
+    f = df_obj._ao_grid
+    yT = d.empty((q1 - q0, nip, ngrid))
+    d.ctx.call("fisdf_build_y", _lib.ptr(f), ngrid * nao, 0, ngrid, ngrid, _lib.ptr(X), nip, nao,
+               km_p, a_p, q0, q1, _lib.ptr(yT))                          # :67-87
+
+    ranks = np.zeros(q1 - q0, np.int32)
+    d.ctx.call("fisdf_factor_x4", _lib.ptr(x4), q0, q1, nip, float(df_obj.fit_tol),
+               ranks.ctypes.data_as(_lib._ip))
+    Wq = d.empty((q1 - q0, nip, nip))
+    d.ctx.call("fisdf_fit_coulomb", q0, q1, _lib.ptr(yT), nip, mesh_p, km_p, a_p, _lib.ptr(Wq))
+    del yT
+
+    Ws = d.empty((nk, nip, nip))
+    d.ctx.call("fisdf_build_ws", _lib.ptr(Wq), q0, q1, nip, km_p, a_p, _lib.ptr(Ws))  # :204-207
+    if d.size > 1:
+        import torch.distributed as dist
+        dist.all_reduce(Ws, group=d.comm)                                 # k-sum of W_s
+        W0 = Wq[0].clone() if q0 == 0 else d.empty((nip, nip))
+        owner = 0  # rank holding q = 0
+        dist.broadcast(W0, src=dist.get_global_rank(d.comm, owner) if d.comm is not None else owner,
+                       group=d.comm)
+    else:
+        W0 = Wq[0]
+    df_obj._dev_state.update(x4=x4, Wq=Wq, W0=W0, Ws=Ws)
+    df_obj.ranks = ranks
+    df_obj.nip = nip
+    df_obj.timings["build"] = time.perf_counter() - t0
+    return df_obj
+
+
+def _dms_to_dev(df_obj, dm_kpts):
+    nk = int(np.prod(df_obj.kmesh))
+    dms = _format_dms(dm_kpts, nk).astype(np.complex128)
+    return dms, df_obj.device.to_dev(dms)
+
+
+def get_j_kpts(df_obj, dm_kpts, hermi=1, kpts=np.zeros((1, 3)), kpts_band=None, exxdiv=None):
+    """fftisdf.py:133-171."""
+    assert exxdiv is None
+    st = df_obj._dev_state
+    assert st is not None and "W0" in st, "call build() first"
+    d = df_obj.device
+    dms, ddms = _dms_to_dev(df_obj, dm_kpts)
+    nset, nk, nao = dms.shape[:3]
+    nip = st["X"].shape[1]
+    vj = d.empty(dms.shape)
+    d.ctx.call("fisdf_get_j", _lib.ptr(st["X"]), _lib.ptr(st["W0"]), _lib.ptr(ddms), nset, nk,
+               nip, nao, _lib.ptr(vj))
+    out = vj.cpu().numpy()
+    band = np.asarray(kpts if kpts_band is None else kpts_band)
+    if abs(band).max() < 1e-9:                                           # :169-170
+        out = out.real
+    return _format_jks(out, dm_kpts)
+
+
+def get_k_kpts(df_obj, dm_kpts, hermi=1, kpts=np.zeros((1, 3)), kpts_band=None, exxdiv=None):
+    """fftisdf.py:173-228."""
+    assert exxdiv is None
+    st = df_obj._dev_state
+    assert st is not None and "Ws" in st, "call build() first"
+    d = df_obj.device
+    dms, ddms = _dms_to_dev(df_obj, dm_kpts)
+    nset, nk, nao = dms.shape[:3]
+    nip = st["X"].shape[1]
+    km_c, km_p = _lib.iarr(df_obj.kmesh)
+    a_c, a_p = _lib.darr(np.asarray(df_obj.cell.lattice_vectors(), float).ravel())
+    vk = d.empty(dms.shape)
+    d.ctx.call("fisdf_get_k", _lib.ptr(st["X"]), _lib.ptr(st["Ws"]), _lib.ptr(ddms), nset, nip,
+               nao, km_p, a_p, _lib.ptr(vk))
+    return _format_jks(vk.cpu().numpy(), dm_kpts)

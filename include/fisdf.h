@@ -1,0 +1,143 @@
+/*
+ * fisdf — MI355X-native FFT-ISDF kernel library: the C-ABI drop-in boundary.
+ *
+ * The reference (yangjunjie0320/fft-isdf-scratch) has no native boundary: its hot
+ * path is the Python module fftisdf.py calling NumPy/SciPy/PySCF.  Each entry point
+ * below replaces one stage of that path; the Python mirror of the reference's
+ * `ISDF` class (fft-isdf-scratch_amd/fisdf/isdf.py) binds them with ctypes
+ * (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - complex arrays are complex128 (interleaved double re/im), C-contiguous.
+ *  - pointers named d_* are DEVICE pointers (hipMalloc'ed, or from fisdf_malloc);
+ *    pointers named h_* are host pointers.  Work is enqueued on the context's stream
+ *    and is asynchronous unless the function says "synchronous".
+ *  - every function returns 0 on success or a negative code; fisdf_last_error()
+ *    returns the message of the last failure on the calling thread.
+ *  - one context per process/device; not thread-safe.
+ */
+#ifndef FISDF_H
+#define FISDF_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FISDF_ABI_VERSION 1
+
+typedef struct fisdf_ctx fisdf_ctx;
+
+/* stage ids for fisdf_timings */
+enum {
+  FISDF_ST_SELECT = 0, /* Gram + pivoted Cholesky (fftisdf.py:357-388)          */
+  FISDF_ST_X4 = 1,     /* x2_k, x2_s, x4_s, x4_k (fftisdf.py:38-48)               */
+  FISDF_ST_Y = 2,      /* y build (fftisdf.py:67-87)                              */
+  FISDF_ST_FACTOR = 3, /* per-q factorisation of x4_q (replaces zgelsy QRCP :108) */
+  FISDF_ST_FFT = 4,    /* fft(z_q * f_q) * coulG weight (fftisdf.py:113-115)      */
+  FISDF_ST_TRSM = 5,   /* factored fit application (fftisdf.py:108)               */
+  FISDF_ST_HERK = 6,   /* W_q = zeta z_q^H (fftisdf.py:118-121, Parseval HERK)   */
+  FISDF_ST_SMALL = 7,  /* nip x nip back-substitutions + scatter                  */
+  FISDF_ST_J = 8,      /* get_j_kpts (fftisdf.py:133-171)                         */
+  FISDF_ST_K = 9,      /* get_k_kpts (fftisdf.py:173-228)                         */
+  FISDF_ST_WS = 10,    /* W_s = Re(Phi W) sqrt(nk) (fftisdf.py:204-207)           */
+  FISDF_NSTAGES = 11
+};
+
+/* ---- context / memory ---------------------------------------------------- */
+int fisdf_abi_version(void);
+int fisdf_create(int device, void* hip_stream /* NULL: own stream */, fisdf_ctx** out);
+int fisdf_destroy(fisdf_ctx* ctx);
+const char* fisdf_last_error(void);
+int fisdf_sync(fisdf_ctx* ctx);
+int fisdf_malloc(fisdf_ctx* ctx, size_t bytes, void** d_ptr);
+int fisdf_free(fisdf_ctx* ctx, void* d_ptr);
+int fisdf_memcpy_htod(fisdf_ctx* ctx, void* d_dst, const void* h_src, size_t bytes); /* synchronous */
+int fisdf_memcpy_dtoh(fisdf_ctx* ctx, void* h_dst, const void* d_src, size_t bytes); /* synchronous */
+int fisdf_set_timing(fisdf_ctx* ctx, int enable);
+int fisdf_timings(fisdf_ctx* ctx, double* h_ms /* FISDF_NSTAGES */, int* h_calls); /* synchronous; resets */
+/* reality invariants, max |Im| seen since the last call: [0] x2_s (fftisdf.py:43),
+ * [1] fx_s (fftisdf.py:81), [2] rho_s (fftisdf.py:216).  synchronous; resets. */
+int fisdf_max_imag(fisdf_ctx* ctx, double* h_out /* 3 */);
+
+/* ---- A1: interpolation-point selection ------------------------------------
+ * Replaces InterpolativeSeparableDensityFitting.select_interpolation_points
+ * (fftisdf.py:357-388): x2 = sum_q Re(x0_q^* x0_q^T); x4 = x2*x2/nk; greedy pivoted
+ * Cholesky of x4 (LAPACK dpstrf semantics, tol <= 0 -> ng0*eps*max(diag)).
+ * Produces the first min(nip_max, rank) pivots.  synchronous.
+ *   d_x0 (nk, ng0, nao) c128;  h_perm (nip_max) int;  *h_npiv = pivots produced;
+ *   *h_full_rank = 1 if the tolerance (not nip_max) stopped the factorisation. */
+int fisdf_select_points(fisdf_ctx* ctx, const void* d_x0, int nk, int ng0, int nao, int nip_max,
+                        double tol, int* h_perm, int* h_npiv, int* h_full_rank);
+
+/* X[k, I, :] = x0[k, perm[I], :]  (fftisdf.py:388) */
+int fisdf_gather_points(fisdf_ctx* ctx, const void* d_x0, int nk, int ng0, int nao,
+                        const int* h_perm, int nip, void* d_X);
+
+/* ---- A2: x4_k = Phi^H ((Phi x2_k)^2), x2_k = X_k^* X_k^T  (fftisdf.py:38-48) ----
+ *   d_X (nk, nip, nao); d_x4 (nk, nip, nip); a: lattice (3x3 rows, bohr) */
+int fisdf_build_x4(fisdf_ctx* ctx, const void* d_X, int nip, int nao, const int kmesh[3],
+                   const double a[9], void* d_x4);
+
+/* ---- A3: y build for one grid block (fftisdf.py:67-87) ---------------------
+ * d_f: Bloch AOs of the block, element (k, g, m) at d_f[k*f_kstride + g*nao + m],
+ * g in [0, nblk); writes y_q, q in [q0, q1) (a k-point shard), for grid points
+ * [g0, g0+nblk) into the library's transposed layout d_yT[q-q0][I][g]
+ * (q1-q0, nip, ngrid). */
+int fisdf_build_y(fisdf_ctx* ctx, const void* d_f, long f_kstride, int g0, int nblk, int ngrid,
+                  const void* d_X, int nip, int nao, const int kmesh[3], const double a[9],
+                  int q0, int q1, void* d_yT);
+
+/* ---- A4: per-q factorisation of x4_q, q in [q0, q1) (replaces zgelsy's QRCP,
+ * fftisdf.py:108).  Pivoted Cholesky with rank cut tol_rel*max(diag); factors stay in
+ * the context.  d_x4: (nk, nip, nip) (all q).  synchronous: h_ranks (q1-q0) receives
+ * the numerical ranks (logged at fftisdf.py:122). */
+int fisdf_factor_x4(fisdf_ctx* ctx, const void* d_x4, int q0, int q1, int nip, double tol_rel,
+                    int* h_ranks);
+
+/* ---- A4+A5: fit + FFT Coulomb for the factored shard q in [q0, q1) (fftisdf.py:97-121)
+ * Needs fisdf_factor_x4 on the same range.  W_q = zeta_q z_q^H computed as
+ * (vol/N^2) Zhat diag(coulG(k_q+G)) Zhat^H with Zhat = FFT(z_q * f_q), the
+ * fit applied in factored order.  d_yT: (q1-q0, nip, ngrid) from fisdf_build_y;
+ * d_Wq: (q1-q0, nip, nip). */
+int fisdf_fit_coulomb(fisdf_ctx* ctx, int q0, int q1, const void* d_yT, int nip,
+                      const int mesh[3], const int kmesh[3], const double a[9], void* d_Wq);
+
+/* ---- A8 prep: W_s[R] = sqrt(nk) Re(sum_{q in [q0,q1)} Phi[R,q] W_q) (fftisdf.py:204-207)
+ * d_Wq: (q1-q0, nip, nip) shard; d_Ws: (nimg, nip, nip) c128 with zero imaginary part
+ * (partial sum for a q-shard; shards are summed with an all-reduce). */
+int fisdf_build_ws(fisdf_ctx* ctx, const void* d_Wq, int q0, int q1, int nip,
+                   const int kmesh[3], const double a[9], void* d_Ws);
+
+/* ---- A7: get_j_kpts (fftisdf.py:133-171) ------------------------------------
+ * d_dms (nset, nk, nao, nao); d_vj same shape (complex; caller takes .real for Gamma). */
+int fisdf_get_j(fisdf_ctx* ctx, const void* d_X, const void* d_W0, const void* d_dms, int nset,
+                int nk, int nip, int nao, void* d_vj);
+
+/* ---- A8: get_k_kpts (fftisdf.py:173-228) ------------------------------------ */
+int fisdf_get_k(fisdf_ctx* ctx, const void* d_X, const void* d_Ws, const void* d_dms, int nset,
+                int nip, int nao, const int kmesh[3], const double a[9], void* d_vk);
+
+/* ---- building blocks exported for tests / other callers -------------------- */
+/* C[b] = alpha op(A[b]) op(B[b]) + beta C[b]; op: 0 N, 1 T, 2 conj, 3 conj-transpose */
+int fisdf_zgemm(fisdf_ctx* ctx, int opA, int opB, int M, int N, int K, const double alpha[2],
+                const void* d_A, long lda, long strideA, const void* d_B, long ldb, long strideB,
+                const double beta[2], void* d_C, long ldc, long strideC, int batch, int ksplit);
+/* C = alpha A A^H (A: n x K, lda; C: n x n, ldc), Hermitian: lower tiles + mirror */
+int fisdf_herk(fisdf_ctx* ctx, int n, int K, double alpha, const void* d_A, long lda, void* d_C,
+               long ldc, int ksplit);
+/* forward 3-D FFT (numpy fftn sign, unnormalised) of `rows` rows of n0*n1*n2 points */
+int fisdf_fft3d(fisdf_ctx* ctx, const void* d_in, void* d_out, int rows, const int mesh[3]);
+/* sqrt(coulG(k+G) * scale) (or without sqrt), PySCF get_coulG(exxdiv=None) restated */
+int fisdf_coulg(fisdf_ctx* ctx, const int mesh[3], const double a[9], const double k[3],
+                double scale, int take_sqrt, double* d_w);
+/* batched pivoted Cholesky (pivots + ranks to host; synchronous) */
+int fisdf_pivoted_cholesky(fisdf_ctx* ctx, const void* d_A, int n, int batch, int rmax,
+                           double tol_rel, int* h_piv /* batch*rmax */, int* h_rank /* batch */);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FISDF_H */

@@ -1,0 +1,40 @@
+"""Shared small cases for CPU and GPU tests (inputs are regenerated deterministically)."""
+import functools
+
+import numpy as np
+
+from fisdf import cell as C
+from oracle import isdf_ref as R
+
+
+CASES = {
+    # name: (cell factory, kmesh, m0, c0)
+    "toy222": (lambda: C.toy_cell(mesh=(12, 12, 12)), (2, 2, 2), (9, 9, 9), 40.0),
+    "toy331": (lambda: C.toy_cell(mesh=(15, 15, 15)), (3, 3, 1), (9, 9, 9), 40.0),
+    "diamond_szv_gamma": (lambda: C.diamond_cell(basis="gth-szv", mesh=(8, 8, 8)), (1, 1, 1),
+                          (15, 15, 15), 20.0),
+}
+
+
+@functools.lru_cache(maxsize=None)
+def inputs(name):
+    make, kmesh, m0, c0 = CASES[name]
+    cell = make()
+    x0 = C.eval_ao_kpts(cell, cell.gen_uniform_grids(m0), kmesh)
+    coords = cell.gen_uniform_grids(cell.mesh)
+    chi = C.eval_ao_kpts(cell, coords, kmesh)
+    dm = C.make_dm(cell.nao_nr(), kmesh, cell, seed=1234)[None]
+    return cell, kmesh, m0, c0, x0, coords, chi, dm
+
+
+@functools.lru_cache(maxsize=None)
+def oracle(name):
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
+    perm, rank, nip, x4sel = R.select_interpolation_points(x0, cell.nao_nr(), c0)
+    xip = x0[:, perm, :]
+    out = R.build(xip, chi, coords, cell.a, kmesh, cell.mesh)
+    kpts = R.get_kpts(cell.a, kmesh)
+    phase = R.get_phase(cell.a, kpts, kmesh)
+    vj = R.get_j_kpts(xip, out["w0"], dm)
+    vk = R.get_k_kpts(xip, out["wq"], dm, phase)
+    return dict(perm=perm, rank=rank, nip=nip, x4sel=x4sel, xip=xip, vj=vj, vk=vk, **out)
