@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-q", type=int, default=2, help="q-points timed in the CPU sample")
+    p.add_argument("--cpu-q", type=int, default=1, help="q-points timed in the CPU sample")
     return p.parse_args()
 
 

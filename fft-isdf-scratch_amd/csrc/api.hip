@@ -198,12 +198,9 @@ int fisdf_create(int device, void* stream, fisdf_ctx** out) {
   FISDF_HIP(hipSetDevice(device));
   fisdf_ctx* c = new fisdf_ctx();
   c->device = device;
-  if (stream) {
-    c->stream = (hipStream_t)stream;
-  } else {
-    FISDF_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    c->own_stream = true;
-  }
+  // NULL = the device's default (null) stream, which orders with torch's default stream
+  c->stream = (hipStream_t)stream;
+  c->own_stream = false;
   FISDF_HIP(hipMalloc(&c->maximag, 4 * sizeof(unsigned long long)));
   FISDF_HIP(hipMemsetAsync(c->maximag, 0, 4 * sizeof(unsigned long long), c->stream));
   *out = c;

@@ -22,7 +22,7 @@ import time
 
 import numpy as np
 
-from . import _lib
+from . import _lib, kshard
 from .cell import eval_ao_kpts, make_kpts
 
 log = logging.getLogger("fisdf")
@@ -76,10 +76,7 @@ class _Device:
 
     def shard(self, nk):
         """Contiguous q-range of this rank."""
-        base, rem = divmod(nk, self.size)
-        q0 = self.rank * base + min(self.rank, rem)
-        q1 = q0 + base + (1 if self.rank < rem else 0)
-        return q0, q1
+        return kshard.shard_range(nk, self.rank, self.size)
 
     def empty(self, shape, dtype="c128"):
         t = self.torch
@@ -303,12 +300,9 @@ def build(df_obj):
     Ws = d.empty((nk, nip, nip))
     d.ctx.call("fisdf_build_ws", _lib.ptr(Wq), q0, q1, nip, km_p, a_p, _lib.ptr(Ws))  # :204-207
     if d.size > 1:
-        import torch.distributed as dist
-        dist.all_reduce(Ws, group=d.comm)                                 # k-sum of W_s
+        kshard.allreduce_ws(Ws, d.comm)                                  # k-sum of W_s
         W0 = Wq[0].clone() if q0 == 0 else d.empty((nip, nip))
-        owner = 0  # rank holding q = 0
-        dist.broadcast(W0, src=dist.get_global_rank(d.comm, owner) if d.comm is not None else owner,
-                       group=d.comm)
+        kshard.broadcast_w0(W0, nk, d.comm)                               # W_0 for get_j
     else:
         W0 = Wq[0]
     df_obj._dev_state.update(x4=x4, Wq=Wq, W0=W0, Ws=Ws)

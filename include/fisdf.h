@@ -47,7 +47,7 @@ enum {
 
 /* ---- context / memory ---------------------------------------------------- */
 int fisdf_abi_version(void);
-int fisdf_create(int device, void* hip_stream /* NULL: own stream */, fisdf_ctx** out);
+int fisdf_create(int device, void* hip_stream /* NULL: default (null) stream */, fisdf_ctx** out);
 int fisdf_destroy(fisdf_ctx* ctx);
 const char* fisdf_last_error(void);
 int fisdf_sync(fisdf_ctx* ctx);

@@ -35,6 +35,7 @@ def oracle(name):
     out = R.build(xip, chi, coords, cell.a, kmesh, cell.mesh)
     kpts = R.get_kpts(cell.a, kmesh)
     phase = R.get_phase(cell.a, kpts, kmesh)
-    vj = R.get_j_kpts(xip, out["w0"], dm)
+    # fftisdf.py:169-170: vj.real when the k-points are all zero (Gamma-only runs)
+    vj = R.get_j_kpts(xip, out["w0"], dm, kpts_band_is_zero=bool(abs(kpts).max() < 1e-9))
     vk = R.get_k_kpts(xip, out["wq"], dm, phase)
     return dict(perm=perm, rank=rank, nip=nip, x4sel=x4sel, xip=xip, vj=vj, vk=vk, **out)

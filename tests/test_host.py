@@ -1,0 +1,135 @@
+"""CPU tests of the host side: the C-ABI library loads and exports every symbol the
+header declares, the product fails loudly without a GPU, the reference-mirror helpers,
+and the k-shard (multi-GPU) orchestration with a world_size-2 gloo group."""
+import os
+import re
+import socket
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fisdf.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(fisdf_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_header_symbols():
+    from fisdf import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libfisdf.so not built (run __graft_entry__.build())")
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    # and the ctypes signature table covers the whole header
+    assert set(syms) == set(_lib._SIGS), set(syms) ^ set(_lib._SIGS)
+    assert lib.fisdf_abi_version() == 1
+
+
+def test_no_cpu_fallback():
+    """Without a GPU the product path raises (never silently runs on the CPU)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from fisdf import ISDF, _lib, cell as C
+    if os.path.exists(_lib.LIB_PATH):
+        with pytest.raises(_lib.FisdfError):
+            _lib.Context(0)
+    cell = C.toy_cell(mesh=(6, 6, 6))
+    df = ISDF(cell, cell.get_kpts((1, 1, 2)))
+    with pytest.raises(_lib.FisdfError):
+        df.build()
+
+
+def test_reference_surface():
+    from fisdf import ISDF, cell as C
+    from fisdf.isdf import kpts_to_kmesh, _format_dms, _format_jks
+    cell = C.diamond_cell(mesh=(8, 8, 8))
+    kpts = cell.get_kpts((2, 3, 1))
+    assert list(kpts_to_kmesh(cell, kpts)) == [2, 3, 1]
+    df = ISDF(cell, kpts)                      # fftisdf.py:302-306 defaults
+    assert df.m0 == [15, 15, 15] and df.c0 == 20.0 and df.blksize == 8000
+    assert df._x is None and df._w0 is None and df._wq is None
+    dm = np.zeros((6, 8, 8))
+    assert _format_dms(dm, 6).shape == (1, 6, 8, 8)
+    assert _format_jks(np.zeros((1, 6, 8, 8)), dm).shape == dm.shape
+    blocks = list(df.aoR_loop(blksize=200))
+    assert blocks[0][1] == 0 and blocks[-1][2] == 512
+    assert blocks[0][0][0].shape == (6, 200, cell.nao_nr())
+    with pytest.raises(NotImplementedError):
+        df.get_jk(dm, omega=0.1)
+
+
+def test_shard_ranges():
+    from fisdf.kshard import shard_range, owner_of
+    for nk in (1, 7, 8, 64):
+        for size in (1, 2, 3, 8):
+            rs = [shard_range(nk, r, size) for r in range(size)]
+            assert rs[0][0] == 0 and rs[-1][1] == nk
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+            assert owner_of(0, nk, size) == 0
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, size, port, result):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "fft-isdf-scratch_amd"), os.path.join(ROOT, "tests")]
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    from cases import inputs, oracle
+    from fisdf import kshard
+    from oracle import isdf_ref as R
+    name = "toy222"
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
+    o = oracle(name)
+    nk = len(o["wq"])
+    kpts = R.get_kpts(cell.a, kmesh)
+    phase = R.get_phase(cell.a, kpts, kmesh)
+    q0, q1 = kshard.shard_range(nk, rank, size)
+    # this rank's W_q shard, recomputed per q exactly as a GPU rank would (fftisdf.py:97-121)
+    Gv = R.get_Gv(cell.a, cell.mesh)
+    wq_own = np.asarray([R.fit_and_coulomb(o["x4"][q], o["y"][q], kpts[q], coords, cell.a,
+                                           cell.mesh, cell.vol, Gv)[0] for q in range(q0, q1)])
+    ws = np.sqrt(nk) * (phase[:, q0:q1] @ wq_own.reshape(q1 - q0, -1)).real
+    Ws = torch.from_numpy(ws.astype(np.complex128))
+    kshard.allreduce_ws(Ws, None)
+    W0 = torch.from_numpy(wq_own[0].copy()) if q0 == 0 else torch.zeros(o["w0"].shape, dtype=torch.complex128)
+    kshard.broadcast_w0(W0, nk, None)
+    ws_full = np.sqrt(nk) * (phase @ o["wq"].reshape(nk, -1)).real
+    err_ws = abs(Ws.numpy().real - ws_full).max() / abs(ws_full).max()
+    err_w0 = abs(W0.numpy() - o["w0"]).max()
+    result.put((rank, err_ws, err_w0))
+    dist.destroy_process_group()
+
+
+def test_kshard_gloo_world2():
+    """N>1 path on CPU: per-rank q-shards + all-reduce(W_s) + broadcast(W_0) == unsharded."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, err_ws, err_w0 in res:
+        assert err_ws < 1e-12, (rank, err_ws)
+        assert err_w0 < 1e-12, (rank, err_w0)

@@ -1,0 +1,196 @@
+"""CPU tests: the oracle pinned by known-answer tests, the golden
+fixtures, and the host-side conventions.  No GPU needed."""
+import os
+
+import numpy as np
+import pytest
+import scipy.linalg
+
+from cases import inputs, oracle
+from fisdf import cell as C
+from oracle import exact_ref as E
+from oracle import isdf_ref as R
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_phase_is_kmesh_dft():
+    """K5 / SURVEY A1: Phi = exp(i T.k)/sqrt(nk) is unitary and equals sqrt(nk)*IDFT."""
+    cell = C.diamond_cell(mesh=(8, 8, 8))
+    kmesh = (3, 2, 4)
+    kpts = R.get_kpts(cell.a, kmesh)
+    phase = R.get_phase(cell.a, kpts, kmesh)
+    nk = len(kpts)
+    assert abs(phase.conj().T @ phase - np.eye(nk)).max() < 1e-13
+    x = np.random.default_rng(0).standard_normal((nk, 5)) + 0j
+    via_fft = np.fft.ifftn(x.reshape(*kmesh, 5), axes=(0, 1, 2)).reshape(nk, 5) * np.sqrt(nk)
+    assert abs(phase @ x - via_fft).max() < 1e-12
+    # the product's own phase (cell.get_phase) uses the same convention
+    assert abs(C.get_phase(cell, kmesh) - phase).max() < 1e-14
+
+
+def test_coulG_conventions():
+    cell = C.diamond_cell(mesh=(9, 9, 9))
+    g0 = R.get_coulG(cell.a, np.zeros(3), cell.mesh)
+    assert g0[0] == 0.0 and np.all(g0[1:] > 0)
+    Gv = R.get_Gv(cell.a, cell.mesh)
+    assert np.allclose(g0[1:], 4 * np.pi / np.einsum("gi,gi->g", Gv, Gv)[1:])
+    k = R.get_kpts(cell.a, (2, 2, 2))[5]
+    gk = R.get_coulG(cell.a, k, cell.mesh)
+    assert np.all(gk >= 0) and np.isfinite(gk).all()
+
+
+def test_pivoted_cholesky_api():
+    """T5 (test-chol.ipynb cell 1): returns (chol, perm, rank) with A[p][:,p] = R^T R."""
+    rng = np.random.default_rng(1)
+    B = rng.standard_normal((40, 25))
+    A = B @ B.T
+    chol, perm, rank = R.pivoted_cholesky(A)
+    assert rank == 25
+    Ap = A[np.ix_(perm, perm)]
+    assert abs(chol.T @ chol - Ap).max() < 1e-10 * abs(A).max()
+
+
+@pytest.mark.parametrize("name", ["toy222", "diamond_szv_gamma"])
+def test_oracle_jk_vs_exact_fft(name):
+    """K1 / SURVEY A2: ISDF J/K (restated reference) ~ exact FFT-grid J/K (fftisdf.py:441-473)."""
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
+    o = oracle(name)
+    kpts = R.get_kpts(cell.a, kmesh)
+    ej = E.exact_j(chi, dm, cell.a, cell.mesh)
+    ek = E.exact_k(chi, dm, cell.a, cell.mesh, kpts, coords)
+    dj = abs(o["vj"] - ej).max()
+    dk = abs(o["vk"] - ek).max()
+    print(name, "nip", o["nip"], "rank", o["rank"], "dJ", dj, "dK", dk)
+    # toy222 is converged in nip (ISDF error ~1e-9); C1 at nip=160 carries a real ISDF error
+    tol = 5e-8 if name == "toy222" else 1e-3
+    assert dj < tol and dk < tol
+
+
+def test_oracle_eri_identity_q_convention():
+    """K2 / SURVEY A5: (m k1, n k2 | k k3, l k4) = sum W_q X*X X*X with q = k2 - k1."""
+    name = "toy222"
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
+    o = oracle(name)
+    kpts = R.get_kpts(cell.a, kmesh)
+    nk = len(kpts)
+    ks = C.cartesian_prod([np.arange(n) for n in kmesh])
+
+    def kidx(v):
+        v = np.mod(v, kmesh)
+        return int((v[0] * kmesh[1] + v[1]) * kmesh[2] + v[2])
+
+    x = o["xip"]
+    worst = 0.0
+    for (k1, k2, k3) in [(0, 1, 2), (3, 5, 6), (7, 7, 1)]:
+        q = kidx(ks[k2] - ks[k1])
+        k4 = kidx(ks[k1] - ks[k2] + ks[k3])
+        eri = np.einsum("IJ,Im,In,Jk,Jl->mnkl", o["wq"][q], x[k1].conj(), x[k2], x[k3].conj(),
+                        x[k4], optimize=True)
+        ref = E.exact_eri(chi, cell.a, cell.mesh, kpts, coords, k1, k2, k3, k4)
+        worst = max(worst, abs(eri - ref).max())
+    assert worst < 1e-6   # reference harness fails above 1e-4 (fftdf-with-k-lstsq.py:238)
+
+
+def test_gamma_fit_kat():
+    """K3 (fftisdf-supercell-2.py:62-85): Gamma fit reproduces the pair densities."""
+    name = "diamond_szv_gamma"
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
+    o = oracle(name)
+    x = o["xip"][0]
+    f = chi[0]
+    x4 = o["x4"][0]
+    y = o["y"][0]
+    z = scipy.linalg.lstsq(x4, y.T, lapack_driver="gelsy")[0]
+    resid = abs(x4 @ z - y.T).max() / abs(y).max()
+    assert resid < 1e-8
+    # rho(g, m, n) = f_m f_n ~ sum_I z_I(g) x_Im x_In
+    rho = np.einsum("gm,gn->gmn", f, f)
+    fit = np.einsum("Ig,Im,In->gmn", z, x, x)
+    assert abs(rho - fit).max() / abs(rho).max() < 1e-5
+
+
+def test_reality_invariants():
+    """K4: x2_s, fx_s, rho_s are real (fftisdf.py:43,81,216) — asserted inside the oracle."""
+    o = oracle("toy222")
+    assert np.isfinite(o["vk"]).all()
+
+
+def test_golden_fixture():
+    """Oracle outputs match the committed golden vectors (tests/golden/make_golden.py)."""
+    path = os.path.join(GOLDEN, "toy222.npz")
+    g = np.load(path)
+    o = oracle("toy222")
+    assert np.array_equal(g["perm"], o["perm"])
+    assert abs(g["vj"] - o["vj"]).max() < 1e-10
+    assert abs(g["vk"] - o["vk"]).max() < 1e-10
+    assert abs(g["vj_exact"] - o["vj"]).max() < 5e-8
+    assert abs(g["vk_exact"] - o["vk"]).max() < 5e-8
+
+
+def test_fit_numerics_factored_cholesky():
+    """SURVEY A3 decision record: the GPU's fit (pivoted Cholesky of x4_q, tol 1e-14,
+    factored application + Parseval half-Gram) matches the gelsy oracle to < 1e-8 in J/K.
+    NumPy model of the exact GPU algorithm (same blocking nb=64)."""
+    name = "toy222"
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
+    o = oracle(name)
+    kpts = R.get_kpts(cell.a, kmesh)
+    phase = R.get_phase(cell.a, kpts, kmesh)
+    ngrid = coords.shape[0]
+    Gv = R.get_Gv(cell.a, cell.mesh)
+    wq = []
+    for q in range(len(kpts)):
+        P, L = _pchol(o["x4"][q], 1e-14)
+        n = o["x4"].shape[1]
+        fq = np.exp(-1j * coords @ kpts[q])
+        c = R.get_coulG(cell.a, kpts[q], cell.mesh, Gv) * cell.vol / ngrid ** 2
+        Yh = R.fft(o["y"][q].T[P] * fq, cell.mesh) * np.sqrt(c)
+        U = _blocked_trsm(L, Yh, 64)
+        G = U @ U.conj().T
+        T = scipy.linalg.solve_triangular(L.conj().T, G, lower=False)
+        Wpp = scipy.linalg.solve_triangular(L.conj().T, T.conj().T, lower=False).conj().T
+        W = np.zeros((n, n), complex)
+        W[np.ix_(P, P)] = Wpp
+        wq.append(W)
+    wq = np.asarray(wq)
+    vj = R.get_j_kpts(o["xip"], wq[0], dm)
+    vk = R.get_k_kpts(o["xip"], wq, dm, phase)
+    assert abs(vj - o["vj"]).max() < 1e-8
+    assert abs(vk - o["vk"]).max() < 1e-8
+
+
+def _pchol(A, tol):
+    n = A.shape[0]
+    L = np.zeros((n, n), complex)
+    d = A.diagonal().real.copy()
+    thr = tol * d.max()
+    piv = []
+    chosen = np.zeros(n, bool)
+    for j in range(n):
+        dd = np.where(chosen, -np.inf, d)
+        p = int(np.argmax(dd))
+        if not dd[p] > thr:
+            break
+        col = (A[:, p] - L[:, :j] @ L[p, :j].conj()) / np.sqrt(d[p])
+        col[chosen] = 0
+        col[p] = np.sqrt(d[p])
+        L[:, j] = col
+        d = d - abs(col) ** 2
+        chosen[p] = True
+        piv.append(p)
+    P = np.array(piv)
+    return P, L[P][:, :len(P)]
+
+
+def _blocked_trsm(L, B, nb):
+    r = L.shape[0]
+    X = np.zeros_like(B)
+    B = B.copy()
+    for b0 in range(0, r, nb):
+        b1 = min(b0 + nb, r)
+        if b0:
+            B[b0:b1] -= L[b0:b1, :b0] @ X[:b0]
+        Linv = scipy.linalg.solve_triangular(L[b0:b1, b0:b1], np.eye(b1 - b0), lower=True)
+        X[b0:b1] = Linv @ B[b0:b1]
+    return X
