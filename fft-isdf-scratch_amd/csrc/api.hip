@@ -36,6 +36,7 @@ struct fisdf_ctx {
   cplx* f_Lp = nullptr;     // (nk, nip*nip) pivot-order factor, ld = rank_q
   cplx* f_Linv = nullptr;   // (nk, nblk*nb*nb)
   int* f_piv = nullptr;     // (nk, nip)
+  int* f_rank_dev = nullptr;
   std::vector<int> f_rank;  // host copy
   // reality-invariant monitors
   unsigned long long* maximag = nullptr;  // 3 slots
@@ -167,8 +168,9 @@ int free_factors(fisdf_ctx* c) {
   if (c->f_Lp) FISDF_HIP(hipFree(c->f_Lp));
   if (c->f_Linv) FISDF_HIP(hipFree(c->f_Linv));
   if (c->f_piv) FISDF_HIP(hipFree(c->f_piv));
+  if (c->f_rank_dev) FISDF_HIP(hipFree(c->f_rank_dev));
   c->f_L = c->f_Lp = c->f_Linv = nullptr;
-  c->f_piv = nullptr;
+  c->f_piv = c->f_rank_dev = nullptr;
   c->f_rank.clear();
   c->f_nk = c->f_nip = 0;
   return 0;
@@ -522,13 +524,17 @@ int fisdf_factor_x4(fisdf_ctx* c, const void* x4v, int q0, int q1, int nip, doub
   FISDF_HIP(hipMemcpyAsync(c->f_rank.data(), b + oR, sizeof(int) * nk, hipMemcpyDeviceToHost,
                            c->stream));
   FISDF_HIP(hipStreamSynchronize(c->stream));
+  FISDF_HIP(hipMalloc(&c->f_rank_dev, sizeof(int) * nk));
+  FISDF_HIP(hipMemcpyAsync(c->f_rank_dev, b + oR, sizeof(int) * nk, hipMemcpyDeviceToDevice,
+                           c->stream));
+  // pivot-order factor padded to nip x nip (identity beyond the rank) so the small
+  // back-substitutions of all q can run as one batch
   for (int q = 0; q < nk; ++q) {
     const int r = c->f_rank[q];
     if (h_ranks) h_ranks[q] = r;
-    if (r == 0) continue;
     cplx* Lp = c->f_Lp + (long)q * nn;
-    FISDF_TRY(gather_lp(c->stream, c->f_L + (long)q * nn, nip, c->f_piv + (long)q * nip, r, r, Lp));
-    FISDF_TRY(trinv_blocks(c->stream, Lp, r, nb, c->f_Linv + (long)q * nblk * nb * nb));
+    FISDF_TRY(gather_lp(c->stream, c->f_L + (long)q * nn, nip, c->f_piv + (long)q * nip, r, nip, Lp));
+    FISDF_TRY(trinv_blocks(c->stream, Lp, nip, nip, nb, c->f_Linv + (long)q * nblk * nb * nb));
   }
   return 0;
 }
@@ -550,16 +556,19 @@ int fisdf_fit_coulomb(fisdf_ctx* c, int q0, int q1, const void* yTv, int nip, co
   const double vol = cell_volume(a);
   const cplx* yT = (const cplx*)yTv;
   cplx* Wq = (cplx*)Wqv;
+  const int nq = q1 - q0;
   int rmax = 0;
   for (int q = q0; q < q1; ++q) rmax = std::max(rmax, c->f_rank[q - q0]);
   const int ks = pick_ksplit(rmax, rmax, (int)ngrid);
+  const long rr = (long)rmax * rmax;
+  const long sLi = (long)nblk * nb * nb;
   Carver cv;
   size_t oY = cv.take(sizeof(cplx) * rmax * ngrid);
   size_t oU = cv.take(sizeof(cplx) * rmax * ngrid);
   size_t oWt = cv.take(sizeof(double) * ngrid);
-  size_t oG = cv.take(sizeof(cplx) * nn);
-  size_t oT = cv.take(sizeof(cplx) * nn);
-  size_t oS = cv.take(sizeof(cplx) * nn);
+  size_t oG = cv.take(sizeof(cplx) * nq * rr);
+  size_t oT = cv.take(sizeof(cplx) * nq * rr);
+  size_t oS = cv.take(sizeof(cplx) * nq * rr);
   size_t oK = cv.take(sizeof(cplx) * (size_t)ks * rmax * rmax);
   void* base;
   FISDF_TRY(arena_get(c, cv.off, &base));
@@ -567,21 +576,22 @@ int fisdf_fit_coulomb(fisdf_ctx* c, int q0, int q1, const void* yTv, int nip, co
   cplx* Yh = (cplx*)(b + oY);
   cplx* U = (cplx*)(b + oU);
   double* wt = (double*)(b + oWt);
-  cplx* G = (cplx*)(b + oG);
+  cplx* G = (cplx*)(b + oG);   // (nq, rmax, rmax): G_q in the leading r_q x r_q block, zero elsewhere
   cplx* T = (cplx*)(b + oT);
   cplx* S = (cplx*)(b + oS);
   cplx* kw = (cplx*)(b + oK);
+  if (rmax == 0) {
+    FISDF_HIP(hipMemsetAsync(Wq, 0, sizeof(cplx) * nq * nn, c->stream));
+    return 0;
+  }
+  FISDF_HIP(hipMemsetAsync(G, 0, sizeof(cplx) * nq * rr, c->stream));
   for (int q = q0; q < q1; ++q) {
     const int lq = q - q0;
     const int r = c->f_rank[lq];
-    cplx* Wout = Wq + (long)lq * nn;
-    if (r == 0) {
-      FISDF_HIP(hipMemsetAsync(Wout, 0, sizeof(cplx) * nn, c->stream));
-      continue;
-    }
+    if (r == 0) continue;
     const int* piv = c->f_piv + (long)lq * nip;
     const cplx* Lp = c->f_Lp + (long)lq * nn;
-    const cplx* Linv = c->f_Linv + (long)lq * nblk * nb * nb;
+    const cplx* Linv = c->f_Linv + (long)lq * sLi;
     double kq[3], kd[3];
     kpoint(kmesh, g, q, kq);
     for (int i = 0; i < 3; ++i) kd[i] = g.a[i][0] * kq[0] + g.a[i][1] * kq[1] + g.a[i][2] * kq[2];
@@ -596,22 +606,26 @@ int fisdf_fit_coulomb(fisdf_ctx* c, int q0, int q1, const void* yTv, int nip, co
     {
       StageTimer tm(c, FISDF_ST_TRSM);
       // U = L^{-1} Yh   (fit, factored order; (x4_q)_PP = L L^H)
-      FISDF_TRY(trsm_blocked(c->stream, 1, Lp, r, Linv, nb, Yh, ngrid, U, ngrid, (int)ngrid));
+      FISDF_TRY(trsm_blocked(c->stream, 1, Lp, nip, 0, r, Linv, 0, nb, Yh, ngrid, 0, U, ngrid, 0,
+                             (int)ngrid, 1));
     }
     {
       StageTimer tm(c, FISDF_ST_HERK);
       // G = U U^H  (:121 by Parseval)
-      FISDF_TRY(herk(c->stream, r, (int)ngrid, 1.0, U, ngrid, G, r, ks, kw));
+      FISDF_TRY(herk(c->stream, r, (int)ngrid, 1.0, U, ngrid, G + lq * rr, rmax, ks, kw));
     }
-    {
-      StageTimer tm(c, FISDF_ST_SMALL);
-      // W_PP = L^{-H} G L^{-1}:  T = L^{-H} G ; S = L^{-H} T^H ; W_PP = S^H
-      FISDF_TRY(trsm_blocked(c->stream, 0, Lp, r, Linv, nb, G, r, T, r, r));
-      FISDF_TRY(conj_transpose(c->stream, T, r, G));
-      FISDF_TRY(trsm_blocked(c->stream, 0, Lp, r, Linv, nb, G, r, S, r, r));
-      FISDF_TRY(conj_transpose(c->stream, S, r, T));
-      FISDF_TRY(scatter_w(c->stream, T, r, piv, Wout, nip));
-    }
+  }
+  {
+    StageTimer tm(c, FISDF_ST_SMALL);
+    // W_PP = L^{-H} G L^{-1} for all q of the shard at once (L padded with identity, G with
+    // zeros beyond each rank):  T = L^{-H} G ; S = L^{-H} T^H ; W_PP = S^H ; scatter by pivots
+    FISDF_TRY(trsm_blocked(c->stream, 0, c->f_Lp, nip, nn, rmax, c->f_Linv, sLi, nb, G, rmax, rr,
+                           T, rmax, rr, rmax, nq));
+    FISDF_TRY(conj_transpose(c->stream, T, rmax, rr, G, nq));
+    FISDF_TRY(trsm_blocked(c->stream, 0, c->f_Lp, nip, nn, rmax, c->f_Linv, sLi, nb, G, rmax, rr,
+                           S, rmax, rr, rmax, nq));
+    FISDF_TRY(conj_transpose(c->stream, S, rmax, rr, T, nq));
+    FISDF_TRY(scatter_w(c->stream, T, rmax, rr, rmax, c->f_piv, c->f_rank_dev, Wq, nip, nq));
   }
   return 0;
 }

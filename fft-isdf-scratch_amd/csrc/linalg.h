@@ -9,11 +9,13 @@ struct CellGeom {
 };
 
 int gather_lp(hipStream_t s, const cplx* L, int rmax, const int* piv, int r, int rpad, cplx* Lp);
-int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int nb, cplx* Linv);
-int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, int r, const cplx* Linv, int nb,
-                 cplx* B, long ldb, cplx* X, long ldx, int ncol);
-int scatter_w(hipStream_t s, const cplx* Wpp, int r, const int* piv, cplx* W, int nip);
-int conj_transpose(hipStream_t s, const cplx* A, int n, cplx* B);
+int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int ldl, int nb, cplx* Linv);
+int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, long ldl, long sL, int r,
+                 const cplx* Linv, long sLi, int nb, cplx* B, long ldb, long sB, cplx* X, long ldx,
+                 long sX, int ncol, int batch);
+int scatter_w(hipStream_t s, const cplx* Wpp, int ldw, long sW, int rmax, const int* piv,
+              const int* rank, cplx* W, int nip, int batch);
+int conj_transpose(hipStream_t s, const cplx* A, int n, long sA, cplx* B, int batch);
 int coulg_weight(hipStream_t s, const int mesh[3], const CellGeom& g, const double k[3],
                  double scale, int take_sqrt, double* w);
 int square_real(hipStream_t s, const cplx* in, cplx* out, long n, unsigned long long* maximag);

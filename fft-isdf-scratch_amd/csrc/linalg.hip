@@ -25,9 +25,9 @@ __global__ void gather_lp_kernel(const cplx* __restrict__ L, int rmax, const int
   Lp[e] = v;
 }
 
-// inverse of each nb x nb lower-triangular diagonal block of Lp (r x r, ld = r)
+// inverse of each nb x nb lower-triangular diagonal block of Lp (r x r, ld = ldl)
 __global__ __launch_bounds__(64) void trinv_blocks_kernel(const cplx* __restrict__ Lp, int r,
-                                                          int nb, cplx* __restrict__ Linv) {
+                                                          int ldl, int nb, cplx* __restrict__ Linv) {
   __shared__ cplx Ls[64][65];
   __shared__ cplx Xs[64][65];
   const int blk = blockIdx.x;
@@ -35,7 +35,7 @@ __global__ __launch_bounds__(64) void trinv_blocks_kernel(const cplx* __restrict
   const int m = min(nb, r - b0);
   const int j = threadIdx.x;
   for (int i = 0; i < m; ++i)
-    if (j < m) Ls[i][j] = Lp[(long)(b0 + i) * r + b0 + j];
+    if (j < m) Ls[i][j] = Lp[(long)(b0 + i) * ldl + b0 + j];
   __syncthreads();
   if (j < m) {
     for (int i = 0; i < m; ++i) {
@@ -53,20 +53,26 @@ __global__ __launch_bounds__(64) void trinv_blocks_kernel(const cplx* __restrict
     if (j < nb) out[i * nb + j] = (i < m && j < m) ? Xs[i][j] : cmk(i == j ? 1.0 : 0.0, 0.0);
 }
 
-// W[piv[s]][piv[t]] = Wpp[s][t]   (W zeroed beforehand)
-__global__ void scatter_w_kernel(const cplx* __restrict__ Wpp, int r, const int* __restrict__ piv,
+// W[b][piv[b][s]][piv[b][t]] = Wpp[b][s][t] for s,t < rank[b]   (W zeroed beforehand)
+__global__ void scatter_w_kernel(const cplx* __restrict__ Wpp, int ldw, long sW,
+                                 const int* __restrict__ piv, const int* __restrict__ rank,
                                  cplx* __restrict__ W, int nip) {
+  const int b = blockIdx.y;
+  const int r = rank[b];
   long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (e >= (long)r * r) return;
   int s = (int)(e / r), t = (int)(e % r);
-  W[(long)piv[s] * nip + piv[t]] = Wpp[e];
+  const int* p = piv + (long)b * nip;
+  W[(long)b * nip * nip + (long)p[s] * nip + p[t]] = Wpp[b * sW + (long)s * ldw + t];
 }
 
-__global__ void conj_transpose_kernel(const cplx* __restrict__ A, int n, cplx* __restrict__ B) {
+__global__ void conj_transpose_kernel(const cplx* __restrict__ A, int n, long sA,
+                                      cplx* __restrict__ B) {
+  const int b = blockIdx.y;
   long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (e >= (long)n * n) return;
   int i = (int)(e / n), j = (int)(e % n);
-  B[(long)j * n + i] = cconj(A[e]);
+  B[b * sA + (long)j * n + i] = cconj(A[b * sA + e]);
 }
 
 // sqrt(coulG(k+G) * scale); PySCF get_coulG (exxdiv=None, wrap_around=True) restated
@@ -235,19 +241,22 @@ int gather_lp(hipStream_t s, const cplx* L, int rmax, const int* piv, int r, int
   return 0;
 }
 
-int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int nb, cplx* Linv) {
+int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int ldl, int nb, cplx* Linv) {
   FISDF_CHECK(nb >= 1 && nb <= 64, "trinv_blocks: nb must be <= 64");
   int nblk = (r + nb - 1) / nb;
   if (nblk == 0) return 0;
-  hipLaunchKernelGGL(trinv_blocks_kernel, dim3(nblk), dim3(64), 0, s, Lp, r, nb, Linv);
+  hipLaunchKernelGGL(trinv_blocks_kernel, dim3(nblk), dim3(64), 0, s, Lp, r, ldl, nb, Linv);
   FISDF_HIP(hipGetLastError());
   return 0;
 }
 
 // X = L^{-1} B  (lower=1) or X = L^{-H} B (lower=0, backward with L^H); B is overwritten.
-// L: r x r lower (ld = r); Linv: diagonal-block inverses; B, X: r x ncol (ld given).
-int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, int r, const cplx* Linv, int nb,
-                 cplx* B, long ldb, cplx* X, long ldx, int ncol) {
+// L: r x r lower (ld = ldl, batch stride sL); Linv: diagonal-block inverses (batch stride
+// sLi); B, X: r x ncol (ld, batch strides given).  Blocked: one ZGEMM update + one
+// ZGEMM with the block inverse per 64-row block (factored order, never an explicit inverse).
+int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, long ldl, long sL, int r,
+                 const cplx* Linv, long sLi, int nb, cplx* B, long ldb, long sB, cplx* X, long ldx,
+                 long sX, int ncol, int batch) {
   const cplx one = cmk(1, 0), mone = cmk(-1, 0), zero = cmk(0, 0);
   int nblk = (r + nb - 1) / nb;
   for (int bi = 0; bi < nblk; ++bi) {
@@ -255,36 +264,37 @@ int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, int r, const cplx* Li
     int b0 = blk * nb, b1 = std::min(r, b0 + nb), m = b1 - b0;
     if (lower) {
       if (b0 > 0)  // B_b -= L[b, :b] X[:b]
-        FISDF_TRY(zgemm(s, OP_N, OP_N, m, ncol, b0, mone, Lp + (long)b0 * r, r, 0, X, ldx, 0,
-                        one, B + (long)b0 * ldb, ldb, 0, 1));
-      FISDF_TRY(zgemm(s, OP_N, OP_N, m, ncol, m, one, Linv + (long)blk * nb * nb, nb, 0,
-                      B + (long)b0 * ldb, ldb, 0, zero, X + (long)b0 * ldx, ldx, 0, 1));
+        FISDF_TRY(zgemm(s, OP_N, OP_N, m, ncol, b0, mone, Lp + (long)b0 * ldl, ldl, sL, X, ldx,
+                        sX, one, B + (long)b0 * ldb, ldb, sB, batch));
+      FISDF_TRY(zgemm(s, OP_N, OP_N, m, ncol, m, one, Linv + (long)blk * nb * nb, nb, sLi,
+                      B + (long)b0 * ldb, ldb, sB, zero, X + (long)b0 * ldx, ldx, sX, batch));
     } else {
       if (b1 < r)  // B_b -= (L^H)[b, >b] X[>b] = conj(L[>b, b])^T X[>b]
-        FISDF_TRY(zgemm(s, OP_C, OP_N, m, ncol, r - b1, mone, Lp + (long)b1 * r + b0, r, 0,
-                        X + (long)b1 * ldx, ldx, 0, one, B + (long)b0 * ldb, ldb, 0, 1));
-      FISDF_TRY(zgemm(s, OP_C, OP_N, m, ncol, m, one, Linv + (long)blk * nb * nb, nb, 0,
-                      B + (long)b0 * ldb, ldb, 0, zero, X + (long)b0 * ldx, ldx, 0, 1));
+        FISDF_TRY(zgemm(s, OP_C, OP_N, m, ncol, r - b1, mone, Lp + (long)b1 * ldl + b0, ldl, sL,
+                        X + (long)b1 * ldx, ldx, sX, one, B + (long)b0 * ldb, ldb, sB, batch));
+      FISDF_TRY(zgemm(s, OP_C, OP_N, m, ncol, m, one, Linv + (long)blk * nb * nb, nb, sLi,
+                      B + (long)b0 * ldb, ldb, sB, zero, X + (long)b0 * ldx, ldx, sX, batch));
     }
   }
   return 0;
 }
 
-int scatter_w(hipStream_t s, const cplx* Wpp, int r, const int* piv, cplx* W, int nip) {
-  FISDF_HIP(hipMemsetAsync(W, 0, sizeof(cplx) * (size_t)nip * nip, s));
-  long n = (long)r * r;
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(scatter_w_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, Wpp, r,
-                     piv, W, nip);
+int scatter_w(hipStream_t s, const cplx* Wpp, int ldw, long sW, int rmax, const int* piv,
+              const int* rank, cplx* W, int nip, int batch) {
+  FISDF_HIP(hipMemsetAsync(W, 0, sizeof(cplx) * (size_t)nip * nip * batch, s));
+  long n = (long)rmax * rmax;
+  if (n == 0 || batch == 0) return 0;
+  hipLaunchKernelGGL(scatter_w_kernel, dim3(nblocks(n, 256, 1L << 30), batch), dim3(256), 0, s,
+                     Wpp, ldw, sW, piv, rank, W, nip);
   FISDF_HIP(hipGetLastError());
   return 0;
 }
 
-int conj_transpose(hipStream_t s, const cplx* A, int n, cplx* B) {
+int conj_transpose(hipStream_t s, const cplx* A, int n, long sA, cplx* B, int batch) {
   long e = (long)n * n;
-  if (e == 0) return 0;
-  hipLaunchKernelGGL(conj_transpose_kernel, dim3(nblocks(e, 256, 1L << 30)), dim3(256), 0, s, A,
-                     n, B);
+  if (e == 0 || batch == 0) return 0;
+  hipLaunchKernelGGL(conj_transpose_kernel, dim3(nblocks(e, 256, 1L << 30), batch), dim3(256), 0,
+                     s, A, n, sA, B);
   FISDF_HIP(hipGetLastError());
   return 0;
 }
