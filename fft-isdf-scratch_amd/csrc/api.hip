@@ -478,13 +478,11 @@ int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk
     // fx_k^T = X_k f_k^H  -> FX[k][I][g]   (:76, transposed layout)
     FISDF_TRY(zgemm(c->stream, OP_N, OP_C, nip, m, nao, ONE, X, nao, (long)nip * nao,
                     f + (long)s0 * nao, nao, f_kstride, ZERO, FX, m, nm, nk));
-    // fx_s = Phi fx_k  (:79), real (:81)
+    // fx_s = Phi fx_k (:79), real (:81, monitored), y_s = fx_s^2 (:83) fused in the epilogue
     FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nm, nk, ONE, phase, nk, 0, FX, nm, 0, ZERO, FS, nm,
-                    0, 1));
-    // y_s = fx_s^2 (:83)
-    FISDF_TRY(square_real(c->stream, FS, FX, (long)nk * nm, c->maximag + 1));
+                    0, 1, 1, nullptr, EPI_SQUARE_RE, c->maximag + 1));
     // y_k = Phi^T y_s (:84) for the shard's k rows, scattered into yT[k-q0][I][g0+s0+g] (:85)
-    FISDF_TRY(zgemm(c->stream, OP_T, OP_N, q1 - q0, m, nk, ONE, phase + q0, nk, 0, FX, nm, m,
+    FISDF_TRY(zgemm(c->stream, OP_T, OP_N, q1 - q0, m, nk, ONE, phase + q0, nk, 0, FS, nm, m,
                     ZERO, yT + g0 + s0, (long)nip * ngrid, ngrid, nip));
   }
   return 0;
@@ -529,13 +527,11 @@ int fisdf_factor_x4(fisdf_ctx* c, const void* x4v, int q0, int q1, int nip, doub
                            c->stream));
   // pivot-order factor padded to nip x nip (identity beyond the rank) so the small
   // back-substitutions of all q can run as one batch
-  for (int q = 0; q < nk; ++q) {
-    const int r = c->f_rank[q];
-    if (h_ranks) h_ranks[q] = r;
-    cplx* Lp = c->f_Lp + (long)q * nn;
-    FISDF_TRY(gather_lp(c->stream, c->f_L + (long)q * nn, nip, c->f_piv + (long)q * nip, r, nip, Lp));
-    FISDF_TRY(trinv_blocks(c->stream, Lp, nip, nip, nb, c->f_Linv + (long)q * nblk * nb * nb));
-  }
+  for (int q = 0; q < nk; ++q)
+    if (h_ranks) h_ranks[q] = c->f_rank[q];
+  FISDF_TRY(gather_lp(c->stream, c->f_L, nip, nip, c->f_piv, c->f_rank_dev, nip, c->f_Lp, nk));
+  FISDF_TRY(trinv_blocks(c->stream, c->f_Lp, nip, nip, nn, nb, (long)nblk * nb * nb, c->f_Linv,
+                         nk));
   return 0;
 }
 

@@ -52,9 +52,12 @@ enum Op { OP_N = 0, OP_T = 1, OP_R = 2 /*conj only*/, OP_C = 3 /*conj-transpose*
 // ---- kernels (launchers return 0 or negative; all asynchronous on `stream`)
 // C[b] = alpha * op(A[b]) * op(B[b]) + beta * C[b]; lda/ldb/ldc in complex elements,
 // strides sA/sB/sC per batch in complex elements. ksplit>1 uses `work` (ksplit*M*N cplx).
+// epilogues: EPI_SQUARE_RE writes Re(alpha*acc)^2 + 0i and records max|Im| into *mon
+enum Epi { EPI_NONE = 0, EPI_SQUARE_RE = 1 };
 int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha,
           const cplx* A, long lda, long sA, const cplx* B, long ldb, long sB, cplx beta,
-          cplx* C, long ldc, long sC, int batch, int ksplit = 1, cplx* work = nullptr);
+          cplx* C, long ldc, long sC, int batch, int ksplit = 1, cplx* work = nullptr,
+          int epi = EPI_NONE, unsigned long long* mon = nullptr);
 
 // C = alpha A A^H (Hermitian rank-K update; lower tiles computed, upper mirrored)
 int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cplx* C, long ldc,

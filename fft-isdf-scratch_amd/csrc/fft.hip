@@ -62,10 +62,11 @@ __device__ __forceinline__ void dft_small(cplx* v, const cplx* __restrict__ tw, 
   }
 }
 
+// one Stockham radix-R stage over TL lines held in LDS; element p of line l at p*ps + l*ls
 template <int R>
 __device__ __forceinline__ void stockham_stage(const cplx* __restrict__ src, cplx* __restrict__ dst,
                                                const cplx* __restrict__ tw, int n, int Ns, int TL,
-                                               int tid, int nthr) {
+                                               int ps, int ls, int tid, int nthr) {
   const int nb = n / R;
   const int total = nb * TL;
   const int twstep = n / (Ns * R);
@@ -73,7 +74,7 @@ __device__ __forceinline__ void stockham_stage(const cplx* __restrict__ src, cpl
     const int l = bf % TL, j = bf / TL;
     cplx v[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[r] = src[(j + r * nb) * TL + l];
+    for (int r = 0; r < R; ++r) v[r] = src[(j + r * nb) * ps + l * ls];
     const int k = j % Ns;
     if (Ns > 1) {
 #pragma unroll
@@ -82,8 +83,35 @@ __device__ __forceinline__ void stockham_stage(const cplx* __restrict__ src, cpl
     dft_small<R>(v, tw, n);
     const int idx = (j / Ns) * Ns * R + k;
 #pragma unroll
-    for (int r = 0; r < R; ++r) dst[(idx + r * Ns) * TL + l] = v[r];
+    for (int r = 0; r < R; ++r) dst[(idx + r * Ns) * ps + l * ls] = v[r];
   }
+}
+
+// full line FFT of TL lines (all stages), ping-pong a <-> b; returns the buffer holding the result.
+// BIG instantiates the generic radix 7/11/13 butterflies (register-hungry: only for meshes
+// that need them, so the common 2/3/4/5 meshes keep occupancy).
+template <bool BIG>
+__device__ cplx* lds_fft_lines(cplx* a, cplx* b, const cplx* tw, int n, const int* radix, int nst,
+                               int TL, int ps, int ls, int tid, int nthr) {
+  int Ns = 1;
+  for (int s = 0; s < nst; ++s) {
+    const int R = radix[s];
+    switch (R) {
+      case 2: stockham_stage<2>(a, b, tw, n, Ns, TL, ps, ls, tid, nthr); break;
+      case 3: stockham_stage<3>(a, b, tw, n, Ns, TL, ps, ls, tid, nthr); break;
+      case 4: stockham_stage<4>(a, b, tw, n, Ns, TL, ps, ls, tid, nthr); break;
+      case 5: stockham_stage<5>(a, b, tw, n, Ns, TL, ps, ls, tid, nthr); break;
+      case 7: if constexpr (BIG) stockham_stage<7>(a, b, tw, n, Ns, TL, ps, ls, tid, nthr); break;
+      case 11: if constexpr (BIG) stockham_stage<11>(a, b, tw, n, Ns, TL, ps, ls, tid, nthr); break;
+      case 13: if constexpr (BIG) stockham_stage<13>(a, b, tw, n, Ns, TL, ps, ls, tid, nthr); break;
+    }
+    Ns *= R;
+    __syncthreads();
+    cplx* t = a;
+    a = b;
+    b = t;
+  }
+  return a;
 }
 
 __device__ __forceinline__ double fftfreq(int i, int n) {
@@ -92,6 +120,7 @@ __device__ __forceinline__ double fftfreq(int i, int n) {
 
 // axis pass. contiguous=1: lines are `n` contiguous elements (axis 2); tiles = TL consecutive lines.
 // contiguous=0: element p of line (o, ii) at o*n*inner + p*inner + ii; tile = TL consecutive ii.
+template <bool BIG>
 __global__ __launch_bounds__(256) void fft_axis_kernel(
     const cplx* __restrict__ in, long in_ld, const int* __restrict__ rowidx, cplx* out, long out_ld,
     int rows, int n, int inner, int outer, int TL, int contiguous, Stages st,
@@ -150,24 +179,7 @@ __global__ __launch_bounds__(256) void fft_axis_kernel(
     buf0[p * TL + l] = v;
   }
   __syncthreads();
-  cplx* a = buf0;
-  cplx* b = buf1;
-  int Ns = 1;
-  for (int s = 0; s < st.nst; ++s) {
-    int R = st.radix[s];
-    switch (R) {
-      case 2: stockham_stage<2>(a, b, tw, n, Ns, TL, tid, nthr); break;
-      case 3: stockham_stage<3>(a, b, tw, n, Ns, TL, tid, nthr); break;
-      case 4: stockham_stage<4>(a, b, tw, n, Ns, TL, tid, nthr); break;
-      case 5: stockham_stage<5>(a, b, tw, n, Ns, TL, tid, nthr); break;
-      case 7: stockham_stage<7>(a, b, tw, n, Ns, TL, tid, nthr); break;
-      case 11: stockham_stage<11>(a, b, tw, n, Ns, TL, tid, nthr); break;
-      case 13: stockham_stage<13>(a, b, tw, n, Ns, TL, tid, nthr); break;
-    }
-    Ns *= R;
-    __syncthreads();
-    cplx* t = a; a = b; b = t;
-  }
+  cplx* a = lds_fft_lines<BIG>(buf0, buf1, tw, n, st.radix, st.nst, TL, TL, 1, tid, nthr);
   for (int e = tid; e < tot; e += nthr) {
     int l, p;
     if (contiguous) { l = e / n; p = e % n; } else { l = e % TL; p = e / TL; }
@@ -178,6 +190,53 @@ __global__ __launch_bounds__(256) void fft_axis_kernel(
       dstp[g] = v;
     }
   }
+}
+
+// 2-D FFT of one (i1, i2) plane (n1*n2 contiguous points) per workgroup: axes 2 and 1 in
+// LDS, one HBM round trip instead of two.  Fuses the row gather and exp(-i k.r).
+template <bool BIG>
+__global__ __launch_bounds__(256) void fft_plane_kernel(
+    const cplx* __restrict__ in, long in_ld, const int* __restrict__ rowidx, cplx* out, long out_ld,
+    int rows, Stages st1, Stages st2, const cplx* __restrict__ tw1g, const cplx* __restrict__ tw2g,
+    int n0, int n1, int n2, double kd0, double kd1, double kd2, int use_phase) {
+  extern __shared__ cplx smem[];
+  cplx* tw1 = smem;
+  cplx* tw2 = smem + MAXN;
+  const int P = n1 * n2;
+  cplx* buf0 = smem + 2 * MAXN;
+  cplx* buf1 = buf0 + P;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  for (int t = tid; t < n1; t += nthr) tw1[t] = tw1g[t];
+  for (int t = tid; t < n2; t += nthr) tw2[t] = tw2g[t];
+  const int row = blockIdx.x / n0, i0 = blockIdx.x % n0;
+  if (row >= rows) return;
+  const cplx* src = in + (long)(rowidx ? rowidx[row] : row) * in_ld + (long)i0 * P;
+  cplx* dstp = out + (long)row * out_ld + (long)i0 * P;
+  const double f0 = fftfreq(i0, n0) * kd0;
+  for (int e = tid; e < P; e += nthr) {
+    cplx v = src[e];
+    if (use_phase) {
+      const int i1 = e / n2, i2 = e % n2;
+      double th = -(f0 + fftfreq(i1, n1) * kd1 + fftfreq(i2, n2) * kd2);
+      double s, c;
+      sincos(th, &s, &c);
+      v = cmul(v, cmk(c, s));
+    }
+    buf0[e] = v;
+  }
+  __syncthreads();
+  // axis 2: n1 lines of n2 contiguous points (p stride 1, line stride n2)
+  cplx* a = lds_fft_lines<BIG>(buf0, buf1, tw2, n2, st2.radix, st2.nst, n1, 1, n2, tid, nthr);
+  cplx* b = a == buf0 ? buf1 : buf0;
+  // axis 1: n2 lines of n1 points (p stride n2, line stride 1)
+  a = lds_fft_lines<BIG>(a, b, tw1, n1, st1.radix, st1.nst, n2, n2, 1, tid, nthr);
+  for (int e = tid; e < P; e += nthr) dstp[e] = a[e];
+}
+
+bool needs_big(const Stages& st) {
+  for (int i = 0; i < st.nst; ++i)
+    if (st.radix[i] > 5) return true;
+  return false;
 }
 
 bool factorize(int n, Stages& st) {
@@ -261,9 +320,14 @@ int axis_pass(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx
   double k0 = 0, k1 = 0, k2 = 0;
   int use_phase = kd != nullptr;
   if (kd) { k0 = kd[0]; k1 = kd[1]; k2 = kd[2]; }
-  hipLaunchKernelGGL(fft_axis_kernel, dim3((unsigned)tiles), dim3(256), lds, s, in, in_ld, rowidx,
-                     out, out_ld, rows, n, inner, outer, TL, contiguous, st, tw, n0, n1, n2, k0, k1,
-                     k2, use_phase, weight);
+  if (needs_big(st))
+    hipLaunchKernelGGL(fft_axis_kernel<true>, dim3((unsigned)tiles), dim3(256), lds, s, in, in_ld,
+                       rowidx, out, out_ld, rows, n, inner, outer, TL, contiguous, st, tw, n0, n1,
+                       n2, k0, k1, k2, use_phase, weight);
+  else
+    hipLaunchKernelGGL(fft_axis_kernel<false>, dim3((unsigned)tiles), dim3(256), lds, s, in, in_ld,
+                       rowidx, out, out_ld, rows, n, inner, outer, TL, contiguous, st, tw, n0, n1,
+                       n2, k0, k1, k2, use_phase, weight);
   FISDF_HIP(hipGetLastError());
   return 0;
 }
@@ -274,8 +338,32 @@ int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* ou
           int rows, int n0, int n1, int n2, const double* kd, const double* weight, cplx* /*work*/) {
   if (rows == 0) return 0;
   FISDF_CHECK(in != out || rowidx == nullptr, "fft: in-place pass cannot gather rows");
-  FISDF_TRY(axis_pass(s, in, in_ld, rowidx, out, out_ld, rows, 2, n0, n1, n2, kd, nullptr));
-  FISDF_TRY(axis_pass(s, out, out_ld, nullptr, out, out_ld, rows, 1, n0, n1, n2, nullptr, nullptr));
+  const size_t plane_lds = sizeof(cplx) * (2 * MAXN + 2 * (size_t)n1 * n2);
+  if (plane_lds <= 96 * 1024) {
+    // axes 2+1 fused per (i1,i2) plane, then axis 0 with the Coulomb weight: 2 HBM passes
+    Stages st1, st2;
+    FISDF_CHECK(n1 <= MAXN && n2 <= MAXN && factorize(n1, st1) && factorize(n2, st2),
+                "fft: mesh dimension must be <= 64 and factor into 2,3,5,7,11,13");
+    const cplx *tw1 = nullptr, *tw2 = nullptr;
+    FISDF_TRY(get_twiddles(n1, &tw1));
+    FISDF_TRY(get_twiddles(n2, &tw2));
+    const long planes = (long)rows * n0;
+    FISDF_CHECK(planes < (1L << 31), "fft: too many planes");
+    double k0 = 0, k1 = 0, k2 = 0;
+    if (kd) { k0 = kd[0]; k1 = kd[1]; k2 = kd[2]; }
+    if (needs_big(st1) || needs_big(st2))
+      hipLaunchKernelGGL(fft_plane_kernel<true>, dim3((unsigned)planes), dim3(256), plane_lds, s,
+                         in, in_ld, rowidx, out, out_ld, rows, st1, st2, tw1, tw2, n0, n1, n2, k0,
+                         k1, k2, kd != nullptr ? 1 : 0);
+    else
+      hipLaunchKernelGGL(fft_plane_kernel<false>, dim3((unsigned)planes), dim3(256), plane_lds, s,
+                         in, in_ld, rowidx, out, out_ld, rows, st1, st2, tw1, tw2, n0, n1, n2, k0,
+                         k1, k2, kd != nullptr ? 1 : 0);
+    FISDF_HIP(hipGetLastError());
+  } else {
+    FISDF_TRY(axis_pass(s, in, in_ld, rowidx, out, out_ld, rows, 2, n0, n1, n2, kd, nullptr));
+    FISDF_TRY(axis_pass(s, out, out_ld, nullptr, out, out_ld, rows, 1, n0, n1, n2, nullptr, nullptr));
+  }
   FISDF_TRY(axis_pass(s, out, out_ld, nullptr, out, out_ld, rows, 0, n0, n1, n2, nullptr, weight));
   return 0;
 }

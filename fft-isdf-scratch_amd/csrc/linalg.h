@@ -8,8 +8,10 @@ struct CellGeom {
   double b[3][3];  // reciprocal vectors (rows), 2*pi*inv(a)^T
 };
 
-int gather_lp(hipStream_t s, const cplx* L, int rmax, const int* piv, int r, int rpad, cplx* Lp);
-int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int ldl, int nb, cplx* Linv);
+int gather_lp(hipStream_t s, const cplx* L, int n, int rmax, const int* piv, const int* rank,
+              int rpad, cplx* Lp, int batch);
+int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int ldl, long sL, int nb, long sLi,
+                 cplx* Linv, int batch);
 int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, long ldl, long sL, int r,
                  const cplx* Linv, long sLi, int nb, cplx* B, long ldb, long sB, cplx* X, long ldx,
                  long sX, int ncol, int batch);

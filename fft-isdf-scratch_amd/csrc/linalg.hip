@@ -10,9 +10,16 @@ namespace fisdf {
 
 namespace {
 
-// Lp[s][t] = L[piv[s]][t] (t <= s < r), zero above the diagonal; identity beyond rank.
-__global__ void gather_lp_kernel(const cplx* __restrict__ L, int rmax, const int* __restrict__ piv,
-                                 int r, int rpad, cplx* __restrict__ Lp) {
+// Lp[b][s][t] = L[b][piv[b][s]][t] (t <= s < r_b), zero above the diagonal; identity beyond
+// the rank.  L: (batch, n, rmax), piv: (batch, rmax), Lp: (batch, rpad, rpad).
+__global__ void gather_lp_kernel(const cplx* __restrict__ L, int n, int rmax,
+                                 const int* __restrict__ piv, const int* __restrict__ rank,
+                                 int rpad, cplx* __restrict__ Lp) {
+  const int b = blockIdx.y;
+  const int r = rank[b];
+  L += (long)b * n * rmax;
+  piv += (long)b * rmax;
+  Lp += (long)b * rpad * rpad;
   long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (e >= (long)rpad * rpad) return;
   int s = (int)(e / rpad), t = (int)(e % rpad);
@@ -27,9 +34,12 @@ __global__ void gather_lp_kernel(const cplx* __restrict__ L, int rmax, const int
 
 // inverse of each nb x nb lower-triangular diagonal block of Lp (r x r, ld = ldl)
 __global__ __launch_bounds__(64) void trinv_blocks_kernel(const cplx* __restrict__ Lp, int r,
-                                                          int ldl, int nb, cplx* __restrict__ Linv) {
+                                                          int ldl, long sL, int nb, long sLi,
+                                                          cplx* __restrict__ Linv) {
   __shared__ cplx Ls[64][65];
   __shared__ cplx Xs[64][65];
+  Lp += blockIdx.y * sL;
+  Linv += blockIdx.y * sLi;
   const int blk = blockIdx.x;
   const int b0 = blk * nb;
   const int m = min(nb, r - b0);
@@ -232,20 +242,23 @@ inline int nblocks(long n, int bs = 256, long cap = 1L << 20) {
 
 }  // namespace
 
-int gather_lp(hipStream_t s, const cplx* L, int rmax, const int* piv, int r, int rpad, cplx* Lp) {
-  long n = (long)rpad * rpad;
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(gather_lp_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, L, rmax,
-                     piv, r, rpad, Lp);
+int gather_lp(hipStream_t s, const cplx* L, int n, int rmax, const int* piv, const int* rank,
+              int rpad, cplx* Lp, int batch) {
+  long e = (long)rpad * rpad;
+  if (e == 0 || batch == 0) return 0;
+  hipLaunchKernelGGL(gather_lp_kernel, dim3(nblocks(e, 256, 1L << 30), batch), dim3(256), 0, s, L,
+                     n, rmax, piv, rank, rpad, Lp);
   FISDF_HIP(hipGetLastError());
   return 0;
 }
 
-int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int ldl, int nb, cplx* Linv) {
+int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int ldl, long sL, int nb, long sLi,
+                 cplx* Linv, int batch) {
   FISDF_CHECK(nb >= 1 && nb <= 64, "trinv_blocks: nb must be <= 64");
   int nblk = (r + nb - 1) / nb;
-  if (nblk == 0) return 0;
-  hipLaunchKernelGGL(trinv_blocks_kernel, dim3(nblk), dim3(64), 0, s, Lp, r, ldl, nb, Linv);
+  if (nblk == 0 || batch == 0) return 0;
+  hipLaunchKernelGGL(trinv_blocks_kernel, dim3(nblk, batch), dim3(64), 0, s, Lp, r, ldl, sL, nb,
+                     sLi, Linv);
   FISDF_HIP(hipGetLastError());
   return 0;
 }

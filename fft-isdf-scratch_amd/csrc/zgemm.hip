@@ -1,16 +1,24 @@
-// Batched complex128 GEMM on CDNA4 FP64 matrix cores (v_mfma_f64_16x16x4_f64).
+// Batched complex128 GEMM / HERK on CDNA4 FP64 matrix cores (v_mfma_f64_16x16x4_f64).
 //
 // Replaces every BLAS zgemm the reference issues through NumPy `@` on the hot path
-// (fftisdf.py:38,41,46,76,79,84,121,205,211,215,222,225; einsums :155,159,166).
+// (fftisdf.py:38,41,46,76,79,84,121,205,211,215,222,225; einsums :155,159,166) and the
+// HERK that W_q = zeta_q z_q^H (fftisdf.py:121) becomes after the Parseval rewrite.
 //
-// Tile: 64x64 complex per 256-thread workgroup (4 waves, each 32x32 = 2x2 MFMA
-// blocks of 16x16), BK = 16 complex.  A and B tiles are staged global -> registers
-// -> LDS as split real/imag planes (double), so each MFMA operand is one f64 per
-// lane; the next K-tile is prefetched into registers while the current one is
-// consumed.  Complex product = 4 real MFMAs per 16x16x4 block:
-//   Cr += Ar*Br - Ai*Bi ;  Ci += Ar*Bi + Ai*Br
+// Tile: 64x64 complex per 256-thread workgroup (4 waves, each 32x32 = 2x2 MFMA blocks of
+// 16x16).  K advances BK complex per step through a DOUBLE-BUFFERED LDS ring (one barrier
+// per step): the registers loaded during step k are written to the other buffer at the
+// top of step k+1, the loads of step k+2 are issued, then the MFMAs of step k+1 run.
+// LDS holds interleaved complex (16 B), so each MFMA operand pair (re, im) is one
+// ds_read_b128.  Layout per operand follows its global order so stores stay coalesced
+// and conflict-free:
+//   * M/N-contiguous operand: LDS [k][m] plain (64 complex rows = 256 dwords: the
+//     ds_read_b128 lane groups hit disjoint banks);
+//   * K-contiguous operand:   LDS [m][k ^ (m & 15)] (XOR swizzle on the 16-complex row:
+//     fragment reads and 8-lane row stores both conflict-free).
+// Complex product = 4 real MFMAs per 16x16x4 block, issued term-major so an accumulator
+// is reused only every 4th MFMA:   Cr += Ar Br - Ai Bi ;  Ci += Ar Bi + Ai Br.
 // f64 MFMA fragment maps (cdna_hip_programming.md §3):
-//   A: lane l holds A[i=l&15][k=l>>4];  B: B[k=l>>4][j=l&15]
+//   A: lane l holds A[i=l&15][k=l>>4];  B: B[k=l>>4][j=l&15];
 //   C/D: 4 f64 per lane, col = l&15, row = (l>>4) + 4*r.
 #include "common.h"
 
@@ -19,10 +27,12 @@ namespace fisdf {
 namespace {
 
 constexpr int BM = 64, BN = 64, BK = 16;
-constexpr int LDP = BM + 16;  // padded LDS row: k-rows 160 dwords apart -> conflict-free fragment reads
+constexpr int TILE = 64 * BK;   // complex elements per operand tile
+constexpr int LPT = TILE / 256;  // loads per thread per operand per step
 
 template <int OP>
-__device__ __forceinline__ cplx load_op(const cplx* __restrict__ P, long ld, int r, int c, int R, int Ccols) {
+__device__ __forceinline__ cplx load_op(const cplx* __restrict__ P, long ld, int r, int c, int R,
+                                        int Ccols) {
   // element (r, c) of op(P) where op(P) is R x Ccols
   cplx v = cmk(0.0, 0.0);
   if (r < R && c < Ccols) {
@@ -32,17 +42,38 @@ __device__ __forceinline__ cplx load_op(const cplx* __restrict__ P, long ld, int
   return v;
 }
 
+// Operand staging. ROW_IS_K: the tile's "outer" index is the M (or N) index and k is
+// contiguous in global memory (A op N/conj, B op T/conj-T).
+template <bool KCONTIG>
+struct Stage {
+  // thread-element e -> (outer index x in [0,64), k in [0,BK)) chosen for coalesced loads
+  __device__ static __forceinline__ void coord(int e, int& x, int& k) {
+    if (KCONTIG) { x = e / BK; k = e % BK; }
+    else { x = e % 64; k = e / 64; }
+  }
+  // LDS slot of (x, k)
+  __device__ static __forceinline__ int slot(int x, int k) {
+    if (KCONTIG) return x * BK + (k ^ (x & (BK - 1)));
+    else return k * 64 + x;
+  }
+};
+
 // HERK=true: C = alpha A A^H (OPA = N, OPB = C, B == A, M == N); only lower-triangle tiles
 // (ti >= tj) are launched, blockIdx.x enumerates them, and the epilogue mirrors the
-// conjugate into the upper triangle — half the MFMA work of the GEMM (fftisdf.py:121).
+// conjugate into the upper triangle — half the MFMA work of the GEMM.
 template <int OPA, int OPB, bool HERK>
 __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx alpha,
                                                     const cplx* __restrict__ A, long lda, long sA,
                                                     const cplx* __restrict__ B, long ldb, long sB,
                                                     cplx beta, cplx* __restrict__ C, long ldc, long sC,
-                                                    int ksplit, int kchunk, cplx* __restrict__ work) {
-  __shared__ double As[2][BK][LDP];
-  __shared__ double Bs[2][BK][LDP];
+                                                    int ksplit, int kchunk, cplx* __restrict__ work,
+                                                    int epi, unsigned long long* __restrict__ mon) {
+  constexpr bool AK = !(OPA & 1);  // A stored [m][k]
+  constexpr bool BKc = (OPB & 1);  // B stored [n][k]
+  typedef Stage<AK> SA;
+  typedef Stage<BKc> SB;
+  __shared__ cplx As[2][TILE];
+  __shared__ cplx Bs[2][TILE];
 
   const int split = blockIdx.z % ksplit;
   const int bz = blockIdx.z / ksplit;
@@ -72,72 +103,77 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx al
       accI[i][j] = f64x4{0, 0, 0, 0};
     }
 
-  // per-thread element coordinates of the 4 loads per operand tile (64x16 = 1024 elements)
-  // A tile is op(A)[m0:m0+64, k:k+16]; B tile is op(B)[k:k+16, n0:n0+64]
-  cplx ra[4], rb[4];
-  auto a_coord = [&](int j, int& m, int& k) {
-    int e = tid + 256 * j;
-    if (OPA & 1) { m = e & 63; k = e >> 6; }   // memory [k][m]: m contiguous
-    else { m = e >> 4; k = e & 15; }           // memory [m][k]: k contiguous
-  };
-  auto b_coord = [&](int j, int& k, int& n) {
-    int e = tid + 256 * j;
-    if (OPB & 1) { n = e >> 4; k = e & 15; }   // memory [n][k]
-    else { n = e & 63; k = e >> 6; }           // memory [k][n]
-  };
+  cplx ra[LPT], rb[LPT];
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int m, k;
-      a_coord(j, m, k);
-      int gk = k0 + k;
-      ra[j] = load_op<OPA>(A, lda, m0 + m, gk, M, gk < kend ? K : 0);
-      int kk, n;
-      b_coord(j, kk, n);
-      int gk2 = k0 + kk;
-      rb[j] = load_op<OPB>(B, ldb, gk2, n0 + n, gk2 < kend ? K : 0, N);
+    for (int j = 0; j < LPT; ++j) {
+      int x, k;
+      SA::coord(tid + 256 * j, x, k);
+      const int gk = k0 + k;
+      ra[j] = load_op<OPA>(A, lda, m0 + x, gk, M, gk < kend ? K : 0);
+      SB::coord(tid + 256 * j, x, k);
+      const int gk2 = k0 + k;
+      rb[j] = load_op<OPB>(B, ldb, gk2, n0 + x, gk2 < kend ? K : 0, N);
     }
   };
-  auto lstore = [&]() {
+  auto lstore = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int m, k;
-      a_coord(j, m, k);
-      As[0][k][m] = ra[j].x;
-      As[1][k][m] = ra[j].y;
-      int kk, n;
-      b_coord(j, kk, n);
-      Bs[0][kk][n] = rb[j].x;
-      Bs[1][kk][n] = rb[j].y;
+    for (int j = 0; j < LPT; ++j) {
+      int x, k;
+      SA::coord(tid + 256 * j, x, k);
+      As[buf][SA::slot(x, k)] = ra[j];
+      SB::coord(tid + 256 * j, x, k);
+      Bs[buf][SB::slot(x, k)] = rb[j];
     }
   };
 
-  if (kbeg < kend) gload(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    __syncthreads();
-    lstore();
-    __syncthreads();
-    if (k0 + BK < kend) gload(k0 + BK);  // prefetch next tile into registers
+  const int nsteps = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nsteps > 0) {
+    gload(kbeg);
+    lstore(0);
+    if (nsteps > 1) gload(kbeg + BK);
+  }
+  const int i16 = lane & 15, kq = lane >> 4;
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    __syncthreads();  // buffer `cur` complete; buffer `cur^1` no longer read
+    if (s + 1 < nsteps) {
+      lstore(cur ^ 1);
+      if (s + 2 < nsteps) gload(kbeg + (s + 2) * BK);
+    }
+    const cplx* as = As[cur];
+    const cplx* bs = Bs[cur];
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
-      const int ka = kk + (lane >> 4), i = lane & 15;
-      double ar[2], ai[2], br[2], bi[2];
+      const int k = kk + kq;
+      cplx a[2], b[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        ar[t] = As[0][ka][wm + t * 16 + i];
-        ai[t] = As[1][ka][wm + t * 16 + i];
-        br[t] = Bs[0][ka][wn + t * 16 + i];
-        bi[t] = Bs[1][ka][wn + t * 16 + i];
+        a[t] = as[SA::slot(wm + t * 16 + i16, k)];
+        b[t] = bs[SB::slot(wn + t * 16 + i16, k)];
       }
+      const double nai0 = -a[0].y, nai1 = -a[1].y;
+      const double nai[2] = {nai0, nai1};
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], accR[mi][ni], 0, 0, 0);
-          accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], bi[ni], accI[mi][ni], 0, 0, 0);
-          accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ai[mi], bi[ni], accR[mi][ni], 0, 0, 0);
-          accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], br[ni], accI[mi][ni], 0, 0, 0);
-        }
+        for (int ni = 0; ni < 2; ++ni)
+          accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].x, b[ni].x, accR[mi][ni], 0, 0, 0);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].x, b[ni].y, accI[mi][ni], 0, 0, 0);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[mi], b[ni].y, accR[mi][ni], 0, 0, 0);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].y, b[ni].x, accI[mi][ni], 0, 0, 0);
     }
   }
 
@@ -160,6 +196,28 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx al
     return;
   }
   C += (long)bz * sC;
+  if (epi == EPI_SQUARE_RE) {
+    // y_s = Re(alpha acc)^2 + 0i, fused (fftisdf.py:83); monitor max|Im| (fftisdf.py:81)
+    double mi_ = 0.0;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
+          int col = n0 + wn + ni * 16 + (lane & 15);
+          if (row < M && col < N) {
+            cplx v = cmul(alpha, cmk(accR[mi][ni][r], accI[mi][ni][r]));
+            C[(long)row * ldc + col] = cmk(v.x * v.x, 0.0);
+            mi_ = fmax(mi_, fabs(v.y));
+          }
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mi_ = fmax(mi_, __shfl_xor(mi_, o, 64));
+    if (lane == 0 && mon) atomicMax(mon, (unsigned long long)__double_as_longlong(mi_));
+    return;
+  }
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -197,20 +255,21 @@ __global__ void ksplit_reduce(int M, int N, int ksplit, const cplx* __restrict__
 template <int OPA, int OPB, bool HERK = false>
 void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cplx* A, long lda,
             long sA, const cplx* B, long ldb, long sB, cplx beta, cplx* C, long ldc, long sC,
-            int ksplit, int kchunk, cplx* work) {
+            int ksplit, int kchunk, cplx* work, int epi, unsigned long long* mon) {
   hipLaunchKernelGGL((zgemm_kernel<OPA, OPB, HERK>), grid, dim3(256), 0, s, M, N, K, alpha, A, lda, sA,
-                     B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work);
+                     B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work, epi, mon);
 }
 
 }  // namespace
 
 int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, const cplx* A,
           long lda, long sA, const cplx* B, long ldb, long sB, cplx beta, cplx* C, long ldc,
-          long sC, int batch, int ksplit, cplx* work) {
+          long sC, int batch, int ksplit, cplx* work, int epi, unsigned long long* mon) {
   FISDF_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 0, "zgemm: negative size");
   FISDF_CHECK(opA >= 0 && opA < 4 && opB >= 0 && opB < 4, "zgemm: bad op");
   if (M == 0 || N == 0 || batch == 0) return 0;
   if (ksplit < 1) ksplit = 1;
+  if (epi != EPI_NONE) ksplit = 1;
   if (ksplit > 1) FISDF_CHECK(work != nullptr, "zgemm: split-K needs a workspace");
   int kchunk = (K + ksplit - 1) / ksplit;
   kchunk = ((kchunk + BK - 1) / BK) * BK;
@@ -219,11 +278,10 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
   FISDF_CHECK((long)batch * ksplit < 65536, "zgemm: batch*ksplit exceeds grid.z");
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch * ksplit);
   FISDF_CHECK(grid.y < 65536, "zgemm: M too large");
-  if (K == 0) ksplit = 1;
 #define FISDF_CASE(a, b)                                                                      \
   case a * 4 + b:                                                                             \
     launch<a, b>(s, grid, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit,   \
-                 kchunk, work);                                                               \
+                 kchunk, work, epi, mon);                                                     \
     break;
   switch (opA * 4 + opB) {
     FISDF_CASE(0, 0) FISDF_CASE(0, 1) FISDF_CASE(0, 2) FISDF_CASE(0, 3)
@@ -256,7 +314,7 @@ int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cpl
   const int nt = (n + BM - 1) / BM;
   dim3 grid(nt * (nt + 1) / 2, 1, ksplit);
   launch<OP_N, OP_C, true>(s, grid, n, n, K, cmk(alpha, 0), A, lda, 0, A, lda, 0, cmk(0, 0), C,
-                           ldc, 0, ksplit, kchunk, work);
+                           ldc, 0, ksplit, kchunk, work, EPI_NONE, nullptr);
   FISDF_HIP(hipGetLastError());
   if (ksplit > 1) {
     long MN = (long)n * n;
