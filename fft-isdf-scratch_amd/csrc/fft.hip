@@ -158,15 +158,24 @@ __global__ __launch_bounds__(256) void fft_axis_kernel(
   };
 
   const int tot = TL * n;
-  __syncthreads();
-  for (int e = tid; e < tot; e += nthr) {
+  // first U elements per thread: loads issued together (branch-free, clamped address)
+  constexpr int U = 8;
+  cplx pre[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = tid + u * nthr;
     int l, p;
     if (contiguous) { l = e / n; p = e % n; } else { l = e % TL; p = e / TL; }
-    cplx v = cmk(0, 0);
+    const bool ok = e < tot && l < nlines;
+    pre[u] = src[ok ? gidx(l, p) : 0];
+  }
+  __syncthreads();
+  auto put = [&](int e, cplx v) {
+    int l, p;
+    if (contiguous) { l = e / n; p = e % n; } else { l = e % TL; p = e / TL; }
     if (l < nlines) {
-      long g = gidx(l, p);
-      v = src[g];
       if (use_phase) {
+        long g = gidx(l, p);
         int i2 = (int)(g % n2);
         int i1 = (int)((g / n2) % n1);
         int i0 = (int)(g / ((long)n1 * n2));
@@ -175,8 +184,20 @@ __global__ __launch_bounds__(256) void fft_axis_kernel(
         sincos(th, &s, &c);
         v = cmul(v, cmk(c, s));
       }
+    } else {
+      v = cmk(0, 0);
     }
     buf0[p * TL + l] = v;
+  };
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = tid + u * nthr;
+    if (e < tot) put(e, pre[u]);
+  }
+  for (int e = tid + U * nthr; e < tot; e += nthr) {
+    int l, p;
+    if (contiguous) { l = e / n; p = e % n; } else { l = e % TL; p = e / TL; }
+    put(e, l < nlines ? src[gidx(l, p)] : cmk(0, 0));
   }
   __syncthreads();
   cplx* a = lds_fft_lines<BIG>(buf0, buf1, tw, n, st.radix, st.nst, TL, TL, 1, tid, nthr);
@@ -202,27 +223,55 @@ __global__ __launch_bounds__(256) void fft_plane_kernel(
   extern __shared__ cplx smem[];
   cplx* tw1 = smem;
   cplx* tw2 = smem + MAXN;
+  cplx* ph1 = smem + 2 * MAXN;  // exp(-i f(i1) kd1) * exp(-i f(i0) kd0)
+  cplx* ph2 = smem + 3 * MAXN;  // exp(-i f(i2) kd2)
   const int P = n1 * n2;
-  cplx* buf0 = smem + 2 * MAXN;
+  cplx* buf0 = smem + 4 * MAXN;
   cplx* buf1 = buf0 + P;
   const int tid = threadIdx.x, nthr = blockDim.x;
-  for (int t = tid; t < n1; t += nthr) tw1[t] = tw1g[t];
-  for (int t = tid; t < n2; t += nthr) tw2[t] = tw2g[t];
   const int row = blockIdx.x / n0, i0 = blockIdx.x % n0;
   if (row >= rows) return;
   const cplx* src = in + (long)(rowidx ? rowidx[row] : row) * in_ld + (long)i0 * P;
   cplx* dstp = out + (long)row * out_ld + (long)i0 * P;
-  const double f0 = fftfreq(i0, n0) * kd0;
-  for (int e = tid; e < P; e += nthr) {
-    cplx v = src[e];
-    if (use_phase) {
-      const int i1 = e / n2, i2 = e % n2;
-      double th = -(f0 + fftfreq(i1, n1) * kd1 + fftfreq(i2, n2) * kd2);
+  // issue this plane's loads first (branch-free, up to 8 per thread in flight)
+  constexpr int U = 8;
+  cplx v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = tid + u * nthr;
+    v[u] = src[e < P ? e : 0];
+  }
+  for (int t = tid; t < n1; t += nthr) tw1[t] = tw1g[t];
+  for (int t = tid; t < n2; t += nthr) tw2[t] = tw2g[t];
+  if (use_phase) {
+    // separable phase exp(-i k.r) = e0(i0) e1(i1) e2(i2): one sincos per axis entry
+    double s0, c0;
+    sincos(-fftfreq(i0, n0) * kd0, &s0, &c0);
+    for (int t = tid; t < n1; t += nthr) {
       double s, c;
-      sincos(th, &s, &c);
-      v = cmul(v, cmk(c, s));
+      sincos(-fftfreq(t, n1) * kd1, &s, &c);
+      ph1[t] = cmul(cmk(c, s), cmk(c0, s0));
     }
-    buf0[e] = v;
+    for (int t = tid; t < n2; t += nthr) {
+      double s, c;
+      sincos(-fftfreq(t, n2) * kd2, &s, &c);
+      ph2[t] = cmk(c, s);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = tid + u * nthr;
+    if (e < P) {
+      cplx x = v[u];
+      if (use_phase) x = cmul(x, cmul(ph1[e / n2], ph2[e % n2]));
+      buf0[e] = x;
+    }
+  }
+  for (int e = tid + U * nthr; e < P; e += nthr) {  // planes larger than U*256 points
+    cplx x = src[e];
+    if (use_phase) x = cmul(x, cmul(ph1[e / n2], ph2[e % n2]));
+    buf0[e] = x;
   }
   __syncthreads();
   // axis 2: n1 lines of n2 contiguous points (p stride 1, line stride n2)
@@ -338,7 +387,7 @@ int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* ou
           int rows, int n0, int n1, int n2, const double* kd, const double* weight, cplx* /*work*/) {
   if (rows == 0) return 0;
   FISDF_CHECK(in != out || rowidx == nullptr, "fft: in-place pass cannot gather rows");
-  const size_t plane_lds = sizeof(cplx) * (2 * MAXN + 2 * (size_t)n1 * n2);
+  const size_t plane_lds = sizeof(cplx) * (4 * MAXN + 2 * (size_t)n1 * n2);
   if (plane_lds <= 96 * 1024) {
     // axes 2+1 fused per (i1,i2) plane, then axis 0 with the Coulomb weight: 2 HBM passes
     Stages st1, st2;

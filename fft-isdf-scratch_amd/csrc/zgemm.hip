@@ -26,20 +26,32 @@ namespace fisdf {
 
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 16;
+#ifndef FISDF_BK
+#define FISDF_BK 8  // A/B on MI355X (C3 bench): BK=8 (32 KB LDS, 3 WGs/CU) 333 ms vs BK=16 348 ms
+#endif
+constexpr int BM = 64, BN = 64, BK = FISDF_BK;
 constexpr int TILE = 64 * BK;   // complex elements per operand tile
 constexpr int LPT = TILE / 256;  // loads per thread per operand per step
 
+// element (r, c) of op(P) where op(P) is R x Ccols.  Branch-free: the load is issued
+// unconditionally (out-of-range lanes read element 0) and the in-range bit is returned; the
+// zero-masking and conjugation happen at LDS-store time one step later, so the loads of a
+// step stay in flight across the MFMAs instead of being drained right after issue
+// (cdna_hip_programming.md §5, trap (c)).
 template <int OP>
-__device__ __forceinline__ cplx load_op(const cplx* __restrict__ P, long ld, int r, int c, int R,
-                                        int Ccols) {
-  // element (r, c) of op(P) where op(P) is R x Ccols
-  cplx v = cmk(0.0, 0.0);
-  if (r < R && c < Ccols) {
-    v = (OP & 1) ? P[(long)c * ld + r] : P[(long)r * ld + c];
-    if (OP & 2) v.y = -v.y;
-  }
-  return v;
+__device__ __forceinline__ cplx load_raw(const cplx* __restrict__ P, long ld, int r, int c, int R,
+                                         int Ccols, bool& ok) {
+  ok = (r < R) & (c < Ccols);
+  long off = (OP & 1) ? (long)c * ld + r : (long)r * ld + c;
+  return P[ok ? off : 0];
+}
+
+template <int OP>
+__device__ __forceinline__ cplx finish(cplx v, bool ok) {
+  cplx o;
+  o.x = ok ? v.x : 0.0;
+  o.y = ok ? ((OP & 2) ? -v.y : v.y) : 0.0;
+  return o;
 }
 
 // Operand staging. ROW_IS_K: the tile's "outer" index is the M (or N) index and k is
@@ -104,16 +116,17 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx al
     }
 
   cplx ra[LPT], rb[LPT];
+  bool oka[LPT], okb[LPT];
   auto gload = [&](int k0) {
 #pragma unroll
     for (int j = 0; j < LPT; ++j) {
       int x, k;
       SA::coord(tid + 256 * j, x, k);
       const int gk = k0 + k;
-      ra[j] = load_op<OPA>(A, lda, m0 + x, gk, M, gk < kend ? K : 0);
+      ra[j] = load_raw<OPA>(A, lda, m0 + x, gk, M, gk < kend ? K : 0, oka[j]);
       SB::coord(tid + 256 * j, x, k);
       const int gk2 = k0 + k;
-      rb[j] = load_op<OPB>(B, ldb, gk2, n0 + x, gk2 < kend ? K : 0, N);
+      rb[j] = load_raw<OPB>(B, ldb, gk2, n0 + x, gk2 < kend ? K : 0, N, okb[j]);
     }
   };
   auto lstore = [&](int buf) {
@@ -121,26 +134,26 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx al
     for (int j = 0; j < LPT; ++j) {
       int x, k;
       SA::coord(tid + 256 * j, x, k);
-      As[buf][SA::slot(x, k)] = ra[j];
+      As[buf][SA::slot(x, k)] = finish<OPA>(ra[j], oka[j]);
       SB::coord(tid + 256 * j, x, k);
-      Bs[buf][SB::slot(x, k)] = rb[j];
+      Bs[buf][SB::slot(x, k)] = finish<OPB>(rb[j], okb[j]);
     }
   };
 
+  // Branch-free ring: every step stores the prefetched tile into the idle buffer and issues
+  // the loads two steps ahead (past kend they are masked to zero and never consumed).
   const int nsteps = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   if (nsteps > 0) {
     gload(kbeg);
     lstore(0);
-    if (nsteps > 1) gload(kbeg + BK);
+    gload(kbeg + BK);
   }
   const int i16 = lane & 15, kq = lane >> 4;
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s & 1;
     __syncthreads();  // buffer `cur` complete; buffer `cur^1` no longer read
-    if (s + 1 < nsteps) {
-      lstore(cur ^ 1);
-      if (s + 2 < nsteps) gload(kbeg + (s + 2) * BK);
-    }
+    lstore(cur ^ 1);
+    gload(kbeg + (s + 2) * BK);
     const cplx* as = As[cur];
     const cplx* bs = Bs[cur];
 #pragma unroll
