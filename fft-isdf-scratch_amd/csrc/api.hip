@@ -176,6 +176,25 @@ int free_factors(fisdf_ctx* c) {
   return 0;
 }
 
+// x2 = sum_{q in [q0,q1)} conj(x0_q) x0_q^T, via P = x0 permuted to (ng0, nq*nao) and the
+// Hermitian update P P^H (only its real part is used: Re(P P^H) = Re(conj(P) P^T)).
+// `tmp` must hold ng0*nq*nao complex.
+int select_gram(fisdf_ctx* c, const cplx* x0, int nk, int q0, int q1, int ng0, int nao, cplx* x2,
+                cplx* tmp) {
+  const int nq = q1 - q0;
+  FISDF_TRY(permute_kgm(c->stream, x0 + (long)q0 * ng0 * nao, nq, ng0, nao, tmp));
+  const int K = nq * nao;
+  int ks = 1;
+  const long tiles = (long)((ng0 + 63) / 64) * ((ng0 + 63) / 64 + 1) / 2;
+  while (tiles * ks < 512 && K / (ks * 2) >= 256) ks *= 2;
+  cplx* work = nullptr;
+  if (ks > 1) FISDF_HIP(hipMallocAsync((void**)&work, sizeof(cplx) * (size_t)ks * ng0 * ng0, c->stream));
+  FISDF_TRY(herk(c->stream, ng0, K, 1.0, tmp, K, x2, ng0, ks, work));
+  if (work) FISDF_HIP(hipFreeAsync(work, c->stream));
+  (void)nk;
+  return 0;
+}
+
 int pick_ksplit(int M, int N, int K) {
   long tiles = (long)((M + 63) / 64) * ((N + 63) / 64);
   int ks = 1;
@@ -372,6 +391,7 @@ int fisdf_select_points(fisdf_ctx* c, const void* x0v, int nk, int ng0, int nao,
   Carver cv;
   size_t oX2 = cv.take(sizeof(cplx) * (size_t)ng0 * ng0);
   size_t oX4 = cv.take(sizeof(cplx) * (size_t)ng0 * ng0);
+  size_t oPm = cv.take(sizeof(cplx) * (size_t)ng0 * nk * nao);
   size_t oL = cv.take(sizeof(cplx) * (size_t)ng0 * nip_max);
   size_t oP = cv.take(sizeof(int) * nip_max);
   size_t oR = cv.take(sizeof(int) * 4);
@@ -383,12 +403,9 @@ int fisdf_select_points(fisdf_ctx* c, const void* x0v, int nk, int ng0, int nao,
   char* b = (char*)base;
   cplx* X2 = (cplx*)(b + oX2);
   cplx* X4 = (cplx*)(b + oX4);
-  // x2 = sum_q conj(x0_q) x0_q^T   (fftisdf.py:376-378; real part taken below)
-  for (int q = 0; q < nk; ++q) {
-    const cplx* xq = x0 + (size_t)q * ng0 * nao;
-    FISDF_TRY(zgemm(c->stream, OP_R, OP_T, ng0, ng0, nao, ONE, xq, nao, 0, xq, nao, 0,
-                    q ? ONE : ZERO, X2, ng0, 0, 1));
-  }
+  // x2 = sum_q conj(x0_q) x0_q^T   (fftisdf.py:376-378; real part taken below) as one
+  // K = nk*nao Hermitian rank-K update of the permuted x0
+  FISDF_TRY(select_gram(c, x0, nk, 0, nk, ng0, nao, X2, (cplx*)(b + oPm)));
   // x4 = Re(x2)^2 / nk  (:379)
   FISDF_TRY(square_scale(c->stream, X2, 1.0 / nk, X4, (long)ng0 * ng0));
   // greedy pivoted Cholesky (:381-384), first nip_max pivots
@@ -401,6 +418,67 @@ int fisdf_select_points(fisdf_ctx* c, const void* x0v, int nk, int ng0, int nao,
   FISDF_HIP(hipStreamSynchronize(c->stream));
   *h_npiv = rank;
   if (h_full_rank) *h_full_rank = rank < nip_max ? 1 : 0;
+  return 0;
+}
+
+int fisdf_select_gram(fisdf_ctx* c, const void* x0, int nk, int q0, int q1, int ng0, int nao,
+                      void* x2) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(0 <= q0 && q0 <= q1 && q1 <= nk && ng0 > 0 && nao > 0, "select_gram: bad sizes");
+  StageTimer tm(c, FISDF_ST_SELECT);
+  if (q1 == q0) {
+    FISDF_HIP(hipMemsetAsync(x2, 0, sizeof(cplx) * (size_t)ng0 * ng0, c->stream));
+    return 0;
+  }
+  void* base;
+  FISDF_TRY(arena_get(c, sizeof(cplx) * (size_t)ng0 * (q1 - q0) * nao, &base));
+  return select_gram(c, (const cplx*)x0, nk, q0, q1, ng0, nao, (cplx*)x2, (cplx*)base);
+}
+
+int fisdf_select_pivots(fisdf_ctx* c, const void* x2, int nk, int ng0, int nip_max, double tol,
+                        int* h_perm, int* h_npiv, int* h_full_rank) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(nk > 0 && ng0 > 0 && nip_max > 0, "select_pivots: bad sizes");
+  nip_max = std::min(nip_max, ng0);
+  StageTimer tm(c, FISDF_ST_SELECT);
+  Carver cv;
+  size_t oX4 = cv.take(sizeof(cplx) * (size_t)ng0 * ng0);
+  size_t oL = cv.take(sizeof(cplx) * (size_t)ng0 * nip_max);
+  size_t oP = cv.take(sizeof(int) * nip_max);
+  size_t oR = cv.take(sizeof(int) * 4);
+  size_t oD = cv.take(sizeof(double) * ng0);
+  size_t oF = cv.take(sizeof(int) * 4);
+  size_t oW = cv.take(sizeof(double) * (1 + nip_max));
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  char* b = (char*)base;
+  cplx* X4 = (cplx*)(b + oX4);
+  FISDF_TRY(square_scale(c->stream, (const cplx*)x2, 1.0 / nk, X4, (long)ng0 * ng0));  // :379
+  FISDF_TRY(pchol(c->stream, X4, ng0, 0, ng0, 1, nip_max, tol, 0.0, (cplx*)(b + oL),
+                  (int*)(b + oP), (int*)(b + oR), (double*)(b + oD), (int*)(b + oF),
+                  (double*)(b + oW)));                                                // :381-384
+  int rank = 0;
+  FISDF_HIP(hipMemcpyAsync(&rank, b + oR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipMemcpyAsync(h_perm, b + oP, sizeof(int) * nip_max, hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  *h_npiv = rank;
+  if (h_full_rank) *h_full_rank = rank < nip_max ? 1 : 0;
+  return 0;
+}
+
+int fisdf_unpack_slices(fisdf_ctx* c, const void* recv, int nrows, int nparts, const long* h_g0,
+                        const long* h_ng, long ngrid, void* yT) {
+  FISDF_TRY(device_guard(c));
+  StageTimer tm(c, FISDF_ST_Y);
+  const char* src = (const char*)recv;
+  for (int p = 0; p < nparts; ++p) {
+    FISDF_CHECK(h_g0[p] >= 0 && h_ng[p] >= 0 && h_g0[p] + h_ng[p] <= ngrid, "unpack: bad slice");
+    if (h_ng[p] == 0 || nrows == 0) continue;
+    FISDF_HIP(hipMemcpy2DAsync((char*)yT + sizeof(cplx) * h_g0[p], sizeof(cplx) * ngrid, src,
+                               sizeof(cplx) * h_ng[p], sizeof(cplx) * h_ng[p], nrows,
+                               hipMemcpyDeviceToDevice, c->stream));
+    src += sizeof(cplx) * (size_t)h_ng[p] * nrows;
+  }
   return 0;
 }
 

@@ -32,5 +32,6 @@ int scale_rows(hipStream_t s, const cplx* X, const cplx* v, int nset, int nk, in
 int gather_points(hipStream_t s, const cplx* x0, int nk, int ng0, int nao, const int* perm,
                   int nip, cplx* X);
 int square_scale(hipStream_t s, const cplx* in, double sc, cplx* out, long n);
+int permute_kgm(hipStream_t s, const cplx* x0, int nq, int ng, int nao, cplx* out);
 
 }  // namespace fisdf

@@ -202,6 +202,18 @@ __global__ void scale_rows_kernel(const cplx* __restrict__ X, const cplx* __rest
   Xv[e] = cmul(v[(long)x * nip + I], X[r]);
 }
 
+// out[g][q*nao + m] = x0[q][g][m]   (k-point axis folded into the GEMM K dimension)
+__global__ void permute_kgm_kernel(const cplx* __restrict__ x0, int nq, int ng, int nao,
+                                   cplx* __restrict__ out) {
+  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long tot = (long)nq * ng * nao;
+  if (e >= tot) return;
+  const int m = (int)(e % nao);
+  const int g = (int)((e / nao) % ng);
+  const int q = (int)(e / ((long)nao * ng));
+  out[(long)g * nq * nao + (long)q * nao + m] = x0[e];
+}
+
 // X[k,I,:] = x0[k, perm[I], :]
 __global__ void gather_points_kernel(const cplx* __restrict__ x0, int nk, int ng0, int nao,
                                      const int* __restrict__ perm, int nip, cplx* __restrict__ X) {
@@ -370,6 +382,15 @@ int scale_rows(hipStream_t s, const cplx* X, const cplx* v, int nset, int nk, in
   if (n == 0) return 0;
   hipLaunchKernelGGL(scale_rows_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, X, v,
                      nset, nk, nip, nao, Xv);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int permute_kgm(hipStream_t s, const cplx* x0, int nq, int ng, int nao, cplx* out) {
+  long n = (long)nq * ng * nao;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(permute_kgm_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, x0, nq,
+                     ng, nao, out);
   FISDF_HIP(hipGetLastError());
   return 0;
 }

@@ -40,6 +40,9 @@ _SIGS = {
     "fisdf_max_imag": ([_vp, _dp], _i),
     "fisdf_select_points": ([_vp, _vp, _i, _i, _i, _i, _d, _ip, _ip, _ip], _i),
     "fisdf_gather_points": ([_vp, _vp, _i, _i, _i, _ip, _i, _vp], _i),
+    "fisdf_select_gram": ([_vp, _vp, _i, _i, _i, _i, _i, _vp], _i),
+    "fisdf_select_pivots": ([_vp, _vp, _i, _i, _i, _d, _ip, _ip, _ip], _i),
+    "fisdf_unpack_slices": ([_vp, _vp, _i, _i, C.POINTER(_l), C.POINTER(_l), _l, _vp], _i),
     "fisdf_build_x4": ([_vp, _vp, _i, _i, _ip, _dp, _vp], _i),
     "fisdf_build_y": ([_vp, _vp, _l, _i, _i, _i, _vp, _i, _i, _ip, _dp, _i, _i, _vp], _i),
     "fisdf_factor_x4": ([_vp, _vp, _i, _i, _i, _d, _ip], _i),

@@ -180,8 +180,20 @@ class InterpolativeSeparableDensityFitting:
         perm = np.zeros(nip_max, np.int32)
         npiv = C_int()
         full = C_int()
-        d.ctx.call("fisdf_select_points", _lib.ptr(x0), nk, ng0, nao, nip_max,
-                   float(self.select_tol), perm.ctypes.data_as(_lib._ip), byref(npiv), byref(full))
+        if d.size == 1:
+            d.ctx.call("fisdf_select_points", _lib.ptr(x0), nk, ng0, nao, nip_max,
+                       float(self.select_tol), perm.ctypes.data_as(_lib._ip), byref(npiv),
+                       byref(full))
+        else:
+            # k-sharded Gram (fftisdf.py:376-378) + all-reduce, then identical pivots everywhere
+            q0, q1 = d.shard(nk)
+            x2 = d.empty((ng0, ng0))
+            d.ctx.call("fisdf_select_gram", _lib.ptr(x0), nk, q0, q1, ng0, nao, _lib.ptr(x2))
+            kshard.allreduce_sum(x2, d.comm)
+            d.ctx.call("fisdf_select_pivots", _lib.ptr(x2), nk, ng0, nip_max,
+                       float(self.select_tol), perm.ctypes.data_as(_lib._ip), byref(npiv),
+                       byref(full))
+            del x2
         nip = min(nip_max, npiv.value)                                  # fftisdf.py:383
         self.perm = perm[:nip].copy()
         X = d.empty((nk, nip, nao))
@@ -256,7 +268,7 @@ class InterpolativeSeparableDensityFitting:
 
 ISDF = InterpolativeSeparableDensityFitting
 
-from ctypes import c_int as C_int, byref  # noqa: E402
+from ctypes import c_int as C_int, c_long as C_long, byref  # noqa: E402
 
 
 def build(df_obj):
@@ -287,8 +299,26 @@ def build(df_obj):
         df_obj._ao_grid = d.to_dev(eval_ao_kpts(cell, df_obj.grids_coords(), kmesh))
     f = df_obj._ao_grid
     yT = d.empty((q1 - q0, nip, ngrid))
-    d.ctx.call("fisdf_build_y", _lib.ptr(f), ngrid * nao, 0, ngrid, ngrid, _lib.ptr(X), nip, nao,
-               km_p, a_p, q0, q1, _lib.ptr(yT))                          # :67-87
+    if d.size == 1:
+        d.ctx.call("fisdf_build_y", _lib.ptr(f), ngrid * nao, 0, ngrid, ngrid, _lib.ptr(X), nip,
+                   nao, km_p, a_p, q0, q1, _lib.ptr(yT))                 # :67-87
+    else:
+        # grid-sharded y (all q on this rank's plane-aligned grid slice), then one all-to-all
+        # hands every rank the y_q of its own q-shard on the whole grid
+        slices = kshard.grid_slices(df_obj.mesh, d.size)
+        g0, ng = slices[d.rank]
+        send = d.empty((nk, nip, ng))
+        if ng:
+            fptr = _lib._vp(f.data_ptr() + g0 * nao * f.element_size())
+            d.ctx.call("fisdf_build_y", fptr, ngrid * nao, 0, ng, ng, _lib.ptr(X), nip, nao,
+                       km_p, a_p, 0, nk, _lib.ptr(send))
+        recv = kshard.exchange_y(send, nk, nip, slices, d.rank, d.size, d.comm)
+        del send
+        g0s = (C_long * d.size)(*[s[0] for s in slices])
+        ngs = (C_long * d.size)(*[s[1] for s in slices])
+        d.ctx.call("fisdf_unpack_slices", _lib.ptr(recv), (q1 - q0) * nip, d.size, g0s, ngs,
+                   ngrid, _lib.ptr(yT))
+        del recv
 
     ranks = np.zeros(q1 - q0, np.int32)
     d.ctx.call("fisdf_factor_x4", _lib.ptr(x4), q0, q1, nip, float(df_obj.fit_tol),

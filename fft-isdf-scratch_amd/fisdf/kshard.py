@@ -9,6 +9,11 @@ exchange steps are the ones the algorithm has:
   xGMI on the GPUs; gloo in the CPU tests);
 * get_j uses W_0 (fftisdf.py:159), owned by the rank holding q = 0: one broadcast.
 
+* the y build is sharded over plane-aligned grid slices (y_k = Phi^T (Phi fx_k)^2 mixes
+  all k at each grid point, fftisdf.py:79-84): one all-to-all hands each rank the y_q of
+  its q-shard (SURVEY.md §8e);
+* the selection Gram (fftisdf.py:376-378) is a sum over q: per-rank partials + all-reduce.
+
 These helpers take torch tensors on any device, so the same code runs the CPU gloo
 tests and the RCCL path.
 """
@@ -30,16 +35,64 @@ def owner_of(q: int, nk: int, size: int) -> int:
     raise ValueError(q)
 
 
+def grid_slices(mesh, size: int):
+    """Plane-aligned contiguous grid slices [(g0, ng)] of the FFT mesh, one per rank: the
+    y build is sharded over grid points (every rank computes y_q for ALL q on its slice)."""
+    n0 = int(mesh[0])
+    plane = int(mesh[1]) * int(mesh[2])
+    out = []
+    for r in range(size):
+        p0, p1 = shard_range(n0, r, size)
+        out.append((p0 * plane, (p1 - p0) * plane))
+    return out
+
+
+def exchange_y(send, nk: int, nip: int, slices, rank: int, size: int, group=None):
+    """All-to-all of the grid-sliced y: `send` is (nk, nip, ng_rank) = y_q on this rank's
+    slice for every q; the q-blocks are contiguous, so block r of the send buffer is rank
+    r's q-shard.  Returns recv = concat_p (nq_self, nip, ng_p) in rank order p."""
+    import torch
+    import torch.distributed as dist
+    ng_self = slices[rank][1]
+    q0, q1 = shard_range(nk, rank, size)
+    nq = q1 - q0
+    in_splits = [(b - a) * nip * ng_self for a, b in (shard_range(nk, r, size) for r in range(size))]
+    out_splits = [nq * nip * slices[p][1] for p in range(size)]
+    if _host_staged(group, send):
+        return exchange_y(send.cpu(), nk, nip, slices, rank, size, group).to(send.device)
+    recv = torch.empty(sum(out_splits), dtype=send.dtype, device=send.device)
+    flat = send.reshape(-1)
+    if send.is_complex():
+        dist.all_to_all_single(torch.view_as_real(recv), torch.view_as_real(flat), out_splits,
+                               in_splits, group=group)
+    else:
+        dist.all_to_all_single(recv, flat, out_splits, in_splits, group=group)
+    return recv
+
+
+def _host_staged(group, *tensors):
+    """gloo moves host tensors only: device tensors are staged through host copies (used
+    when several ranks share one GPU in tests; the multi-GPU path uses RCCL directly)."""
+    import torch.distributed as dist
+    return dist.get_backend(group) == "gloo" and any(t.is_cuda for t in tensors)
+
+
+def allreduce_sum(t, group=None):
+    """In-place sum over ranks (complex tensors are reduced through their real view)."""
+    import torch
+    import torch.distributed as dist
+    if _host_staged(group, t):
+        h = t.cpu()
+        allreduce_sum(h, group)
+        t.copy_(h)
+        return t
+    dist.all_reduce(torch.view_as_real(t) if t.is_complex() else t, group=group)
+    return t
+
+
 def allreduce_ws(ws, group=None):
     """Sum the per-rank partial W_s (complex tensor, imaginary part zero) in place."""
-    import torch.distributed as dist
-    if ws.is_complex() and not ws.is_cuda:
-        # gloo reduces real tensors; the complex view is summed component-wise
-        import torch
-        dist.all_reduce(torch.view_as_real(ws), group=group)
-    else:
-        dist.all_reduce(ws, group=group)
-    return ws
+    return allreduce_sum(ws, group)
 
 
 def broadcast_w0(w0, nk: int, group=None):
@@ -49,8 +102,10 @@ def broadcast_w0(w0, nk: int, group=None):
     size = dist.get_world_size(group)
     src_local = owner_of(0, nk, size)
     src = dist.get_global_rank(group, src_local) if group is not None else src_local
-    if w0.is_complex() and not w0.is_cuda:
-        dist.broadcast(torch.view_as_real(w0), src=src, group=group)
-    else:
-        dist.broadcast(w0, src=src, group=group)
+    if _host_staged(group, w0):
+        h = w0.cpu()
+        dist.broadcast(torch.view_as_real(h) if h.is_complex() else h, src=src, group=group)
+        w0.copy_(h)
+        return w0
+    dist.broadcast(torch.view_as_real(w0) if w0.is_complex() else w0, src=src, group=group)
     return w0

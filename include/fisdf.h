@@ -71,6 +71,21 @@ int fisdf_max_imag(fisdf_ctx* ctx, double* h_out /* 3 */);
 int fisdf_select_points(fisdf_ctx* ctx, const void* d_x0, int nk, int ng0, int nao, int nip_max,
                         double tol, int* h_perm, int* h_npiv, int* h_full_rank);
 
+/* The two halves of fisdf_select_points, for a k-point-sharded selection:
+ * fisdf_select_gram: d_x2 (ng0, ng0) c128 = sum_{q in [q0,q1)} x0_q x0_q^H (its real part is
+ *   fftisdf.py:376-378's x2; shards are summed with an all-reduce);
+ * fisdf_select_pivots: x4 = Re(x2)^2/nk and the greedy pivoted Cholesky (fftisdf.py:379-384);
+ *   synchronous. */
+int fisdf_select_gram(fisdf_ctx* ctx, const void* d_x0, int nk, int q0, int q1, int ng0, int nao,
+                      void* d_x2);
+int fisdf_select_pivots(fisdf_ctx* ctx, const void* d_x2, int nk, int ng0, int nip_max, double tol,
+                        int* h_perm, int* h_npiv, int* h_full_rank);
+
+/* Reassemble a k-shard's y after the grid-slice all-to-all: d_recv holds, for p = 0..nparts-1,
+ * a (nrows, h_ng[p]) block of grid points [h_g0[p], h_g0[p]+h_ng[p]); d_yT is (nrows, ngrid). */
+int fisdf_unpack_slices(fisdf_ctx* ctx, const void* d_recv, int nrows, int nparts,
+                        const long* h_g0, const long* h_ng, long ngrid, void* d_yT);
+
 /* X[k, I, :] = x0[k, perm[I], :]  (fftisdf.py:388) */
 int fisdf_gather_points(fisdf_ctx* ctx, const void* d_x0, int nk, int ng0, int nao,
                         const int* h_perm, int nip, void* d_X);

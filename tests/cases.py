@@ -28,6 +28,16 @@ def inputs(name):
 
 
 @functools.lru_cache(maxsize=None)
+def oracle_y(name):
+    """Selection + y only (no fit): cheap enough for the spawned multi-rank workers."""
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
+    perm, rank, nip, _ = R.select_interpolation_points(x0, cell.nao_nr(), c0)
+    xip = x0[:, perm, :]
+    phase = R.get_phase(cell.a, R.get_kpts(cell.a, kmesh), kmesh)
+    return dict(perm=perm, xip=xip, y=R.build_y(chi, xip, phase))
+
+
+@functools.lru_cache(maxsize=None)
 def oracle(name):
     cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
     perm, rank, nip, x4sel = R.select_interpolation_points(x0, cell.nao_nr(), c0)

@@ -1,0 +1,41 @@
+"""Worker for the multi-rank tests: one k-shard of the ISDF build + get_jk.
+
+Run as  RANK=r WORLD_SIZE=n MASTER_ADDR=127.0.0.1 MASTER_PORT=p python tests/dist_worker.py
+        <case> <backend> <out.npz>
+On the GPU pool several ranks share cuda:0 with the gloo backend (RCCL needs one GPU per
+rank; the driver's 8-GPU bench exercises RCCL itself)."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path[:0] = [ROOT, os.path.join(ROOT, "fft-isdf-scratch_amd"), HERE]
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    name, backend, out = sys.argv[1], sys.argv[2], sys.argv[3]
+    import torch
+    import torch.distributed as dist
+    from cases import inputs, oracle
+    from fisdf import ISDF
+    dist.init_process_group(backend)
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
+    o = oracle(name)
+    df = ISDF(cell, cell.get_kpts(kmesh), m0=list(m0), c0=c0, device=0,
+              comm=dist.group.WORLD)
+    d = df.device
+    df._kmesh()
+    df._ao_parent = d.to_dev(x0)
+    df._ao_grid = d.to_dev(chi)
+    df.build()
+    vj, vk = df.get_jk(dm)
+    np.savez(out, vj=vj, vk=vk, perm=df.perm, ranks=df.ranks, vj0=o["vj"], vk0=o["vk"],
+             perm0=o["perm"])
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
