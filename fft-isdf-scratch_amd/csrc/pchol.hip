@@ -161,6 +161,120 @@ __global__ void pchol_pick(int n, int rmax, int j, int* __restrict__ piv, double
   }
 }
 
+// ---- blocked variant (dpstrf-style): one workgroup per matrix factors a panel of NB
+// pivots with the panel held in registers (GEMV only over the panel's own columns), then
+// one batched ZGEMM applies the panel to the trailing matrix W -= L_panel L_panel^H.
+// 2 launches per NB pivots instead of 2 per pivot; trailing traffic 2|W| per panel.
+constexpr int PB_THREADS = 1024;
+
+template <int NB>
+__global__ __launch_bounds__(PB_THREADS) void pchol_panel(const cplx* __restrict__ W, long sW,
+                                                          int n, int rmax, int j0,
+                                                          cplx* __restrict__ L,
+                                                          int* __restrict__ piv,
+                                                          int* __restrict__ rank,
+                                                          double* __restrict__ d,
+                                                          int* __restrict__ flags,
+                                                          const double* __restrict__ thr) {
+  const int b = blockIdx.x;
+  if (flags[b]) return;
+  W += b * sW;
+  L += (long)b * n * rmax;
+  piv += (long)b * rmax;
+  d += (long)b * n;
+  __shared__ double s_v[PB_THREADS / 64];
+  __shared__ int s_i[PB_THREADS / 64];
+  __shared__ cplx s_lp[NB];
+  __shared__ int s_p, s_stop;
+  __shared__ double s_dp;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int i = tid;  // one row per thread (n <= PB_THREADS)
+  const bool live = i < n;
+  double dd = live ? d[i] : -1e300;
+  cplx lp[NB];
+#pragma unroll
+  for (int c = 0; c < NB; ++c) lp[c] = cmk(0, 0);
+  const double t = thr[b];
+  int jdone = j0;
+  bool stopped = false;
+  // lp[c] stays zero for columns not yet computed, so every dot runs over all NB columns and
+  // lp is only ever indexed with compile-time indices (no scratch)
+  for (int jj = 0; jj < NB; ++jj) {
+    const int j = j0 + jj;
+    if (!stopped && j < rmax) {
+      // arg-max of the residual diagonal, first index on ties (LAPACK MAXLOC)
+      double bv = live ? dd : -1e300;
+      int bi = live ? i : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        double ov = __shfl_xor(bv, o, 64);
+        int oi = __shfl_xor(bi, o, 64);
+        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      }
+      if (lane == 0) { s_v[wid] = bv; s_i[wid] = bi; }
+      __syncthreads();
+      if (wid == 0) {
+        bv = lane < PB_THREADS / 64 ? s_v[lane] : -1e300;
+        bi = lane < PB_THREADS / 64 ? s_i[lane] : 0x7fffffff;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          double ov = __shfl_xor(bv, o, 64);
+          int oi = __shfl_xor(bi, o, 64);
+          if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+        }
+        if (lane == 0) {
+          s_p = bi;
+          s_dp = bv;
+          s_stop = !(bv > t);
+          if (!s_stop) piv[j] = bi;
+        }
+      }
+      __syncthreads();
+      const int p = s_p;
+      const double dp = s_dp;
+      if (s_stop) {
+        stopped = true;
+      } else {
+        if (i == p) {
+#pragma unroll
+          for (int c = 0; c < NB; ++c) s_lp[c] = lp[c];
+        }
+        __syncthreads();
+        cplx l = cmk(0, 0);
+        if (live) {
+          const double sq = sqrt(dp);
+          if (i == p) {
+            l = cmk(sq, 0.0);
+            dd = -1e300;
+          } else if (dd > -1e299) {
+            cplx w = cconj(W[(long)p * n + i]);  // W[i][p] of the Hermitian trailing matrix
+#pragma unroll
+            for (int c = 0; c < NB; ++c) w = csub(w, cmul(lp[c], cconj(s_lp[c])));
+            l = cmk(w.x / sq, w.y / sq);
+            dd -= l.x * l.x + l.y * l.y;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < NB; ++c)
+          if (c == jj) lp[c] = l;
+        jdone = j + 1;
+        __syncthreads();  // s_lp reused by the next pivot
+      }
+    }
+  }
+  if (live) {
+    d[i] = dd;
+    cplx* Li = L + (long)i * rmax + j0;
+#pragma unroll
+    for (int c = 0; c < NB; ++c)
+      if (j0 + c < rmax) Li[c] = lp[c];
+  }
+  if (tid == 0) {
+    rank[b] = jdone;
+    if (stopped || jdone >= rmax) flags[b] = 1;
+  }
+}
+
 }  // namespace
 
 // pivot values are kept in `dmax0 + batch` (caller allocates 2*batch + batch*rmax doubles: see api)
@@ -175,6 +289,32 @@ int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int
   hipLaunchKernelGGL(pchol_init, dim3(batch), dim3(nt), 0, s, A, lda, sA, n, rmax, tol_rel,
                      tol_abs, piv, pval, rank, d, flags, thr);
   FISDF_HIP(hipGetLastError());
+  if (n <= PB_THREADS) {
+    // blocked: trailing copy W of A, panels of NB pivots, batched ZGEMM trailing updates
+    constexpr int NB = 32;
+    const long nn = (long)n * n;
+    cplx* W = nullptr;
+    FISDF_HIP(hipMallocAsync((void**)&W, sizeof(cplx) * nn * batch, s));
+    FISDF_HIP(hipMemcpy2DAsync(W, sizeof(cplx) * n, A, sizeof(cplx) * lda, sizeof(cplx) * n,
+                               (size_t)n * batch, hipMemcpyDeviceToDevice, s));
+    if (sA != (long)n * lda) {  // batch stride differs from a packed copy: copy per matrix
+      for (int bb = 0; bb < batch; ++bb)
+        FISDF_HIP(hipMemcpy2DAsync(W + bb * nn, sizeof(cplx) * n, A + bb * sA, sizeof(cplx) * lda,
+                                   sizeof(cplx) * n, n, hipMemcpyDeviceToDevice, s));
+    }
+    const cplx mone = cmk(-1, 0), one = cmk(1, 0);
+    for (int j0 = 0; j0 < rmax; j0 += NB) {
+      hipLaunchKernelGGL(pchol_panel<NB>, dim3(batch), dim3(PB_THREADS), 0, s, W, nn, n, rmax, j0,
+                         L, piv, rank, d, flags, thr);
+      FISDF_HIP(hipGetLastError());
+      const int kc = std::min(NB, rmax - j0);
+      if (j0 + kc < rmax)  // W -= L[:, j0:j0+kc] L[:, j0:j0+kc]^H
+        FISDF_TRY(zgemm(s, OP_N, OP_C, n, n, kc, mone, L + j0, rmax, (long)n * rmax, L + j0, rmax,
+                        (long)n * rmax, one, W, n, nn, batch));
+    }
+    FISDF_HIP(hipFreeAsync(W, s));
+    return 0;
+  }
   const int rows_per_block = 4;
   dim3 g((n + rows_per_block - 1) / rows_per_block, batch);
   for (int j = 0; j < rmax; ++j) {
