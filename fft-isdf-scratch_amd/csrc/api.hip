@@ -728,6 +728,50 @@ int fisdf_build_ws(fisdf_ctx* c, const void* Wqv, int q0, int q1, int nip, const
   return 0;
 }
 
+// ---- next-2: ISDF ERIs / ao2mo --------------------------------------------------
+// eri[i*n2+j][k*n4+l] = sum_IJ W_q[I,J] conj(A1[I,i]) A2[I,j] conj(A3[J,k]) A4[J,l],
+// A_s = X_{k_s} C_s (C_s = identity when d_C[s] is null -> AO integrals), q = k2 - k1
+// (identity of fftdf-with-k-lstsq.py:221-232).
+int fisdf_get_eri(fisdf_ctx* c, const void* Xv, int nip, int nao, const int kidx[4],
+                  const void* Wqv, const void* const* Cv, const int nmo[4], void* outv) {
+  FISDF_TRY(device_guard(c));
+  const cplx* X = (const cplx*)Xv;
+  int n[4];
+  for (int s = 0; s < 4; ++s) n[s] = Cv && Cv[s] ? nmo[s] : nao;
+  const long p12 = (long)n[0] * n[1], p34 = (long)n[2] * n[3];
+  Carver cv;
+  size_t oA[4];
+  for (int s = 0; s < 4; ++s) oA[s] = cv.take(sizeof(cplx) * (size_t)nip * n[s]);
+  size_t oP12 = cv.take(sizeof(cplx) * nip * p12);
+  size_t oP34 = cv.take(sizeof(cplx) * nip * p34);
+  size_t oT = cv.take(sizeof(cplx) * nip * p34);
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  char* b = (char*)base;
+  const cplx* A[4];
+  for (int s = 0; s < 4; ++s) {
+    const cplx* Xk = X + (long)kidx[s] * nip * nao;
+    if (Cv && Cv[s]) {
+      cplx* As = (cplx*)(b + oA[s]);
+      FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nip, n[s], nao, ONE, Xk, nao, 0,
+                      (const cplx*)Cv[s], n[s], 0, ZERO, As, n[s], 0, 1));
+      A[s] = As;
+    } else {
+      A[s] = Xk;
+    }
+  }
+  cplx* P12 = (cplx*)(b + oP12);
+  cplx* P34 = (cplx*)(b + oP34);
+  cplx* T = (cplx*)(b + oT);
+  FISDF_TRY(pair_product(c->stream, A[0], n[0], A[1], n[1], nip, P12));
+  FISDF_TRY(pair_product(c->stream, A[2], n[2], A[3], n[3], nip, P34));
+  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nip, (int)p34, nip, ONE, (const cplx*)Wqv, nip, 0, P34,
+                  p34, 0, ZERO, T, p34, 0, 1));
+  FISDF_TRY(zgemm(c->stream, OP_T, OP_N, (int)p12, (int)p34, nip, ONE, P12, p12, 0, T, p34, 0,
+                  ZERO, (cplx*)outv, p34, 0, 1));
+  return 0;
+}
+
 // ---- A7 -----------------------------------------------------------------------
 int fisdf_get_j(fisdf_ctx* c, const void* Xv, const void* W0, const void* dmsv, int nset, int nk,
                 int nip, int nao, void* vjv) {

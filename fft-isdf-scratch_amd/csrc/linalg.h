@@ -33,5 +33,6 @@ int gather_points(hipStream_t s, const cplx* x0, int nk, int ng0, int nao, const
                   int nip, cplx* X);
 int square_scale(hipStream_t s, const cplx* in, double sc, cplx* out, long n);
 int permute_kgm(hipStream_t s, const cplx* x0, int nq, int ng, int nao, cplx* out);
+int pair_product(hipStream_t s, const cplx* A, int n1, const cplx* B, int n2, int nip, cplx* P);
 
 }  // namespace fisdf

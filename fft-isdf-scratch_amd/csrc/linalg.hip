@@ -202,6 +202,18 @@ __global__ void scale_rows_kernel(const cplx* __restrict__ X, const cplx* __rest
   Xv[e] = cmul(v[(long)x * nip + I], X[r]);
 }
 
+// pair densities at the interpolation points: P[I][i*n2 + j] = conj(A[I][i]) * B[I][j]
+__global__ void pair_product_kernel(const cplx* __restrict__ A, int n1, const cplx* __restrict__ B,
+                                    int n2, int nip, cplx* __restrict__ P) {
+  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long tot = (long)nip * n1 * n2;
+  if (e >= tot) return;
+  const int j = (int)(e % n2);
+  const int i = (int)((e / n2) % n1);
+  const int I = (int)(e / ((long)n1 * n2));
+  P[e] = cmul(cconj(A[(long)I * n1 + i]), B[(long)I * n2 + j]);
+}
+
 // out[g][q*nao + m] = x0[q][g][m]   (k-point axis folded into the GEMM K dimension)
 __global__ void permute_kgm_kernel(const cplx* __restrict__ x0, int nq, int ng, int nao,
                                    cplx* __restrict__ out) {
@@ -382,6 +394,15 @@ int scale_rows(hipStream_t s, const cplx* X, const cplx* v, int nset, int nk, in
   if (n == 0) return 0;
   hipLaunchKernelGGL(scale_rows_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, X, v,
                      nset, nk, nip, nao, Xv);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int pair_product(hipStream_t s, const cplx* A, int n1, const cplx* B, int n2, int nip, cplx* P) {
+  long n = (long)nip * n1 * n2;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(pair_product_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, A, n1,
+                     B, n2, nip, P);
   FISDF_HIP(hipGetLastError());
   return 0;
 }

@@ -239,6 +239,75 @@ class InterpolativeSeparableDensityFitting:
             vj = get_j_kpts(self, dm, hermi, kpts, kpts_band)
         return vj, vk
 
+    # ---- 4-index integrals (north-star get_eri / ao2mo surface; next-2 of SURVEY §8f) ----
+    def _kidx(self, kpts):
+        """Indices of k-points on the mesh (scaled coordinates modulo 1)."""
+        kmesh = np.asarray(self._kmesh())
+        scaled = np.asarray(kpts, float).reshape(-1, 3) @ self.cell.lattice_vectors().T / (2 * np.pi)
+        v = np.rint(scaled * kmesh).astype(int) % kmesh
+        if abs(scaled * kmesh - np.rint(scaled * kmesh)).max() > 1e-6:
+            raise ValueError("k-points are not on the ISDF k-mesh")
+        return ((v[:, 0] * kmesh[1] + v[:, 1]) * kmesh[2] + v[:, 2]).astype(np.int32), v
+
+    def _w_of_q(self, q):
+        st = self._dev_state
+        d = self.device
+        if d.size == 1:
+            return st["Wq"][q]
+        q0, q1 = d.shard(int(np.prod(self.kmesh)))
+        if q0 <= q < q1:
+            return st["Wq"][q - q0]
+        return d.to_dev(self._wq[q])
+
+    def ao2mo(self, mo_coeffs, kpts=None, compact=False):
+        """ISDF (ij|kl) for four k-points: eri[ij, kl] = sum_IJ W_q[I,J] conj(XC1)[I,i] (XC2)[I,j]
+        conj(XC3)[J,k] (XC4)[J,l], q = k2 - k1 (fftdf-with-k-lstsq.py:221-232).  Mirrors
+        FFTDF.ao2mo(mo_coeffs, kpts, compact) [pyscf]; mo_coeffs None -> AO integrals."""
+        st = self._dev_state
+        assert st is not None and "Wq" in st, "call build() first"
+        d = self.device
+        kpts = np.zeros((4, 3)) if kpts is None else np.asarray(kpts, float).reshape(-1, 3)
+        if kpts.shape[0] == 1:
+            kpts = np.repeat(kpts, 4, axis=0)
+        kidx, v = self._kidx(kpts)
+        kmesh = np.asarray(self.kmesh)
+        if np.any((v[0] - v[1] + v[2] - v[3]) % kmesh):
+            raise ValueError("k-points violate momentum conservation k1 - k2 + k3 - k4 = G")
+        qv = (v[1] - v[0]) % kmesh
+        q = int((qv[0] * kmesh[1] + qv[1]) * kmesh[2] + qv[2])
+        nao = self.cell.nao_nr()
+        nip = st["X"].shape[1]
+        W = self._w_of_q(q).contiguous()
+        if mo_coeffs is None:
+            Cs = [None] * 4
+        elif isinstance(mo_coeffs, np.ndarray) and mo_coeffs.ndim == 2:
+            Cs = [mo_coeffs] * 4
+        else:
+            Cs = list(mo_coeffs)
+        nmo = [nao if c is None else np.asarray(c).shape[1] for c in Cs]
+        dC = [None if c is None else d.to_dev(np.asarray(c, dtype=np.complex128)) for c in Cs]
+        ptrs = (_lib._vp * 4)(*[None if t is None else t.data_ptr() for t in dC])
+        out = d.empty((nmo[0] * nmo[1], nmo[2] * nmo[3]))
+        kk, kp = _lib.iarr(kidx)
+        nn, np_ = _lib.iarr(nmo)
+        d.ctx.call("fisdf_get_eri", _lib.ptr(st["X"]), nip, nao, kp, _lib.ptr(W), ptrs, np_,
+                   _lib.ptr(out))
+        eri = out.cpu().numpy()
+        if abs(kpts).max() < 1e-9 and all(c is None or np.isrealobj(c) for c in Cs):
+            eri = eri.real
+            if compact and nmo[0] == nmo[1] and nmo[2] == nmo[3]:
+                i0, i1 = np.tril_indices(nmo[0])
+                k0, k1 = np.tril_indices(nmo[2])
+                e4 = eri.reshape(nmo[0], nmo[1], nmo[2], nmo[3])
+                eri = e4[i0, i1][:, k0, k1]
+        return eri
+
+    def get_eri(self, kpts=None, compact=False):
+        """AO ERIs for four k-points (FFTDF.get_eri surface [pyscf]), ISDF-factorised."""
+        return self.ao2mo(None, kpts, compact)
+
+    get_ao_eri = get_eri
+
     # reference attributes, materialised on demand from HBM
     def __getattribute__(self, name):
         if name in ("_x", "_w0", "_wq"):
@@ -312,17 +381,22 @@ def build(df_obj):
             fptr = _lib._vp(f.data_ptr() + g0 * nao * f.element_size())
             d.ctx.call("fisdf_build_y", fptr, ngrid * nao, 0, ng, ng, _lib.ptr(X), nip, nao,
                        km_p, a_p, 0, nk, _lib.ptr(send))
-        recv = kshard.exchange_y(send, nk, nip, slices, d.rank, d.size, d.comm)
+        # the all-to-all runs on the collective stream while this rank factorises its x4_q
+        recv, work = kshard.exchange_y(send, nk, nip, slices, d.rank, d.size, d.comm,
+                                       async_op=True)
+
+    ranks = np.zeros(q1 - q0, np.int32)
+    d.ctx.call("fisdf_factor_x4", _lib.ptr(x4), q0, q1, nip, float(df_obj.fit_tol),
+               ranks.ctypes.data_as(_lib._ip))
+    if d.size > 1:
+        if work is not None:
+            work.wait()
         del send
         g0s = (C_long * d.size)(*[s[0] for s in slices])
         ngs = (C_long * d.size)(*[s[1] for s in slices])
         d.ctx.call("fisdf_unpack_slices", _lib.ptr(recv), (q1 - q0) * nip, d.size, g0s, ngs,
                    ngrid, _lib.ptr(yT))
         del recv
-
-    ranks = np.zeros(q1 - q0, np.int32)
-    d.ctx.call("fisdf_factor_x4", _lib.ptr(x4), q0, q1, nip, float(df_obj.fit_tol),
-               ranks.ctypes.data_as(_lib._ip))
     Wq = d.empty((q1 - q0, nip, nip))
     d.ctx.call("fisdf_fit_coulomb", q0, q1, _lib.ptr(yT), nip, mesh_p, km_p, a_p, _lib.ptr(Wq))
     del yT

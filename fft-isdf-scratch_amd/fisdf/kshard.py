@@ -47,10 +47,12 @@ def grid_slices(mesh, size: int):
     return out
 
 
-def exchange_y(send, nk: int, nip: int, slices, rank: int, size: int, group=None):
+def exchange_y(send, nk: int, nip: int, slices, rank: int, size: int, group=None,
+               async_op: bool = False):
     """All-to-all of the grid-sliced y: `send` is (nk, nip, ng_rank) = y_q on this rank's
     slice for every q; the q-blocks are contiguous, so block r of the send buffer is rank
-    r's q-shard.  Returns recv = concat_p (nq_self, nip, ng_p) in rank order p."""
+    r's q-shard.  Returns recv = concat_p (nq_self, nip, ng_p) in rank order p
+    (with async_op: (recv, work) — call work.wait() before reading recv; work may be None)."""
     import torch
     import torch.distributed as dist
     ng_self = slices[rank][1]
@@ -59,15 +61,17 @@ def exchange_y(send, nk: int, nip: int, slices, rank: int, size: int, group=None
     in_splits = [(b - a) * nip * ng_self for a, b in (shard_range(nk, r, size) for r in range(size))]
     out_splits = [nq * nip * slices[p][1] for p in range(size)]
     if _host_staged(group, send):
-        return exchange_y(send.cpu(), nk, nip, slices, rank, size, group).to(send.device)
+        recv = exchange_y(send.cpu(), nk, nip, slices, rank, size, group).to(send.device)
+        return (recv, None) if async_op else recv
     recv = torch.empty(sum(out_splits), dtype=send.dtype, device=send.device)
     flat = send.reshape(-1)
     if send.is_complex():
-        dist.all_to_all_single(torch.view_as_real(recv), torch.view_as_real(flat), out_splits,
-                               in_splits, group=group)
+        work = dist.all_to_all_single(torch.view_as_real(recv), torch.view_as_real(flat),
+                                      out_splits, in_splits, group=group, async_op=async_op)
     else:
-        dist.all_to_all_single(recv, flat, out_splits, in_splits, group=group)
-    return recv
+        work = dist.all_to_all_single(recv, flat, out_splits, in_splits, group=group,
+                                      async_op=async_op)
+    return (recv, work) if async_op else recv
 
 
 def _host_staged(group, *tensors):

@@ -134,6 +134,14 @@ int fisdf_get_j(fisdf_ctx* ctx, const void* d_X, const void* d_W0, const void* d
 int fisdf_get_k(fisdf_ctx* ctx, const void* d_X, const void* d_Ws, const void* d_dms, int nset,
                 int nip, int nao, const int kmesh[3], const double a[9], void* d_vk);
 
+/* ---- ISDF 4-index integrals (get_eri / ao2mo surface) --------------------------
+ * eri[i*n2+j][k*n4+l] = sum_IJ W_q[I,J] conj(A1[I,i]) A2[I,j] conj(A3[J,k]) A4[J,l] with
+ * A_s = X_{kidx[s]} C_s, q = k2 - k1 (fftdf-with-k-lstsq.py:221-232).  d_Wq: the (nip,nip)
+ * W of that q; h_dC: host array of 4 DEVICE pointers to (nao, nmo[s]) MO coefficients, or
+ * NULL (or NULL entries) for AO integrals.  d_out: (n1*n2, n3*n4) c128. */
+int fisdf_get_eri(fisdf_ctx* ctx, const void* d_X, int nip, int nao, const int kidx[4],
+                  const void* d_Wq, const void* const* h_dC, const int nmo[4], void* d_out);
+
 /* ---- building blocks exported for tests / other callers -------------------- */
 /* C[b] = alpha op(A[b]) op(B[b]) + beta C[b]; op: 0 N, 1 T, 2 conj, 3 conj-transpose */
 int fisdf_zgemm(fisdf_ctx* ctx, int opA, int opB, int M, int N, int K, const double alpha[2],

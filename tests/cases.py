@@ -13,6 +13,11 @@ CASES = {
     "toy331": (lambda: C.toy_cell(mesh=(15, 15, 15)), (3, 3, 1), (9, 9, 9), 40.0),
     "diamond_szv_gamma": (lambda: C.diamond_cell(basis="gth-szv", mesh=(8, 8, 8)), (1, 1, 1),
                           (15, 15, 15), 20.0),
+    # C4-shaped: NiO AFM (nio-afm.vasp), dzvp-molopt-sr-shaped basis with f shells (nao 76);
+    # reduced mesh/k-mesh so the gelsy oracle runs in seconds
+    "nio_small": (lambda: C.nio_cell(mesh=(16, 16, 16)), (1, 1, 2), (9, 9, 9), 5.0),
+    # C5-shaped: Si 2x2x2 diamond supercell, 16 atoms, szv-shaped (nao 64), Gamma only
+    "si_small": (lambda: C.si_supercell(mesh=(12, 12, 12)), (1, 1, 1), (9, 9, 9), 8.0),
 }
 
 

@@ -29,7 +29,7 @@ def make_df(name, inject=True):
     return df, o, dm
 
 
-@pytest.mark.parametrize("name", ["toy222", "toy331", "diamond_szv_gamma"])
+@pytest.mark.parametrize("name", ["toy222", "toy331", "diamond_szv_gamma", "nio_small", "si_small"])
 def test_jk_parity_vs_oracle(name):
     df, o, dm = make_df(name)
     df.build()
@@ -94,3 +94,44 @@ def test_not_implemented_paths():
         df.get_jk(dm, exxdiv="ewald")
     with pytest.raises(NotImplementedError):
         df.get_jk(dm[0, 0], kpts=np.zeros(3))
+
+
+def test_get_eri_and_ao2mo():
+    """next-2: ISDF ERIs vs the exact FFT ERI (fftdf-with-k-lstsq.py:219-258 harness: fails
+    above 1e-4) and vs the oracle's ISDF ERI; ao2mo with MO coefficients == transformed AO ERI."""
+    from oracle import exact_ref as E, isdf_ref as R
+    from fisdf.cell import cartesian_prod
+    df, o, dm = make_df("toy222")
+    df.build()
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs("toy222")
+    kpts = R.get_kpts(cell.a, kmesh)
+    ks = cartesian_prod([np.arange(n) for n in kmesh])
+    nao = cell.nao_nr()
+
+    def kidx(v):
+        v = np.mod(v, kmesh)
+        return int((v[0] * kmesh[1] + v[1]) * kmesh[2] + v[2])
+
+    x = o["xip"]
+    for (k1, k2, k3) in [(0, 0, 0), (0, 1, 2), (3, 5, 6), (7, 7, 1)]:
+        q = kidx(ks[k2] - ks[k1])
+        k4 = kidx(ks[k1] - ks[k2] + ks[k3])
+        eri = df.get_eri(kpts[[k1, k2, k3, k4]]).reshape(nao, nao, nao, nao)
+        ex = E.exact_eri(chi, cell.a, cell.mesh, kpts, coords, k1, k2, k3, k4)
+        ref = np.einsum("IJ,Im,In,Jk,Jl->mnkl", o["wq"][q], x[k1].conj(), x[k2], x[k3].conj(),
+                        x[k4], optimize=True)
+        print(k1, k2, k3, k4, "vs exact", abs(eri - ex).max(), "vs oracle ISDF", abs(eri - ref).max())
+        assert abs(eri - ex).max() < 1e-6
+        assert abs(eri - ref).max() < 1e-7
+    # ao2mo with random MO coefficients equals the AO ERI transformed on the host
+    rng = np.random.default_rng(3)
+    C = [rng.standard_normal((nao, n)) + 1j * rng.standard_normal((nao, n)) for n in (3, 4, 2, 5)]
+    k4 = kidx(ks[3] - ks[5] + ks[6])
+    kq = kpts[[3, 5, 6, k4]]
+    ao = df.get_eri(kq).reshape(nao, nao, nao, nao)
+    mo = df.ao2mo(C, kq).reshape(3, 4, 2, 5)
+    ref = np.einsum("mnkl,mi,nj,ka,lb->ijab", ao, C[0].conj(), C[1], C[2].conj(), C[3],
+                    optimize=True)
+    assert abs(mo - ref).max() < 1e-10 * max(1.0, abs(ref).max())
+    with pytest.raises(ValueError):
+        df.get_eri(kpts[[0, 1, 1, 3]])   # violates k1 - k2 + k3 - k4 = G
