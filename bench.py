@@ -25,15 +25,19 @@ for _p in (ROOT, os.path.join(ROOT, "fft-isdf-scratch_amd")):
 import numpy as np  # noqa: E402
 
 CONFIGS = {
-    # name: (basis, mesh, kmesh, m0, nip)
-    "c3": ("gth-dzvp", (36, 36, 36), (4, 4, 4), (15, 15, 15), 600),
-    "c2": ("gth-dzvp", (36, 36, 36), (2, 2, 2), (15, 15, 15), 300),
-    "c1": ("gth-szv", (8, 8, 8), (1, 1, 1), (15, 15, 15), 160),
+    # name: (cell, basis, mesh, kmesh, m0, nip)   
+    "c3": ("diamond", "gth-dzvp", (36, 36, 36), (4, 4, 4), (15, 15, 15), 600),
+    "c2": ("diamond", "gth-dzvp", (36, 36, 36), (2, 2, 2), (15, 15, 15), 300),
+    "c1": ("diamond", "gth-szv", (8, 8, 8), (1, 1, 1), (15, 15, 15), 160),
+    "c4": ("nio", "gth-dzvp-molopt-sr", (32, 32, 32), (2, 2, 2), (15, 15, 15), 1000),
+    "c5": ("si", "gth-szv", (30, 30, 30), (1, 1, 1), (15, 15, 15), 2000),
 }
 DESC = {
     "c3": "diamond gth-dzvp-shaped, 4x4x4 k-mesh, nip 600, mesh 36^3 (C3)",
     "c2": "diamond gth-dzvp-shaped, 2x2x2 k-mesh, nip 300, mesh 36^3 (C2)",
     "c1": "diamond gth-szv-shaped, Gamma, nip 160, mesh 8^3 (C1)",
+    "c4": "NiO AFM (nio-afm.vasp) dzvp-molopt-sr-shaped, 2x2x2, nip 1000, mesh 32^3 (C4)",
+    "c5": "Si 2x2x2 supercell (16 atoms) szv-shaped, Gamma, nip 2000, mesh 30^3 (C5)",
 }
 PEAK_FP64_TFLOPS = 78.6  # MI355X FP64 matrix (= vector) dense peak, MI355X_MICROARCH / BASELINE.md
 
@@ -51,8 +55,9 @@ def parse():
 
 def setup(cfg):
     from fisdf import cell as C
-    basis, mesh, kmesh, m0, nip = CONFIGS[cfg]
-    cell = C.diamond_cell(basis=basis, mesh=mesh)
+    kind, basis, mesh, kmesh, m0, nip = CONFIGS[cfg]
+    make = {"diamond": C.diamond_cell, "nio": C.nio_cell, "si": C.si_supercell}[kind]
+    cell = make(basis=basis, mesh=mesh)
     nao = cell.nao_nr()
     c0 = (nip + 0.5) / nao                                    # int(nao*c0) == nip
     x0 = C.eval_ao_kpts(cell, cell.gen_uniform_grids(m0), kmesh)

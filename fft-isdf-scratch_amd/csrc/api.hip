@@ -556,12 +556,12 @@ int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk
     // fx_k^T = X_k f_k^H  -> FX[k][I][g]   (:76, transposed layout)
     FISDF_TRY(zgemm(c->stream, OP_N, OP_C, nip, m, nao, ONE, X, nao, (long)nip * nao,
                     f + (long)s0 * nao, nao, f_kstride, ZERO, FX, m, nm, nk));
-    // fx_s = Phi fx_k (:79), real (:81, monitored), y_s = fx_s^2 (:83) fused in the epilogue
-    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nm, nk, ONE, phase, nk, 0, FX, nm, 0, ZERO, FS, nm,
-                    0, 1, 1, nullptr, EPI_SQUARE_RE, c->maximag + 1));
-    // y_k = Phi^T y_s (:84) for the shard's k rows, scattered into yT[k-q0][I][g0+s0+g] (:85)
-    FISDF_TRY(zgemm(c->stream, OP_T, OP_N, q1 - q0, m, nk, ONE, phase + q0, nk, 0, FS, nm, m,
-                    ZERO, yT + g0 + s0, (long)nip * ngrid, ngrid, nip));
+    // fx_s = Phi fx_k (:79, real :81), y_s = fx_s^2 (:83), y_k = Phi^T y_s (:84) for the
+    // shard's q, written into yT[q-q0][I][g0+s0+g] (:85): separable k-mesh DFTs in LDS
+    FISDF_TRY(kmesh_y(c->stream, FX, nm, kmesh, q0, q1, m, yT, (long)nip * ngrid, ngrid,
+                      (long)g0 + s0, c->maximag + 1));
+    (void)FS;
+    (void)phase;
   }
   return 0;
 }

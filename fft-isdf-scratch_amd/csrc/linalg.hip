@@ -202,6 +202,211 @@ __global__ void scale_rows_kernel(const cplx* __restrict__ X, const cplx* __rest
   Xv[e] = cmul(v[(long)x * nip + I], X[r]);
 }
 
+// ---- y build, k-mesh part (fftisdf.py:79-85) -----------------------------------------
+// Phi = exp(i T_R.k)/sqrt(nk) is separable over the k-mesh axes, so
+// fx_s = Phi fx_k and y_k = Phi^T y_s are 3-D inverse-sign DFTs of length kmesh along the
+// k index of every (I, g) column.  One workgroup takes CT columns: the nk x CT tile is
+// staged in LDS (coalesced over columns), transformed axis by axis (direct n_a-point
+// DFTs, n_a <= 16), squared (real part; max|Im| monitored = fftisdf.py:81), transformed
+// again, and the q-shard rows are written straight into yT[q-q0][I][g] — one HBM pass
+// instead of two dense nk x nk GEMMs with an intermediate.
+constexpr int KM_MAXN = 16;
+
+__device__ void kmesh_axis_dft(cplx* T, int CT, int ld, int nk, int na, int stride,
+                               const cplx* __restrict__ w, int tid, int nthr) {
+  // lines: all k with k_a == 0 along this axis, for each column
+  const int nlines = nk / na;
+  const int items = nlines * CT;
+  for (int it = tid; it < items; it += nthr) {
+    const int c = it % CT;
+    const int line = it / CT;
+    // base k index of the line: decompose line over the other axes (k = hi*na*stride + j*stride + lo)
+    const int lo = line % stride;
+    const int hi = line / stride;
+    const int base = hi * na * stride + lo;
+    cplx out[KM_MAXN];
+#pragma unroll
+    for (int x = 0; x < KM_MAXN; ++x) {
+      cplx acc = cmk(0, 0);
+      if (x < na) {
+        for (int j = 0; j < na; ++j)
+          acc = cadd(acc, cmul(T[(base + j * stride) * ld + c], w[(x * j) % na]));
+      }
+      out[x] = acc;
+    }
+#pragma unroll
+    for (int x = 0; x < KM_MAXN; ++x)
+      if (x < na) T[(base + x * stride) * ld + c] = out[x];
+  }
+}
+
+__global__ __launch_bounds__(256) void kmesh_y_kernel(
+    const cplx* __restrict__ FX, long ncol, int nk, int n0, int n1, int n2, int q0, int q1,
+    int m, cplx* __restrict__ yT, long qs, long Is, long goff, int CT,
+    unsigned long long* __restrict__ mon) {
+  extern __shared__ cplx sm[];
+  cplx* w0 = sm;
+  cplx* w1 = sm + KM_MAXN;
+  cplx* w2 = sm + 2 * KM_MAXN;
+  cplx* T = sm + 3 * KM_MAXN;
+  const int ld = CT + 1;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int ns[3] = {n0, n1, n2};
+  for (int a = 0; a < 3; ++a) {
+    cplx* w = a == 0 ? w0 : (a == 1 ? w1 : w2);
+    for (int t = tid; t < ns[a]; t += nthr) {
+      double s, cc;
+      sincospi(2.0 * t / ns[a], &s, &cc);  // exp(+2 pi i t / n_a)
+      w[t] = cmk(cc, s);
+    }
+  }
+  const double sc = 1.0 / sqrt((double)nk);
+  const long ntiles = (ncol + CT - 1) / CT;
+  // persistent over column tiles: twiddles once, U loads in flight per thread
+  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  const long c0 = tile * CT;
+  constexpr int U = 8;
+  const int tot = nk * CT;
+  for (int e0 = 0; e0 < tot; e0 += U * nthr) {
+    cplx v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * nthr + tid;
+      const int k = e / CT, c = e % CT;
+      const long col = c0 + c;
+      const bool ok = e < tot && col < ncol;
+      v[u] = FX[ok ? (long)k * ncol + col : 0];
+      if (!ok) v[u] = cmk(0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * nthr + tid;
+      if (e < tot) T[(e / CT) * ld + (e % CT)] = v[u];
+    }
+  }
+  __syncthreads();
+  // fx_s = Phi fx_k
+  kmesh_axis_dft(T, CT, ld, nk, n0, n1 * n2, w0, tid, nthr);
+  __syncthreads();
+  kmesh_axis_dft(T, CT, ld, nk, n1, n2, w1, tid, nthr);
+  __syncthreads();
+  kmesh_axis_dft(T, CT, ld, nk, n2, 1, w2, tid, nthr);
+  __syncthreads();
+  // y_s = Re(fx_s)^2  (fx_s is real: fftisdf.py:81)
+  double mi = 0.0;
+  for (int e = tid; e < nk * CT; e += nthr) {
+    const int k = e / CT, c = e % CT;
+    cplx v = T[k * ld + c];
+    const double re = v.x * sc;
+    mi = fmax(mi, fabs(v.y * sc));
+    T[k * ld + c] = cmk(re * re, 0.0);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mi = fmax(mi, __shfl_xor(mi, o, 64));
+  if ((tid & 63) == 0 && mon) atomicMax(mon, (unsigned long long)__double_as_longlong(mi));
+  __syncthreads();
+  // y_k = Phi^T y_s  (Phi symmetric in R <-> k)
+  kmesh_axis_dft(T, CT, ld, nk, n0, n1 * n2, w0, tid, nthr);
+  __syncthreads();
+  kmesh_axis_dft(T, CT, ld, nk, n1, n2, w1, tid, nthr);
+  __syncthreads();
+  kmesh_axis_dft(T, CT, ld, nk, n2, 1, w2, tid, nthr);
+  __syncthreads();
+  const int nq = q1 - q0;
+  for (int e = tid; e < nq * CT; e += nthr) {
+    const int qq = e / CT, c = e % CT;
+    const long col = c0 + c;
+    if (col < ncol) {
+      const long I = col / m, g = col % m;
+      cplx v = T[(q0 + qq) * ld + c];
+      yT[qq * qs + I * Is + goff + g] = cmk(v.x * sc, v.y * sc);
+    }
+  }
+  __syncthreads();  // T is reloaded by the next tile
+  }
+}
+
+// Register variant for the common k-meshes (compile-time N0 x N1 x N2): one thread per
+// column holds all NK k-values, so the NK loads of a column are in flight together and the
+// separable DFTs are straight-line code with compile-time twiddle indices.
+template <int N, int S, int NK>
+__device__ __forceinline__ void reg_axis_dft(cplx* v, const cplx* tw) {
+#pragma unroll
+  for (int hi = 0; hi < NK / (N * S); ++hi)
+#pragma unroll
+    for (int lo = 0; lo < S; ++lo) {
+      cplx* p = v + hi * N * S + lo;
+      if constexpr (N == 2) {
+        const cplx a = p[0], b = p[S];
+        p[0] = cadd(a, b);
+        p[S] = csub(a, b);
+      } else if constexpr (N == 4) {  // exp(+2 pi i xj/4): multiplications by +-i are swaps
+        const cplx a = p[0], b = p[S], c = p[2 * S], d = p[3 * S];
+        const cplx s0 = cadd(a, c), d0 = csub(a, c), s1 = cadd(b, d), d1 = csub(b, d);
+        const cplx id1 = cmk(-d1.y, d1.x);  // i * (b - d)
+        p[0] = cadd(s0, s1);
+        p[S] = cadd(d0, id1);
+        p[2 * S] = csub(s0, s1);
+        p[3 * S] = csub(d0, id1);
+      } else if constexpr (N > 1) {
+        cplx u[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) u[j] = p[j * S];
+#pragma unroll
+        for (int x = 0; x < N; ++x) {
+          cplx acc = u[0];
+#pragma unroll
+          for (int j = 1; j < N; ++j) acc = cadd(acc, cmul(u[j], tw[(x * j) % N]));
+          p[x * S] = acc;
+        }
+      }
+    }
+}
+
+template <int N0, int N1, int N2>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void kmesh_y_reg_kernel(
+    const cplx* __restrict__ FX, int ncol, int q0, int q1, int m, cplx* __restrict__ yT, long qs,
+    long Is, long goff, unsigned long long* __restrict__ mon) {
+  constexpr int NK = N0 * N1 * N2;
+  cplx tw0[N0], tw1[N1], tw2[N2];
+#pragma unroll
+  for (int t = 0; t < N0; ++t) { double s, c; sincospi(2.0 * t / N0, &s, &c); tw0[t] = cmk(c, s); }
+#pragma unroll
+  for (int t = 0; t < N1; ++t) { double s, c; sincospi(2.0 * t / N1, &s, &c); tw1[t] = cmk(c, s); }
+#pragma unroll
+  for (int t = 0; t < N2; ++t) { double s, c; sincospi(2.0 * t / N2, &s, &c); tw2[t] = cmk(c, s); }
+  const double sc = 1.0 / sqrt((double)NK);
+  double mi = 0.0;
+  for (int col = blockIdx.x * blockDim.x + threadIdx.x; col < ncol; col += gridDim.x * blockDim.x) {
+    cplx v[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) v[k] = FX[(long)k * ncol + col];
+    // fx_s = Phi fx_k (fftisdf.py:79)
+    reg_axis_dft<N0, N1 * N2, NK>(v, tw0);
+    reg_axis_dft<N1, N2, NK>(v, tw1);
+    reg_axis_dft<N2, 1, NK>(v, tw2);
+    // y_s = fx_s^2, fx_s real (fftisdf.py:81,83)
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const double re = v[k].x * sc;
+      mi = fmax(mi, fabs(v[k].y * sc));
+      v[k] = cmk(re * re, 0.0);
+    }
+    // y_k = Phi^T y_s (fftisdf.py:84)
+    reg_axis_dft<N0, N1 * N2, NK>(v, tw0);
+    reg_axis_dft<N1, N2, NK>(v, tw1);
+    reg_axis_dft<N2, 1, NK>(v, tw2);
+    const unsigned I = (unsigned)col / (unsigned)m, g = (unsigned)col - I * (unsigned)m;
+    cplx* out = yT + (long)I * Is + goff + g;
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+      if (k >= q0 && k < q1) out[(long)(k - q0) * qs] = cmk(v[k].x * sc, v[k].y * sc);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mi = fmax(mi, __shfl_xor(mi, o, 64));
+  if ((threadIdx.x & 63) == 0 && mon) atomicMax(mon, (unsigned long long)__double_as_longlong(mi));
+}
+
 // pair densities at the interpolation points: P[I][i*n2 + j] = conj(A[I][i]) * B[I][j]
 __global__ void pair_product_kernel(const cplx* __restrict__ A, int n1, const cplx* __restrict__ B,
                                     int n2, int nip, cplx* __restrict__ P) {
@@ -394,6 +599,39 @@ int scale_rows(hipStream_t s, const cplx* X, const cplx* v, int nset, int nk, in
   if (n == 0) return 0;
   hipLaunchKernelGGL(scale_rows_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, X, v,
                      nset, nk, nip, nao, Xv);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], int q0, int q1, int m,
+            cplx* yT, long qs, long Is, long goff, unsigned long long* mon) {
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  FISDF_CHECK(kmesh[0] <= KM_MAXN && kmesh[1] <= KM_MAXN && kmesh[2] <= KM_MAXN,
+              "kmesh_y: k-mesh axes must be <= 16");
+  if (ncol < (1L << 31)) {
+    const int nc = (int)ncol;
+    const unsigned grid = (unsigned)std::max<long>(1, std::min<long>((ncol + 63) / 64, 32768));
+#define FISDF_KM(a, b, c)                                                                      \
+  if (kmesh[0] == a && kmesh[1] == b && kmesh[2] == c) {                                       \
+    hipLaunchKernelGGL((kmesh_y_reg_kernel<a, b, c>), dim3(grid), dim3(64), 0, s, FX, nc, q0,   \
+                       q1, m, yT, qs, Is, goff, mon);                                          \
+    FISDF_HIP(hipGetLastError());                                                              \
+    return 0;                                                                                  \
+  }
+    FISDF_KM(1, 1, 1) FISDF_KM(1, 1, 2) FISDF_KM(2, 2, 2) FISDF_KM(3, 3, 1) FISDF_KM(3, 3, 3)
+    FISDF_KM(4, 4, 4) FISDF_KM(2, 2, 1) FISDF_KM(1, 2, 2) FISDF_KM(4, 4, 1) FISDF_KM(2, 2, 4)
+#undef FISDF_KM
+  }
+  int CT = 64;
+  while (CT > 8 && sizeof(cplx) * ((size_t)nk * (CT + 1) + 3 * KM_MAXN) > 64 * 1024) CT /= 2;
+  const size_t lds = sizeof(cplx) * ((size_t)nk * (CT + 1) + 3 * KM_MAXN);
+  FISDF_CHECK(lds <= 160 * 1024, "kmesh_y: k-mesh too large for the LDS tile");
+  const long tiles = (ncol + CT - 1) / CT;
+  FISDF_CHECK(tiles < (1L << 31), "kmesh_y: too many columns");
+  if (tiles == 0) return 0;
+  const unsigned grid = (unsigned)std::min<long>(tiles, 4096);
+  hipLaunchKernelGGL(kmesh_y_kernel, dim3(grid), dim3(256), lds, s, FX, ncol, nk,
+                     kmesh[0], kmesh[1], kmesh[2], q0, q1, m, yT, qs, Is, goff, CT, mon);
   FISDF_HIP(hipGetLastError());
   return 0;
 }
