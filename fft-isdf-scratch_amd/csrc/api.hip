@@ -31,7 +31,8 @@ struct fisdf_ctx {
   // phase matrices Phi (nimg x nk) keyed by kmesh + lattice
   std::map<std::vector<double>, cplx*> phase_cache;
   // per-q factors of x4_q (fisdf_factor_x4)
-  int f_q0 = 0, f_nk = 0, f_nip = 0, f_nb = 64;  // shard [f_q0, f_q0+f_nk)
+  std::vector<int> f_qs;  // the factored q (ascending), slot i <-> q = f_qs[i]
+  int f_nk = 0, f_nip = 0, f_nb = 64;
   cplx* f_L = nullptr;      // (nk, nip, nip) raw left-looking factor (row order)
   cplx* f_Lp = nullptr;     // (nk, nip*nip) pivot-order factor, ld = rank_q
   cplx* f_Linv = nullptr;   // (nk, nblk*nb*nb)
@@ -172,6 +173,7 @@ int free_factors(fisdf_ctx* c) {
   c->f_L = c->f_Lp = c->f_Linv = nullptr;
   c->f_piv = c->f_rank_dev = nullptr;
   c->f_rank.clear();
+  c->f_qs.clear();
   c->f_nk = c->f_nip = 0;
   return 0;
 }
@@ -192,6 +194,20 @@ int select_gram(fisdf_ctx* c, const cplx* x0, int nk, int q0, int q1, int ng0, i
   FISDF_TRY(herk(c->stream, ng0, K, 1.0, tmp, K, x2, ng0, ks, work));
   if (work) FISDF_HIP(hipFreeAsync(work, c->stream));
   (void)nk;
+  return 0;
+}
+
+std::vector<int> q_range(int q0, int q1) {
+  std::vector<int> v;
+  for (int q = q0; q < q1; ++q) v.push_back(q);
+  return v;
+}
+
+int check_qlist(const int* qs, int nq, int nk, const char* who) {
+  FISDF_CHECK(nq >= 0 && (nq == 0 || qs != nullptr), std::string(who) + ": bad q-list");
+  for (int i = 0; i < nq; ++i)
+    FISDF_CHECK(qs[i] >= 0 && qs[i] < nk && (i == 0 || qs[i] > qs[i - 1]),
+                std::string(who) + ": q-list must be ascending and inside the k-mesh");
   return 0;
 }
 
@@ -526,30 +542,30 @@ int fisdf_build_x4(fisdf_ctx* c, const void* Xv, int nip, int nao, const int kme
 }
 
 // ---- A3 ---------------------------------------------------------------------
-int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk, int ngrid,
-                  const void* Xv, int nip, int nao, const int kmesh[3], const double a[9],
-                  int q0, int q1, void* yTv) {
+int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk, int ngrid,
+                     const void* Xv, int nip, int nao, const int kmesh[3], const double a[9],
+                     const int* h_qs, int nq, void* yTv) {
   FISDF_TRY(device_guard(c));
   FISDF_CHECK(g0 >= 0 && nblk >= 0 && g0 + nblk <= ngrid, "build_y: block out of range");
   StageTimer tm(c, FISDF_ST_Y);
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
-  FISDF_CHECK(0 <= q0 && q0 < q1 && q1 <= nk, "build_y: bad q range");
-  const cplx* phase;
-  FISDF_TRY(get_phase(c, kmesh, a, &phase));
+  FISDF_TRY(check_qlist(h_qs, nq, nk, "build_y"));
+  FISDF_CHECK(nq > 0, "build_y: empty q-list");
   const cplx* f = (const cplx*)fv;
   const cplx* X = (const cplx*)Xv;
   cplx* yT = (cplx*)yTv;
-  // sub-block so that the temporaries stay ~<= 2 GB
+  // sub-block so that the temporaries stay ~<= 1 GB
   const long per_g = (long)nk * nip * sizeof(cplx);
   int gb = (int)std::max(64L, std::min<long>(nblk, (1L << 30) / std::max(per_g, 1L)));
   gb = std::min(gb, std::max(nblk, 1));
   Carver cv;
   size_t o1 = cv.take((size_t)per_g * gb);
-  size_t o2 = cv.take((size_t)per_g * gb);
+  size_t oq = cv.take(sizeof(int) * (size_t)nq);
   void* base;
   FISDF_TRY(arena_get(c, cv.off, &base));
   cplx* FX = (cplx*)((char*)base + o1);
-  cplx* FS = (cplx*)((char*)base + o2);
+  int* dq = (int*)((char*)base + oq);
+  FISDF_HIP(hipMemcpyAsync(dq, h_qs, sizeof(int) * nq, hipMemcpyHostToDevice, c->stream));
   for (int s0 = 0; s0 < nblk; s0 += gb) {
     const int m = std::min(gb, nblk - s0);
     const long nm = (long)nip * m;
@@ -557,33 +573,52 @@ int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk
     FISDF_TRY(zgemm(c->stream, OP_N, OP_C, nip, m, nao, ONE, X, nao, (long)nip * nao,
                     f + (long)s0 * nao, nao, f_kstride, ZERO, FX, m, nm, nk));
     // fx_s = Phi fx_k (:79, real :81), y_s = fx_s^2 (:83), y_k = Phi^T y_s (:84) for the
-    // shard's q, written into yT[q-q0][I][g0+s0+g] (:85): separable k-mesh DFTs in LDS
-    FISDF_TRY(kmesh_y(c->stream, FX, nm, kmesh, q0, q1, m, yT, (long)nip * ngrid, ngrid,
+    // listed q, written into yT[slot][I][g0+s0+g] (:85): separable k-mesh DFTs
+    FISDF_TRY(kmesh_y(c->stream, FX, nm, kmesh, h_qs, dq, nq, m, yT, (long)nip * ngrid, ngrid,
                       (long)g0 + s0, c->maximag + 1));
-    (void)FS;
-    (void)phase;
   }
+  FISDF_HIP(hipStreamSynchronize(c->stream));  // h_qs staging
   return 0;
 }
 
+int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk, int ngrid,
+                  const void* Xv, int nip, int nao, const int kmesh[3], const double a[9],
+                  int q0, int q1, void* yTv) {
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  FISDF_CHECK(0 <= q0 && q0 < q1 && q1 <= nk, "build_y: bad q range");
+  std::vector<int> qs = q_range(q0, q1);
+  return fisdf_build_y_qs(c, fv, f_kstride, g0, nblk, ngrid, Xv, nip, nao, kmesh, a, qs.data(),
+                          (int)qs.size(), yTv);
+}
+
 // ---- A4 ---------------------------------------------------------------------
-int fisdf_factor_x4(fisdf_ctx* c, const void* x4v, int q0, int q1, int nip, double tol_rel,
-                    int* h_ranks) {
+int fisdf_factor_x4_qs(fisdf_ctx* c, const void* x4all, const int* h_qs, int nq, int nip,
+                       double tol_rel, int* h_ranks) {
   FISDF_TRY(device_guard(c));
-  const int nk = q1 - q0;
-  FISDF_CHECK(q0 >= 0 && nk > 0 && nip > 0, "factor_x4: bad sizes");
-  x4v = (const cplx*)x4v + (long)q0 * nip * nip;
+  const int nk = nq;
+  FISDF_CHECK(nk > 0 && nip > 0, "factor_x4: bad sizes");
+  FISDF_TRY(check_qlist(h_qs, nq, 1 << 30, "factor_x4"));
   StageTimer tm(c, FISDF_ST_FACTOR);
   FISDF_HIP(hipStreamSynchronize(c->stream));
   FISDF_TRY(free_factors(c));
   const int nb = c->f_nb;
   const int nblk = (nip + nb - 1) / nb;
   const long nn = (long)nip * nip;
+  // the listed x4_q: in place when the list is a contiguous range, else gathered (f_Lp is the
+  // staging buffer: it is overwritten by gather_lp only after pchol has consumed it)
+  const bool contiguous = h_qs[nq - 1] - h_qs[0] == nq - 1;
+  const void* x4v = (const cplx*)x4all + (long)h_qs[0] * nn;
   FISDF_HIP(hipMalloc(&c->f_L, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_Lp, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_Linv, sizeof(cplx) * (size_t)nk * nblk * nb * nb));
   FISDF_HIP(hipMalloc(&c->f_piv, sizeof(int) * (size_t)nk * nip));
-  c->f_q0 = q0;
+  if (!contiguous) {
+    for (int i = 0; i < nq; ++i)
+      FISDF_HIP(hipMemcpyAsync(c->f_Lp + i * nn, (const cplx*)x4all + (long)h_qs[i] * nn,
+                               sizeof(cplx) * nn, hipMemcpyDeviceToDevice, c->stream));
+    x4v = c->f_Lp;
+  }
+  c->f_qs.assign(h_qs, h_qs + nq);
   c->f_nk = nk;
   c->f_nip = nip;
   Carver cv;
@@ -613,14 +648,22 @@ int fisdf_factor_x4(fisdf_ctx* c, const void* x4v, int q0, int q1, int nip, doub
   return 0;
 }
 
+int fisdf_factor_x4(fisdf_ctx* c, const void* x4v, int q0, int q1, int nip, double tol_rel,
+                    int* h_ranks) {
+  FISDF_CHECK(q0 >= 0 && q1 > q0, "factor_x4: bad sizes");
+  std::vector<int> qs = q_range(q0, q1);
+  return fisdf_factor_x4_qs(c, x4v, qs.data(), (int)qs.size(), nip, tol_rel, h_ranks);
+}
+
 // ---- A4 + A5 ------------------------------------------------------------------
-int fisdf_fit_coulomb(fisdf_ctx* c, int q0, int q1, const void* yTv, int nip, const int mesh[3],
-                      const int kmesh[3], const double a[9], void* Wqv) {
+int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv, int nip,
+                         const int mesh[3], const int kmesh[3], const double a[9], void* Wqv) {
   FISDF_TRY(device_guard(c));
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
-  FISDF_CHECK(c->f_q0 == q0 && c->f_nk == q1 - q0 && c->f_nip == nip,
-              "fit_coulomb: call fisdf_factor_x4 on the same q range first");
-  FISDF_CHECK(0 <= q0 && q0 <= q1 && q1 <= nk, "fit_coulomb: bad q range");
+  FISDF_TRY(check_qlist(h_qs, nq, nk, "fit_coulomb"));
+  FISDF_CHECK(c->f_nk == nq && c->f_nip == nip &&
+                  std::equal(c->f_qs.begin(), c->f_qs.end(), h_qs),
+              "fit_coulomb: call fisdf_factor_x4 on the same q-list first");
   const long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
   const long nn = (long)nip * nip;
   const int nb = c->f_nb;
@@ -630,9 +673,8 @@ int fisdf_fit_coulomb(fisdf_ctx* c, int q0, int q1, const void* yTv, int nip, co
   const double vol = cell_volume(a);
   const cplx* yT = (const cplx*)yTv;
   cplx* Wq = (cplx*)Wqv;
-  const int nq = q1 - q0;
   int rmax = 0;
-  for (int q = q0; q < q1; ++q) rmax = std::max(rmax, c->f_rank[q - q0]);
+  for (int lq = 0; lq < nq; ++lq) rmax = std::max(rmax, c->f_rank[lq]);
   const int ks = pick_ksplit(rmax, rmax, (int)ngrid);
   const long rr = (long)rmax * rmax;
   const long sLi = (long)nblk * nb * nb;
@@ -659,8 +701,8 @@ int fisdf_fit_coulomb(fisdf_ctx* c, int q0, int q1, const void* yTv, int nip, co
     return 0;
   }
   FISDF_HIP(hipMemsetAsync(G, 0, sizeof(cplx) * nq * rr, c->stream));
-  for (int q = q0; q < q1; ++q) {
-    const int lq = q - q0;
+  for (int lq = 0; lq < nq; ++lq) {
+    const int q = h_qs[lq];
     const int r = c->f_rank[lq];
     if (r == 0) continue;
     const int* piv = c->f_piv + (long)lq * nip;
@@ -704,28 +746,66 @@ int fisdf_fit_coulomb(fisdf_ctx* c, int q0, int q1, const void* yTv, int nip, co
   return 0;
 }
 
+int fisdf_fit_coulomb(fisdf_ctx* c, int q0, int q1, const void* yTv, int nip, const int mesh[3],
+                      const int kmesh[3], const double a[9], void* Wqv) {
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  FISDF_CHECK(0 <= q0 && q0 <= q1 && q1 <= nk, "fit_coulomb: bad q range");
+  std::vector<int> qs = q_range(q0, q1);
+  return fisdf_fit_coulomb_qs(c, qs.data(), (int)qs.size(), yTv, nip, mesh, kmesh, a, Wqv);
+}
+
 // ---- A8 prep ------------------------------------------------------------------
-int fisdf_build_ws(fisdf_ctx* c, const void* Wqv, int q0, int q1, int nip, const int kmesh[3],
-                   const double a[9], void* Wsv) {
+int fisdf_build_ws_qs(fisdf_ctx* c, const void* Wqv, const int* h_qs, const double* h_wt, int nq,
+                      int nip, const int kmesh[3], const double a[9], void* Wsv) {
   FISDF_TRY(device_guard(c));
   StageTimer tm(c, FISDF_ST_WS);
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
-  FISDF_CHECK(0 <= q0 && q0 <= q1 && q1 <= nk, "build_ws: bad q range");
-  const cplx* phase;
-  FISDF_TRY(get_phase(c, kmesh, a, &phase));
+  FISDF_TRY(check_qlist(h_qs, nq, nk, "build_ws"));
   const long nn = (long)nip * nip;
-  void* base;
-  FISDF_TRY(arena_get(c, sizeof(cplx) * nk * nn, &base));
-  cplx* tmp = (cplx*)base;
-  if (q1 == q0) {
+  if (nq == 0) {
     FISDF_HIP(hipMemsetAsync(Wsv, 0, sizeof(cplx) * nk * nn, c->stream));
     return 0;
   }
-  // ws = Phi W (:205), real part * sqrt(nk) (:207)
-  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nn, q1 - q0, ONE, phase + q0, nk, 0,
-                  (const cplx*)Wqv, nn, 0, ZERO, tmp, nn, 0, 1));
+  // Phi_sel[R, i] = wt_i Phi[R, q_i]  (host; nk x nq)
+  CellGeom g;
+  lattice(a, g);
+  std::vector<cplx> ph((size_t)nk * nq);
+  for (int R = 0; R < nk; ++R) {
+    int r2 = R % kmesh[2], r1 = (R / kmesh[2]) % kmesh[1], r0 = R / (kmesh[1] * kmesh[2]);
+    double T[3];
+    for (int cc = 0; cc < 3; ++cc) T[cc] = r0 * g.a[0][cc] + r1 * g.a[1][cc] + r2 * g.a[2][cc];
+    for (int i = 0; i < nq; ++i) {
+      double k[3];
+      kpoint(kmesh, g, h_qs[i], k);
+      const double th = T[0] * k[0] + T[1] * k[1] + T[2] * k[2];
+      const double w = (h_wt ? h_wt[i] : 1.0) / std::sqrt((double)nk);
+      ph[(size_t)R * nq + i] = cmk(w * std::cos(th), w * std::sin(th));
+    }
+  }
+  Carver cv;
+  size_t oT = cv.take(sizeof(cplx) * nk * nn);
+  size_t oP = cv.take(sizeof(cplx) * ph.size());
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  cplx* tmp = (cplx*)((char*)base + oT);
+  cplx* dph = (cplx*)((char*)base + oP);
+  FISDF_HIP(hipMemcpyAsync(dph, ph.data(), sizeof(cplx) * ph.size(), hipMemcpyHostToDevice,
+                           c->stream));
+  // ws = Phi W (:205), real part * sqrt(nk) (:207).  With time-reversal representatives the
+  // partner -q contributes conj(Phi[R,q] W_q), so Re(.) of the pair is 2 Re(Phi[R,q] W_q): wt = 2.
+  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nn, nq, ONE, dph, nq, 0, (const cplx*)Wqv, nn, 0,
+                  ZERO, tmp, nn, 0, 1));
   FISDF_TRY(real_part(c->stream, tmp, std::sqrt((double)nk), (cplx*)Wsv, nk * nn, nullptr));
+  FISDF_HIP(hipStreamSynchronize(c->stream));  // ph staging
   return 0;
+}
+
+int fisdf_build_ws(fisdf_ctx* c, const void* Wqv, int q0, int q1, int nip, const int kmesh[3],
+                   const double a[9], void* Wsv) {
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  FISDF_CHECK(0 <= q0 && q0 <= q1 && q1 <= nk, "build_ws: bad q range");
+  std::vector<int> qs = q_range(q0, q1);
+  return fisdf_build_ws_qs(c, Wqv, qs.data(), nullptr, (int)qs.size(), nip, kmesh, a, Wsv);
 }
 
 // ---- next-2: ISDF ERIs / ao2mo --------------------------------------------------

@@ -34,7 +34,10 @@ int gather_points(hipStream_t s, const cplx* x0, int nk, int ng0, int nao, const
 int square_scale(hipStream_t s, const cplx* in, double sc, cplx* out, long n);
 int permute_kgm(hipStream_t s, const cplx* x0, int nq, int ng, int nao, cplx* out);
 int pair_product(hipStream_t s, const cplx* A, int n1, const cplx* B, int n2, int nip, cplx* P);
-int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], int q0, int q1, int m,
-            cplx* yT, long qs, long Is, long goff, unsigned long long* mon);
+// y_q = Phi^T (Re(Phi FX))^2 for the ascending q-list (h_qs on the host; d_qs a device copy,
+// needed only when the k-mesh has more than 64 points), written to yT[slot][I][goff + g]
+int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const int* h_qs,
+            const int* d_qs, int nq, int m, cplx* yT, long qs, long Is, long goff,
+            unsigned long long* mon);
 
 }  // namespace fisdf

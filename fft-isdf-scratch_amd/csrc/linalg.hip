@@ -241,8 +241,9 @@ __device__ void kmesh_axis_dft(cplx* T, int CT, int ld, int nk, int na, int stri
 }
 
 __global__ __launch_bounds__(256) void kmesh_y_kernel(
-    const cplx* __restrict__ FX, long ncol, int nk, int n0, int n1, int n2, int q0, int q1,
-    int m, cplx* __restrict__ yT, long qs, long Is, long goff, int CT,
+    const cplx* __restrict__ FX, long ncol, int nk, int n0, int n1, int n2,
+    const int* __restrict__ qlist, int nq, int m, cplx* __restrict__ yT, long qs, long Is,
+    long goff, int CT,
     unsigned long long* __restrict__ mon) {
   extern __shared__ cplx sm[];
   cplx* w0 = sm;
@@ -312,13 +313,12 @@ __global__ __launch_bounds__(256) void kmesh_y_kernel(
   __syncthreads();
   kmesh_axis_dft(T, CT, ld, nk, n2, 1, w2, tid, nthr);
   __syncthreads();
-  const int nq = q1 - q0;
   for (int e = tid; e < nq * CT; e += nthr) {
     const int qq = e / CT, c = e % CT;
     const long col = c0 + c;
     if (col < ncol) {
       const long I = col / m, g = col % m;
-      cplx v = T[(q0 + qq) * ld + c];
+      cplx v = T[qlist[qq] * ld + c];
       yT[qq * qs + I * Is + goff + g] = cmk(v.x * sc, v.y * sc);
     }
   }
@@ -365,8 +365,8 @@ __device__ __forceinline__ void reg_axis_dft(cplx* v, const cplx* tw) {
 
 template <int N0, int N1, int N2>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void kmesh_y_reg_kernel(
-    const cplx* __restrict__ FX, int ncol, int q0, int q1, int m, cplx* __restrict__ yT, long qs,
-    long Is, long goff, unsigned long long* __restrict__ mon) {
+    const cplx* __restrict__ FX, int ncol, unsigned long long qmask, int m, cplx* __restrict__ yT,
+    long qs, long Is, long goff, unsigned long long* __restrict__ mon) {
   constexpr int NK = N0 * N1 * N2;
   cplx tw0[N0], tw1[N1], tw2[N2];
 #pragma unroll
@@ -400,7 +400,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     cplx* out = yT + (long)I * Is + goff + g;
 #pragma unroll
     for (int k = 0; k < NK; ++k)
-      if (k >= q0 && k < q1) out[(long)(k - q0) * qs] = cmk(v[k].x * sc, v[k].y * sc);
+      if ((qmask >> k) & 1ull)  // slot of q = k in the ascending q-list
+        out[(long)__popcll(qmask & ((1ull << k) - 1ull)) * qs] = cmk(v[k].x * sc, v[k].y * sc);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mi = fmax(mi, __shfl_xor(mi, o, 64));
@@ -603,18 +604,24 @@ int scale_rows(hipStream_t s, const cplx* X, const cplx* v, int nset, int nk, in
   return 0;
 }
 
-int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], int q0, int q1, int m,
-            cplx* yT, long qs, long Is, long goff, unsigned long long* mon) {
+int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const int* h_qs,
+            const int* d_qs, int nq, int m, cplx* yT, long qs, long Is, long goff,
+            unsigned long long* mon) {
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  for (int i = 0; i < nq; ++i)
+    FISDF_CHECK(h_qs[i] >= 0 && h_qs[i] < nk && (i == 0 || h_qs[i] > h_qs[i - 1]),
+                "kmesh_y: q-list must be ascending and inside the k-mesh");
   FISDF_CHECK(kmesh[0] <= KM_MAXN && kmesh[1] <= KM_MAXN && kmesh[2] <= KM_MAXN,
               "kmesh_y: k-mesh axes must be <= 16");
-  if (ncol < (1L << 31)) {
+  if (ncol < (1L << 31) && nk <= 64) {
     const int nc = (int)ncol;
+    unsigned long long qmask = 0;
+    for (int i = 0; i < nq; ++i) qmask |= 1ull << h_qs[i];
     const unsigned grid = (unsigned)std::max<long>(1, std::min<long>((ncol + 63) / 64, 32768));
 #define FISDF_KM(a, b, c)                                                                      \
   if (kmesh[0] == a && kmesh[1] == b && kmesh[2] == c) {                                       \
-    hipLaunchKernelGGL((kmesh_y_reg_kernel<a, b, c>), dim3(grid), dim3(64), 0, s, FX, nc, q0,   \
-                       q1, m, yT, qs, Is, goff, mon);                                          \
+    hipLaunchKernelGGL((kmesh_y_reg_kernel<a, b, c>), dim3(grid), dim3(64), 0, s, FX, nc,       \
+                       qmask, m, yT, qs, Is, goff, mon);                                       \
     FISDF_HIP(hipGetLastError());                                                              \
     return 0;                                                                                  \
   }
@@ -626,12 +633,13 @@ int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], int q0
   while (CT > 8 && sizeof(cplx) * ((size_t)nk * (CT + 1) + 3 * KM_MAXN) > 64 * 1024) CT /= 2;
   const size_t lds = sizeof(cplx) * ((size_t)nk * (CT + 1) + 3 * KM_MAXN);
   FISDF_CHECK(lds <= 160 * 1024, "kmesh_y: k-mesh too large for the LDS tile");
+  FISDF_CHECK(d_qs != nullptr, "kmesh_y: device q-list required for this k-mesh");
   const long tiles = (ncol + CT - 1) / CT;
   FISDF_CHECK(tiles < (1L << 31), "kmesh_y: too many columns");
   if (tiles == 0) return 0;
   const unsigned grid = (unsigned)std::min<long>(tiles, 4096);
   hipLaunchKernelGGL(kmesh_y_kernel, dim3(grid), dim3(256), lds, s, FX, ncol, nk,
-                     kmesh[0], kmesh[1], kmesh[2], q0, q1, m, yT, qs, Is, goff, CT, mon);
+                     kmesh[0], kmesh[1], kmesh[2], d_qs, nq, m, yT, qs, Is, goff, CT, mon);
   FISDF_HIP(hipGetLastError());
   return 0;
 }

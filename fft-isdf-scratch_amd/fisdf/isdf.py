@@ -98,6 +98,8 @@ class InterpolativeSeparableDensityFitting:
     blksize = 8000          # fftisdf.py:300
     fit_tol = 1e-14         # relative pivot cut of the x4_q factorisation
     select_tol = -1.0       # dpstrf default tolerance (ng0*eps*max diag)
+    # fit one q of each (q, -q) pair and take W_{-q} = conj(W_q) (y_s, x4_s real: :43,:81)
+    time_reversal = True
 
     def __init__(self, cell, kpts, m0=None, c0=20.0, device=None, comm=None):
         self.cell = cell
@@ -250,14 +252,17 @@ class InterpolativeSeparableDensityFitting:
         return ((v[:, 0] * kmesh[1] + v[:, 1]) * kmesh[2] + v[:, 2]).astype(np.int32), v
 
     def _w_of_q(self, q):
+        """W_q on the device: a fitted q's own W (local or fetched from the host copy), or
+        conj(W_{-q}) for the partner of a time-reversal representative."""
         st = self._dev_state
         d = self.device
-        if d.size == 1:
-            return st["Wq"][q]
-        q0, q1 = d.shard(int(np.prod(self.kmesh)))
-        if q0 <= q < q1:
-            return st["Wq"][q - q0]
-        return d.to_dev(self._wq[q])
+        rep = q if q in set(int(x) for x in self.fit_qs) else int(self.q_partner[q])
+        slot = np.nonzero(self.my_qs == rep)[0]
+        if len(slot):
+            W = st["Wq"][int(slot[0])]
+        else:
+            W = d.to_dev(self._wq[rep])
+        return W.conj().resolve_conj() if rep != q else W
 
     def ao2mo(self, mo_coeffs, kpts=None, compact=False):
         """ISDF (ij|kl) for four k-points: eri[ij, kl] = sum_IJ W_q[I,J] conj(XC1)[I,i] (XC2)[I,j]
@@ -321,17 +326,23 @@ class InterpolativeSeparableDensityFitting:
         return object.__getattribute__(self, name)
 
     def _gather_wq(self):
+        """All W_q (nk, nip, nip) on the host: fitted q from every rank, partners by conj."""
         st = self._dev_state
         d = self.device
-        if d.size == 1:
-            return st["Wq"].cpu().numpy()
-        import torch.distributed as dist
         nk = int(np.prod(self.kmesh))
-        parts = [None] * d.size
-        dist.all_gather_object(parts, (d.shard(nk), st["Wq"].cpu().numpy()), group=d.comm)
+        if d.size == 1:
+            parts = [(self.my_qs, st["Wq"].cpu().numpy())]
+        else:
+            import torch.distributed as dist
+            parts = [None] * d.size
+            dist.all_gather_object(parts, (self.my_qs, st["Wq"].cpu().numpy()), group=d.comm)
         out = np.zeros((nk, self.nip, self.nip), complex)
-        for (q0, q1), w in parts:
-            out[q0:q1] = w
+        for qs, w in parts:
+            out[np.asarray(qs, dtype=int)] = w
+        for q in range(nk):
+            p = int(self.q_partner[q])
+            if p != q and q not in set(int(x) for x in self.fit_qs):
+                out[q] = out[p].conj()
         return out
 
 
@@ -363,57 +374,82 @@ def build(df_obj):
     x4 = d.empty((nk, nip, nip))
     d.ctx.call("fisdf_build_x4", _lib.ptr(X), nip, nao, km_p, a_p, _lib.ptr(x4))   # :38-48
 
-    q0, q1 = d.shard(nk)
+    # q to fit: time-reversal representatives (W_{-q} = conj(W_q)) or every q, sharded in
+    # contiguous chunks over the ranks
+    fit_qs, partner, weight = _fit_qset(df_obj, kmesh)
+    chunks = [kshard.shard_range(len(fit_qs), r, d.size) for r in range(d.size)]
+    a0, a1 = chunks[d.rank]
+    my_qs = np.ascontiguousarray(fit_qs[a0:a1], dtype=np.int32)
+    my_wt = np.ascontiguousarray(weight[a0:a1], dtype=np.float64)
+    nq = len(my_qs)
+    qs_c = my_qs.ctypes.data_as(_lib._ip)
     if df_obj._ao_grid is None:
         df_obj._ao_grid = d.to_dev(eval_ao_kpts(cell, df_obj.grids_coords(), kmesh))
     f = df_obj._ao_grid
-    yT = d.empty((q1 - q0, nip, ngrid))
+    yT = d.empty((nq, nip, ngrid))
     if d.size == 1:
-        d.ctx.call("fisdf_build_y", _lib.ptr(f), ngrid * nao, 0, ngrid, ngrid, _lib.ptr(X), nip,
-                   nao, km_p, a_p, q0, q1, _lib.ptr(yT))                 # :67-87
+        d.ctx.call("fisdf_build_y_qs", _lib.ptr(f), ngrid * nao, 0, ngrid, ngrid, _lib.ptr(X),
+                   nip, nao, km_p, a_p, qs_c, nq, _lib.ptr(yT))                 # :67-87
     else:
-        # grid-sharded y (all q on this rank's plane-aligned grid slice), then one all-to-all
-        # hands every rank the y_q of its own q-shard on the whole grid
+        # grid-sharded y (all fitted q on this rank's plane-aligned grid slice), then one
+        # all-to-all hands every rank the y_q of its own q-chunk on the whole grid
         slices = kshard.grid_slices(df_obj.mesh, d.size)
         g0, ng = slices[d.rank]
-        send = d.empty((nk, nip, ng))
+        all_qs = np.ascontiguousarray(fit_qs, dtype=np.int32)
+        send = d.empty((len(all_qs), nip, ng))
         if ng:
             fptr = _lib._vp(f.data_ptr() + g0 * nao * f.element_size())
-            d.ctx.call("fisdf_build_y", fptr, ngrid * nao, 0, ng, ng, _lib.ptr(X), nip, nao,
-                       km_p, a_p, 0, nk, _lib.ptr(send))
+            d.ctx.call("fisdf_build_y_qs", fptr, ngrid * nao, 0, ng, ng, _lib.ptr(X), nip, nao,
+                       km_p, a_p, all_qs.ctypes.data_as(_lib._ip), len(all_qs), _lib.ptr(send))
         # the all-to-all runs on the collective stream while this rank factorises its x4_q
         recv, work = kshard.exchange_y(send, nk, nip, slices, d.rank, d.size, d.comm,
-                                       async_op=True)
+                                       async_op=True, counts=[b - a for a, b in chunks])
 
-    ranks = np.zeros(q1 - q0, np.int32)
-    d.ctx.call("fisdf_factor_x4", _lib.ptr(x4), q0, q1, nip, float(df_obj.fit_tol),
-               ranks.ctypes.data_as(_lib._ip))
+    ranks = np.zeros(nq, np.int32)
+    if nq:
+        d.ctx.call("fisdf_factor_x4_qs", _lib.ptr(x4), qs_c, nq, nip, float(df_obj.fit_tol),
+                   ranks.ctypes.data_as(_lib._ip))
     if d.size > 1:
         if work is not None:
             work.wait()
         del send
         g0s = (C_long * d.size)(*[s[0] for s in slices])
         ngs = (C_long * d.size)(*[s[1] for s in slices])
-        d.ctx.call("fisdf_unpack_slices", _lib.ptr(recv), (q1 - q0) * nip, d.size, g0s, ngs,
-                   ngrid, _lib.ptr(yT))
+        if nq:
+            d.ctx.call("fisdf_unpack_slices", _lib.ptr(recv), nq * nip, d.size, g0s, ngs, ngrid,
+                       _lib.ptr(yT))
         del recv
-    Wq = d.empty((q1 - q0, nip, nip))
-    d.ctx.call("fisdf_fit_coulomb", q0, q1, _lib.ptr(yT), nip, mesh_p, km_p, a_p, _lib.ptr(Wq))
+    Wq = d.empty((nq, nip, nip))
+    if nq:
+        d.ctx.call("fisdf_fit_coulomb_qs", qs_c, nq, _lib.ptr(yT), nip, mesh_p, km_p, a_p,
+                   _lib.ptr(Wq))
     del yT
 
     Ws = d.empty((nk, nip, nip))
-    d.ctx.call("fisdf_build_ws", _lib.ptr(Wq), q0, q1, nip, km_p, a_p, _lib.ptr(Ws))  # :204-207
+    d.ctx.call("fisdf_build_ws_qs", _lib.ptr(Wq), qs_c, my_wt.ctypes.data_as(_lib._dp), nq, nip,
+               km_p, a_p, _lib.ptr(Ws))                                          # :204-207
     if d.size > 1:
         kshard.allreduce_ws(Ws, d.comm)                                  # k-sum of W_s
-        W0 = Wq[0].clone() if q0 == 0 else d.empty((nip, nip))
-        kshard.broadcast_w0(W0, nk, d.comm)                               # W_0 for get_j
+        owner0 = next(r for r, (a, b) in enumerate(chunks) if b > a)     # fit_qs[0] == 0
+        W0 = Wq[0].clone() if d.rank == owner0 else d.empty((nip, nip))
+        kshard.broadcast_w0(W0, nk, d.comm, src_local=owner0)           # W_0 for get_j
     else:
         W0 = Wq[0]
+    df_obj.fit_qs, df_obj.q_partner = fit_qs, partner
+    df_obj.my_qs = my_qs
     df_obj._dev_state.update(x4=x4, Wq=Wq, W0=W0, Ws=Ws)
     df_obj.ranks = ranks
     df_obj.nip = nip
     df_obj.timings["build"] = time.perf_counter() - t0
     return df_obj
+
+
+def _fit_qset(df_obj, kmesh):
+    """(fit_qs, partner, weight): the q whose W_q is computed, the -q map and the W_s weights."""
+    nk = int(np.prod(kmesh))
+    if df_obj.time_reversal:
+        return kshard.time_reversal_reps(kmesh)
+    return (np.arange(nk, dtype=np.int32), np.arange(nk, dtype=np.int32), np.ones(nk))
 
 
 def _dms_to_dev(df_obj, dm_kpts):

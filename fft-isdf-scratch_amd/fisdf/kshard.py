@@ -27,6 +27,30 @@ def shard_range(nk: int, rank: int, size: int):
     return q0, q0 + base + (1 if rank < rem else 0)
 
 
+def time_reversal_reps(kmesh):
+    """Time-reversal classes of the q-mesh (get_kpts order, wrap_around=False).
+
+    y_s and x4_s are real (fftisdf.py:43,81), so y_{-q} = conj(y_q) and x4_{-q} = conj(x4_q)
+    and hence W_{-q} = conj(W_q): only one q of each (q, -q) pair needs a fit.  Returns
+    (reps, partner, weight): ascending representatives (the smaller index of each pair),
+    partner[q] = index of -q mod kmesh, weight[i] = 1 if reps[i] is its own partner else 2."""
+    import numpy as np
+    kmesh = np.asarray(kmesh, dtype=int)
+    nk = int(np.prod(kmesh))
+    v = np.stack(np.unravel_index(np.arange(nk), tuple(kmesh)), axis=1)
+    mv = (-v) % kmesh
+    partner = (mv[:, 0] * kmesh[1] + mv[:, 1]) * kmesh[2] + mv[:, 2]
+    reps = np.array([q for q in range(nk) if partner[q] >= q], dtype=np.int32)
+    weight = np.where(partner[reps] == reps, 1.0, 2.0)
+    return reps, partner.astype(np.int32), weight
+
+
+def shard_list(items, rank: int, size: int):
+    """Contiguous, balanced chunk of `items` owned by `rank`."""
+    a, b = shard_range(len(items), rank, size)
+    return items[a:b]
+
+
 def owner_of(q: int, nk: int, size: int) -> int:
     for r in range(size):
         q0, q1 = shard_range(nk, r, size)
@@ -48,20 +72,23 @@ def grid_slices(mesh, size: int):
 
 
 def exchange_y(send, nk: int, nip: int, slices, rank: int, size: int, group=None,
-               async_op: bool = False):
-    """All-to-all of the grid-sliced y: `send` is (nk, nip, ng_rank) = y_q on this rank's
-    slice for every q; the q-blocks are contiguous, so block r of the send buffer is rank
-    r's q-shard.  Returns recv = concat_p (nq_self, nip, ng_p) in rank order p
-    (with async_op: (recv, work) — call work.wait() before reading recv; work may be None)."""
+               async_op: bool = False, counts=None):
+    """All-to-all of the grid-sliced y: `send` is (nq_all, nip, ng_rank) = y_q on this rank's
+    slice for every fitted q; the q-blocks are contiguous, so block r of the send buffer is
+    rank r's q-shard (`counts[r]` q each; default: shard_range over nk).  Returns
+    recv = concat_p (nq_self, nip, ng_p) in rank order p (with async_op: (recv, work) — call
+    work.wait() before reading recv; work may be None)."""
     import torch
     import torch.distributed as dist
     ng_self = slices[rank][1]
-    q0, q1 = shard_range(nk, rank, size)
-    nq = q1 - q0
-    in_splits = [(b - a) * nip * ng_self for a, b in (shard_range(nk, r, size) for r in range(size))]
+    if counts is None:
+        counts = [b - a for a, b in (shard_range(nk, r, size) for r in range(size))]
+    nq = counts[rank]
+    in_splits = [c * nip * ng_self for c in counts]
     out_splits = [nq * nip * slices[p][1] for p in range(size)]
     if _host_staged(group, send):
-        recv = exchange_y(send.cpu(), nk, nip, slices, rank, size, group).to(send.device)
+        recv = exchange_y(send.cpu(), nk, nip, slices, rank, size, group,
+                          counts=counts).to(send.device)
         return (recv, None) if async_op else recv
     recv = torch.empty(sum(out_splits), dtype=send.dtype, device=send.device)
     flat = send.reshape(-1)
@@ -99,12 +126,13 @@ def allreduce_ws(ws, group=None):
     return allreduce_sum(ws, group)
 
 
-def broadcast_w0(w0, nk: int, group=None):
-    """Broadcast W_0 from the rank that owns q = 0."""
+def broadcast_w0(w0, nk: int, group=None, src_local=None):
+    """Broadcast W_0 from the rank that owns q = 0 (default: contiguous q-ranges over nk)."""
     import torch
     import torch.distributed as dist
     size = dist.get_world_size(group)
-    src_local = owner_of(0, nk, size)
+    if src_local is None:
+        src_local = owner_of(0, nk, size)
     src = dist.get_global_rank(group, src_local) if group is not None else src_local
     if _host_staged(group, w0):
         h = w0.cpu()

@@ -104,12 +104,21 @@ int fisdf_build_y(fisdf_ctx* ctx, const void* d_f, long f_kstride, int g0, int n
                   const void* d_X, int nip, int nao, const int kmesh[3], const double a[9],
                   int q0, int q1, void* d_yT);
 
+/* Same for an explicit ascending q-list h_qs[0..nq) (e.g. the time-reversal representatives
+ * of this rank, see fisdf_fit_coulomb_qs): y_q is written to d_yT[i] for q = h_qs[i]. */
+int fisdf_build_y_qs(fisdf_ctx* ctx, const void* d_f, long f_kstride, int g0, int nblk, int ngrid,
+                     const void* d_X, int nip, int nao, const int kmesh[3], const double a[9],
+                     const int* h_qs, int nq, void* d_yT);
+
 /* ---- A4: per-q factorisation of x4_q, q in [q0, q1) (replaces zgelsy's QRCP,
  * fftisdf.py:108).  Pivoted Cholesky with rank cut tol_rel*max(diag); factors stay in
  * the context.  d_x4: (nk, nip, nip) (all q).  synchronous: h_ranks (q1-q0) receives
  * the numerical ranks (logged at fftisdf.py:122). */
 int fisdf_factor_x4(fisdf_ctx* ctx, const void* d_x4, int q0, int q1, int nip, double tol_rel,
                     int* h_ranks);
+/* q-list form: factors x4_q for q = h_qs[i] (ascending); h_ranks (nq). */
+int fisdf_factor_x4_qs(fisdf_ctx* ctx, const void* d_x4, const int* h_qs, int nq, int nip,
+                       double tol_rel, int* h_ranks);
 
 /* ---- A4+A5: fit + FFT Coulomb for the factored shard q in [q0, q1) (fftisdf.py:97-121)
  * Needs fisdf_factor_x4 on the same range.  W_q = zeta_q z_q^H computed as
@@ -118,12 +127,21 @@ int fisdf_factor_x4(fisdf_ctx* ctx, const void* d_x4, int q0, int q1, int nip, d
  * d_Wq: (q1-q0, nip, nip). */
 int fisdf_fit_coulomb(fisdf_ctx* ctx, int q0, int q1, const void* d_yT, int nip,
                       const int mesh[3], const int kmesh[3], const double a[9], void* d_Wq);
+/* q-list form (the list given to fisdf_factor_x4_qs).  Time reversal: y_s and x4_s are real
+ * (fftisdf.py:43,81), so y_{-q} = conj(y_q), x4_{-q} = conj(x4_q) and W_{-q} = conj(W_q);
+ * callers may fit only one q of each (q, -q) pair and weight it 2 in fisdf_build_ws_qs. */
+int fisdf_fit_coulomb_qs(fisdf_ctx* ctx, const int* h_qs, int nq, const void* d_yT, int nip,
+                         const int mesh[3], const int kmesh[3], const double a[9], void* d_Wq);
 
 /* ---- A8 prep: W_s[R] = sqrt(nk) Re(sum_{q in [q0,q1)} Phi[R,q] W_q) (fftisdf.py:204-207)
  * d_Wq: (q1-q0, nip, nip) shard; d_Ws: (nimg, nip, nip) c128 with zero imaginary part
  * (partial sum for a q-shard; shards are summed with an all-reduce). */
 int fisdf_build_ws(fisdf_ctx* ctx, const void* d_Wq, int q0, int q1, int nip,
                    const int kmesh[3], const double a[9], void* d_Ws);
+/* q-list form: W_s[R] = sqrt(nk) Re(sum_i h_wt[i] Phi[R,q_i] W_{q_i}) (h_wt NULL: all 1;
+ * 2 for a time-reversal representative whose partner -q is not listed).  synchronous. */
+int fisdf_build_ws_qs(fisdf_ctx* ctx, const void* d_Wq, const int* h_qs, const double* h_wt,
+                      int nq, int nip, const int kmesh[3], const double a[9], void* d_Ws);
 
 /* ---- A7: get_j_kpts (fftisdf.py:133-171) ------------------------------------
  * d_dms (nset, nk, nao, nao); d_vj same shape (complex; caller takes .real for Gamma). */

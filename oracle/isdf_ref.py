@@ -162,7 +162,7 @@ def fit_and_coulomb(x4_q, y_q, vq, coord, a, mesh, vol, Gv=None):
     return zeta @ z_q.conj().T, rank                                  # :121
 
 
-def build(xip, f_k, coord, a, kmesh, mesh, blksize=8000):
+def build(xip, f_k, coord, a, kmesh, mesh, blksize=8000, progress=False):
     """fftisdf.py:22-128 given the interpolation-point AOs ``xip`` and the grid AOs ``f_k``.
 
     Returns dict(x=xip, w0=W_0, wq=W_q, ranks=[...], y=y, x4=x4_k).
@@ -183,6 +183,8 @@ def build(xip, f_k, coord, a, kmesh, mesh, blksize=8000):
         w, r = fit_and_coulomb(x4_k[q], y[q], vq, coord, a, mesh, vol, Gv)
         wq.append(w)
         ranks.append(r)
+        if progress:
+            print(f"oracle fit q {q + 1}/{nkpt} rank {r}", flush=True)
     wq = np.asarray(wq).reshape(nkpt, nip, nip)                       # :124
     return dict(x=xip, w0=wq[0], wq=wq, ranks=ranks, x4=x4_k, y=y)
 

@@ -11,6 +11,10 @@ CASES = {
     # name: (cell factory, kmesh, m0, c0)
     "toy222": (lambda: C.toy_cell(mesh=(12, 12, 12)), (2, 2, 2), (9, 9, 9), 40.0),
     "toy331": (lambda: C.toy_cell(mesh=(15, 15, 15)), (3, 3, 1), (9, 9, 9), 40.0),
+    # production regime: nip below the numerical rank, every x4_q full rank (as at C2/C3,
+    # ranks == nip); the toy cases above have nip > rank (x4_q rank-deficient)
+    "toy331_fr": (lambda: C.toy_cell(mesh=(15, 15, 15)), (3, 3, 1), (9, 9, 9), 25.0),
+    "toy333_fr": (lambda: C.toy_cell(mesh=(12, 12, 12)), (3, 3, 3), (9, 9, 9), 20.0),
     "diamond_szv_gamma": (lambda: C.diamond_cell(basis="gth-szv", mesh=(8, 8, 8)), (1, 1, 1),
                           (15, 15, 15), 20.0),
     # C4-shaped: NiO AFM (nio-afm.vasp), dzvp-molopt-sr-shaped basis with f shells (nao 76);

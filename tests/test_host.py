@@ -65,6 +65,19 @@ def test_reference_surface():
         df.get_jk(dm, omega=0.1)
 
 
+def test_time_reversal_reps():
+    from fisdf.kshard import time_reversal_reps
+    for kmesh, nrep in [((4, 4, 4), 36), ((2, 2, 2), 8), ((3, 3, 1), 5), ((1, 1, 1), 1),
+                        ((3, 3, 3), 14)]:
+        reps, partner, w = time_reversal_reps(kmesh)
+        nk = int(np.prod(kmesh))
+        assert len(reps) == nrep and list(reps) == sorted(reps) and reps[0] == 0
+        assert all(partner[partner[q]] == q for q in range(nk))
+        assert sum(w) == nk                       # every q counted once
+        covered = set(reps.tolist()) | set(partner[reps].tolist())
+        assert covered == set(range(nk))
+
+
 def test_shard_ranges():
     from fisdf.kshard import shard_range, owner_of
     for nk in (1, 7, 8, 64):
