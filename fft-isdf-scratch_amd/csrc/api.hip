@@ -39,6 +39,17 @@ struct fisdf_ctx {
   int* f_piv = nullptr;     // (nk, nip)
   int* f_rank_dev = nullptr;
   std::vector<int> f_rank;  // host copy
+  // the factorisation runs on a side stream, overlapped with the y build on `stream`
+  hipStream_t side = nullptr;
+  hipEvent_t ev_x4 = nullptr, ev_fac = nullptr;
+  bool f_pending = false;
+  int* f_rank_pinned = nullptr;  // host (pinned) copy target, f_nk ints
+  void* f_scratch = nullptr;     // device scratch of the factorisation
+  size_t f_scratch_size = 0;
+  // pinned staging of small host arrays copied asynchronously (q-lists)
+  int* stage_pinned = nullptr;
+  size_t stage_cap = 0;
+  hipEvent_t ev_stage = nullptr;
   // reality-invariant monitors
   unsigned long long* maximag = nullptr;  // 3 slots
   // timing
@@ -73,20 +84,39 @@ struct Carver {
   }
 };
 
+// Asynchronous upload of a small host int array: staged through a pinned buffer whose reuse
+// waits for the previous copy (no host sync on the stream).
+int upload_ints(fisdf_ctx* c, const int* h, int n, int* d) {
+  if (n <= 0) return 0;
+  if (!c->ev_stage) FISDF_HIP(hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
+  FISDF_HIP(hipEventSynchronize(c->ev_stage));
+  if ((size_t)n > c->stage_cap) {
+    if (c->stage_pinned) FISDF_HIP(hipHostFree(c->stage_pinned));
+    FISDF_HIP(hipHostMalloc((void**)&c->stage_pinned, sizeof(int) * n, hipHostMallocDefault));
+    c->stage_cap = n;
+  }
+  std::memcpy(c->stage_pinned, h, sizeof(int) * n);
+  FISDF_HIP(hipMemcpyAsync(d, c->stage_pinned, sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
+  FISDF_HIP(hipEventRecord(c->ev_stage, c->stream));
+  return 0;
+}
+
 struct StageTimer {
   fisdf_ctx* c;
   int stage;
+  hipStream_t st;
   hipEvent_t a = nullptr, b = nullptr;
-  StageTimer(fisdf_ctx* c_, int st) : c(c_), stage(st) {
+  StageTimer(fisdf_ctx* c_, int stg, hipStream_t on = nullptr)
+      : c(c_), stage(stg), st(on ? on : c_->stream) {
     if (c->timing) {
       (void)hipEventCreate(&a);
       (void)hipEventCreate(&b);
-      (void)hipEventRecord(a, c->stream);
+      (void)hipEventRecord(a, st);
     }
   }
   ~StageTimer() {
     if (c->timing) {
-      (void)hipEventRecord(b, c->stream);
+      (void)hipEventRecord(b, st);
       c->events.push_back({stage, a, b});
     }
   }
@@ -170,6 +200,8 @@ int free_factors(fisdf_ctx* c) {
   if (c->f_Linv) FISDF_HIP(hipFree(c->f_Linv));
   if (c->f_piv) FISDF_HIP(hipFree(c->f_piv));
   if (c->f_rank_dev) FISDF_HIP(hipFree(c->f_rank_dev));
+  if (c->f_rank_pinned) FISDF_HIP(hipHostFree(c->f_rank_pinned));
+  c->f_rank_pinned = nullptr;
   c->f_L = c->f_Lp = c->f_Linv = nullptr;
   c->f_piv = c->f_rank_dev = nullptr;
   c->f_rank.clear();
@@ -211,6 +243,35 @@ int check_qlist(const int* qs, int nq, int nk, const char* who) {
   return 0;
 }
 
+// K-split for a HERK of n x n over K: the lower-triangle tile count times ks is chosen just
+// below a whole number of rounds of resident workgroups (3 per CU for the 64x64 ZGEMM tile),
+// so the last round is not a nearly empty tail; each split keeps >= 2048 of K (the split
+// partials cost 2 ks n^2 x 16 B of extra traffic).
+int pick_ksplit_herk(int n, int K, int ncu) {
+  const long nt = (n + 63) / 64, tiles = nt * (nt + 1) / 2;
+  const long slots = 3L * ncu;
+  int best = 1;
+  double best_eff = 0;
+  for (int m = 1; m <= 4; ++m) {
+    long ks = std::max(1L, (m * slots) / tiles);
+    ks = std::min<long>(ks, std::max(1, K / 2048));
+    const long T = tiles * ks;
+    const double eff = (double)T / ((double)((T + slots - 1) / slots) * slots);
+    if (eff > best_eff + 0.01 || (eff > best_eff - 0.01 && ks > best)) {
+      if (eff > best_eff) best_eff = eff;
+      best = (int)ks;
+    }
+  }
+  return best;
+}
+
+int num_cus(int device) {
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0)
+    n = 256;
+  return n;
+}
+
 int pick_ksplit(int M, int N, int K) {
   long tiles = (long)((M + 63) / 64) * ((N + 63) / 64);
   int ks = 1;
@@ -250,8 +311,18 @@ int fisdf_destroy(fisdf_ctx* c) {
   FISDF_HIP(hipStreamSynchronize(c->stream));
   for (auto& e : c->events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto& kv : c->phase_cache) (void)hipFree(kv.second);
+  if (c->f_pending) (void)hipEventSynchronize(c->ev_fac);
   free_factors(c);
+  if (c->f_scratch) (void)hipFree(c->f_scratch);
+  if (c->side) {
+    (void)hipStreamSynchronize(c->side);
+    (void)hipStreamDestroy(c->side);
+    (void)hipEventDestroy(c->ev_x4);
+    (void)hipEventDestroy(c->ev_fac);
+  }
   if (c->arena) (void)hipFree(c->arena);
+  if (c->ev_stage) (void)hipEventSynchronize(c->ev_stage), (void)hipEventDestroy(c->ev_stage);
+  if (c->stage_pinned) (void)hipHostFree(c->stage_pinned);
   if (c->maximag) (void)hipFree(c->maximag);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -565,7 +636,7 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
   FISDF_TRY(arena_get(c, cv.off, &base));
   cplx* FX = (cplx*)((char*)base + o1);
   int* dq = (int*)((char*)base + oq);
-  FISDF_HIP(hipMemcpyAsync(dq, h_qs, sizeof(int) * nq, hipMemcpyHostToDevice, c->stream));
+  FISDF_TRY(upload_ints(c, h_qs, nq, dq));
   for (int s0 = 0; s0 < nblk; s0 += gb) {
     const int m = std::min(gb, nblk - s0);
     const long nm = (long)nip * m;
@@ -577,7 +648,6 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
     FISDF_TRY(kmesh_y(c->stream, FX, nm, kmesh, h_qs, dq, nq, m, yT, (long)nip * ngrid, ngrid,
                       (long)g0 + s0, c->maximag + 1));
   }
-  FISDF_HIP(hipStreamSynchronize(c->stream));  // h_qs staging
   return 0;
 }
 
@@ -592,60 +662,86 @@ int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk
 }
 
 // ---- A4 ---------------------------------------------------------------------
-int fisdf_factor_x4_qs(fisdf_ctx* c, const void* x4all, const int* h_qs, int nq, int nip,
-                       double tol_rel, int* h_ranks) {
+int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int nq, int nip,
+                          double tol_rel) {
   FISDF_TRY(device_guard(c));
   const int nk = nq;
   FISDF_CHECK(nk > 0 && nip > 0, "factor_x4: bad sizes");
   FISDF_TRY(check_qlist(h_qs, nq, 1 << 30, "factor_x4"));
-  StageTimer tm(c, FISDF_ST_FACTOR);
-  FISDF_HIP(hipStreamSynchronize(c->stream));
+  if (c->f_pending) FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
+  if (!c->side) {
+    FISDF_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    FISDF_HIP(hipEventCreateWithFlags(&c->ev_x4, hipEventDisableTiming));
+    FISDF_HIP(hipEventCreateWithFlags(&c->ev_fac, hipEventDisableTiming));
+  }
   FISDF_TRY(free_factors(c));
   const int nb = c->f_nb;
   const int nblk = (nip + nb - 1) / nb;
   const long nn = (long)nip * nip;
-  // the listed x4_q: in place when the list is a contiguous range, else gathered (f_Lp is the
-  // staging buffer: it is overwritten by gather_lp only after pchol has consumed it)
   const bool contiguous = h_qs[nq - 1] - h_qs[0] == nq - 1;
   const void* x4v = (const cplx*)x4all + (long)h_qs[0] * nn;
   FISDF_HIP(hipMalloc(&c->f_L, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_Lp, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_Linv, sizeof(cplx) * (size_t)nk * nblk * nb * nb));
   FISDF_HIP(hipMalloc(&c->f_piv, sizeof(int) * (size_t)nk * nip));
-  if (!contiguous) {
-    for (int i = 0; i < nq; ++i)
-      FISDF_HIP(hipMemcpyAsync(c->f_Lp + i * nn, (const cplx*)x4all + (long)h_qs[i] * nn,
-                               sizeof(cplx) * nn, hipMemcpyDeviceToDevice, c->stream));
-    x4v = c->f_Lp;
-  }
-  c->f_qs.assign(h_qs, h_qs + nq);
-  c->f_nk = nk;
-  c->f_nip = nip;
+  FISDF_HIP(hipMalloc(&c->f_rank_dev, sizeof(int) * nk));
+  FISDF_HIP(hipHostMalloc((void**)&c->f_rank_pinned, sizeof(int) * nk, hipHostMallocDefault));
   Carver cv;
   size_t oR = cv.take(sizeof(int) * nk);
   size_t oD = cv.take(sizeof(double) * (size_t)nk * nip);
   size_t oF = cv.take(sizeof(int) * nk);
   size_t oW = cv.take(sizeof(double) * (size_t)nk * (1 + nip));
-  void* base;
-  FISDF_TRY(arena_get(c, cv.off, &base));
-  char* b = (char*)base;
-  FISDF_TRY(pchol(c->stream, (const cplx*)x4v, nip, nn, nip, nk, nip, tol_rel, 0.0, c->f_L,
-                  c->f_piv, (int*)(b + oR), (double*)(b + oD), (int*)(b + oF), (double*)(b + oW)));
-  c->f_rank.assign(nk, 0);
-  FISDF_HIP(hipMemcpyAsync(c->f_rank.data(), b + oR, sizeof(int) * nk, hipMemcpyDeviceToHost,
-                           c->stream));
-  FISDF_HIP(hipStreamSynchronize(c->stream));
-  FISDF_HIP(hipMalloc(&c->f_rank_dev, sizeof(int) * nk));
-  FISDF_HIP(hipMemcpyAsync(c->f_rank_dev, b + oR, sizeof(int) * nk, hipMemcpyDeviceToDevice,
-                           c->stream));
+  if (cv.off > c->f_scratch_size) {
+    if (c->f_scratch) FISDF_HIP(hipFree(c->f_scratch));
+    FISDF_HIP(hipMalloc(&c->f_scratch, cv.off));
+    c->f_scratch_size = cv.off;
+  }
+  char* b = (char*)c->f_scratch;
+  // the side stream starts once everything enqueued on `stream` so far (x4) is done; work
+  // enqueued on `stream` after this call (the y build) runs concurrently
+  FISDF_HIP(hipEventRecord(c->ev_x4, c->stream));
+  FISDF_HIP(hipStreamWaitEvent(c->side, c->ev_x4, 0));
+  StageTimer tm(c, FISDF_ST_FACTOR, c->side);
+  hipStream_t s = c->side;
+  if (!contiguous) {  // gather the listed x4_q (f_Lp is overwritten by gather_lp only later)
+    for (int i = 0; i < nq; ++i)
+      FISDF_HIP(hipMemcpyAsync(c->f_Lp + i * nn, (const cplx*)x4all + (long)h_qs[i] * nn,
+                               sizeof(cplx) * nn, hipMemcpyDeviceToDevice, s));
+    x4v = c->f_Lp;
+  }
+  c->f_qs.assign(h_qs, h_qs + nq);
+  c->f_nk = nk;
+  c->f_nip = nip;
+  FISDF_TRY(pchol(s, (const cplx*)x4v, nip, nn, nip, nk, nip, tol_rel, 0.0, c->f_L, c->f_piv,
+                  (int*)(b + oR), (double*)(b + oD), (int*)(b + oF), (double*)(b + oW)));
+  FISDF_HIP(hipMemcpyAsync(c->f_rank_pinned, b + oR, sizeof(int) * nk, hipMemcpyDeviceToHost, s));
+  FISDF_HIP(hipMemcpyAsync(c->f_rank_dev, b + oR, sizeof(int) * nk, hipMemcpyDeviceToDevice, s));
   // pivot-order factor padded to nip x nip (identity beyond the rank) so the small
   // back-substitutions of all q can run as one batch
-  for (int q = 0; q < nk; ++q)
-    if (h_ranks) h_ranks[q] = c->f_rank[q];
-  FISDF_TRY(gather_lp(c->stream, c->f_L, nip, nip, c->f_piv, c->f_rank_dev, nip, c->f_Lp, nk));
-  FISDF_TRY(trinv_blocks(c->stream, c->f_Lp, nip, nip, nn, nb, (long)nblk * nb * nb, c->f_Linv,
-                         nk));
+  FISDF_TRY(gather_lp(s, c->f_L, nip, nip, c->f_piv, c->f_rank_dev, nip, c->f_Lp, nk));
+  FISDF_TRY(trinv_blocks(s, c->f_Lp, nip, nip, nn, nb, (long)nblk * nb * nb, c->f_Linv, nk));
+  FISDF_HIP(hipEventRecord(c->ev_fac, s));
+  c->f_pending = true;
   return 0;
+}
+
+int fisdf_factor_x4_wait(fisdf_ctx* c, int* h_ranks) {
+  FISDF_TRY(device_guard(c));
+  if (c->f_pending) {
+    FISDF_HIP(hipEventSynchronize(c->ev_fac));
+    c->f_rank.assign(c->f_rank_pinned, c->f_rank_pinned + c->f_nk);
+    FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_fac, 0));  // factors before any later use
+    c->f_pending = false;
+  }
+  if (h_ranks)
+    for (int q = 0; q < c->f_nk; ++q) h_ranks[q] = c->f_rank[q];
+  return 0;
+}
+
+int fisdf_factor_x4_qs(fisdf_ctx* c, const void* x4all, const int* h_qs, int nq, int nip,
+                       double tol_rel, int* h_ranks) {
+  FISDF_TRY(fisdf_factor_x4_async(c, x4all, h_qs, nq, nip, tol_rel));
+  return fisdf_factor_x4_wait(c, h_ranks);
 }
 
 int fisdf_factor_x4(fisdf_ctx* c, const void* x4v, int q0, int q1, int nip, double tol_rel,
@@ -664,6 +760,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   FISDF_CHECK(c->f_nk == nq && c->f_nip == nip &&
                   std::equal(c->f_qs.begin(), c->f_qs.end(), h_qs),
               "fit_coulomb: call fisdf_factor_x4 on the same q-list first");
+  FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
   const long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
   const long nn = (long)nip * nip;
   const int nb = c->f_nb;
@@ -675,7 +772,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   cplx* Wq = (cplx*)Wqv;
   int rmax = 0;
   for (int lq = 0; lq < nq; ++lq) rmax = std::max(rmax, c->f_rank[lq]);
-  const int ks = pick_ksplit(rmax, rmax, (int)ngrid);
+  const int ks = pick_ksplit_herk(rmax, (int)ngrid, num_cus(c->device));
   const long rr = (long)rmax * rmax;
   const long sLi = (long)nblk * nb * nb;
   Carver cv;

@@ -71,15 +71,24 @@ struct Stage {
 };
 
 // HERK=true: C = alpha A A^H (OPA = N, OPB = C, B == A, M == N); only lower-triangle tiles
-// (ti >= tj) are launched, blockIdx.x enumerates them, and the epilogue mirrors the
-// conjugate into the upper triangle — half the MFMA work of the GEMM.
+// (ti >= tj) are launched and the epilogue mirrors the conjugate into the upper triangle —
+// half the MFMA work of the GEMM.
+//
+// XCD-aware tile order.  The grid is 1-D, padded to a multiple of 8: workgroup b runs on
+// XCD b % 8 (the dispatcher's round-robin; used for speed only, never for correctness) and
+// XCD x owns the contiguous chunk [x*per, (x+1)*per) of the tile order (z-slice major, then
+// M-tile fastest).  The workgroups resident on one XCD at a time are therefore neighbours
+// in that order: the M-tiles of one N-panel (GEMM), or all tiles of one K-split (HERK),
+// which read the same operand panels — served by that XCD's own 4 MB L2 instead of
+// each XCD re-fetching them from HBM / Infinity Cache.
 template <int OPA, int OPB, bool HERK>
 __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx alpha,
                                                     const cplx* __restrict__ A, long lda, long sA,
                                                     const cplx* __restrict__ B, long ldb, long sB,
                                                     cplx beta, cplx* __restrict__ C, long ldc, long sC,
                                                     int ksplit, int kchunk, cplx* __restrict__ work,
-                                                    int epi, unsigned long long* __restrict__ mon) {
+                                                    int epi, unsigned long long* __restrict__ mon,
+                                                    int nMt, int ntile, int ntot) {
   constexpr bool AK = !(OPA & 1);  // A stored [m][k]
   constexpr bool BKc = (OPB & 1);  // B stored [n][k]
   typedef Stage<AK> SA;
@@ -87,13 +96,16 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx al
   __shared__ cplx As[2][TILE];
   __shared__ cplx Bs[2][TILE];
 
-  const int split = blockIdx.z % ksplit;
-  const int bz = blockIdx.z / ksplit;
+  const int per = (int)(gridDim.x >> 3);
+  const int order = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (order >= ntot) return;  // padding of the 1-D grid (uniform per workgroup)
+  const int zz = order / ntile, t = order - zz * ntile;
+  const int split = zz % ksplit;
+  const int bz = zz / ksplit;
   A += (long)bz * sA;
   B += (long)bz * sB;
-  int ti = blockIdx.y, tj = blockIdx.x;
+  int ti = t % nMt, tj = t / nMt;
   if (HERK) {  // t = ti*(ti+1)/2 + tj, tj <= ti
-    const int t = blockIdx.x;
     ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
     while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
     while (ti * (ti + 1) / 2 > t) --ti;
@@ -269,8 +281,14 @@ template <int OPA, int OPB, bool HERK = false>
 void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cplx* A, long lda,
             long sA, const cplx* B, long ldb, long sB, cplx beta, cplx* C, long ldc, long sC,
             int ksplit, int kchunk, cplx* work, int epi, unsigned long long* mon) {
-  hipLaunchKernelGGL((zgemm_kernel<OPA, OPB, HERK>), grid, dim3(256), 0, s, M, N, K, alpha, A, lda, sA,
-                     B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work, epi, mon);
+  // grid = (N-tiles or triangle tiles, M-tiles, z-slices) -> padded 1-D XCD-aware order
+  const int nMt = HERK ? 1 : (int)grid.y;
+  const int ntile = (int)(grid.x * (HERK ? 1 : grid.y));
+  const long ntot = (long)ntile * grid.z;
+  const long per = (ntot + 7) / 8;
+  hipLaunchKernelGGL((zgemm_kernel<OPA, OPB, HERK>), dim3((unsigned)(8 * per)), dim3(256), 0, s, M,
+                     N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work,
+                     epi, mon, nMt, ntile, (int)ntot);
 }
 
 }  // namespace
@@ -288,9 +306,9 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
   kchunk = ((kchunk + BK - 1) / BK) * BK;
   if (kchunk == 0) kchunk = BK;
   ksplit = std::max(1, (K + kchunk - 1) / kchunk);
-  FISDF_CHECK((long)batch * ksplit < 65536, "zgemm: batch*ksplit exceeds grid.z");
+  FISDF_CHECK((long)((N + BN - 1) / BN) * ((M + BM - 1) / BM) * batch * ksplit < (1L << 31),
+              "zgemm: too many tiles");
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch * ksplit);
-  FISDF_CHECK(grid.y < 65536, "zgemm: M too large");
 #define FISDF_CASE(a, b)                                                                      \
   case a * 4 + b:                                                                             \
     launch<a, b>(s, grid, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit,   \

@@ -386,6 +386,10 @@ def build(df_obj):
     if df_obj._ao_grid is None:
         df_obj._ao_grid = d.to_dev(eval_ao_kpts(cell, df_obj.grids_coords(), kmesh))
     f = df_obj._ao_grid
+    # x4_q factorisation (replaces zgelsy's QRCP, :108) on the library's side stream,
+    # overlapped with the y build enqueued next on the main stream
+    if nq:
+        d.ctx.call("fisdf_factor_x4_async", _lib.ptr(x4), qs_c, nq, nip, float(df_obj.fit_tol))
     yT = d.empty((nq, nip, ngrid))
     if d.size == 1:
         d.ctx.call("fisdf_build_y_qs", _lib.ptr(f), ngrid * nao, 0, ngrid, ngrid, _lib.ptr(X),
@@ -407,8 +411,7 @@ def build(df_obj):
 
     ranks = np.zeros(nq, np.int32)
     if nq:
-        d.ctx.call("fisdf_factor_x4_qs", _lib.ptr(x4), qs_c, nq, nip, float(df_obj.fit_tol),
-                   ranks.ctypes.data_as(_lib._ip))
+        d.ctx.call("fisdf_factor_x4_wait", ranks.ctypes.data_as(_lib._ip))
     if d.size > 1:
         if work is not None:
             work.wait()

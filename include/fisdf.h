@@ -119,6 +119,13 @@ int fisdf_factor_x4(fisdf_ctx* ctx, const void* d_x4, int q0, int q1, int nip, d
 /* q-list form: factors x4_q for q = h_qs[i] (ascending); h_ranks (nq). */
 int fisdf_factor_x4_qs(fisdf_ctx* ctx, const void* d_x4, const int* h_qs, int nq, int nip,
                        double tol_rel, int* h_ranks);
+/* Asynchronous form: enqueues the factorisation on the context's side stream (after the work
+ * already enqueued on the main stream, i.e. x4) and returns at once, so the y build enqueued
+ * next overlaps it.  fisdf_factor_x4_wait (synchronous on the side stream) returns the ranks;
+ * fisdf_fit_coulomb_qs waits by itself. */
+int fisdf_factor_x4_async(fisdf_ctx* ctx, const void* d_x4, const int* h_qs, int nq, int nip,
+                          double tol_rel);
+int fisdf_factor_x4_wait(fisdf_ctx* ctx, int* h_ranks /* nq, may be NULL */);
 
 /* ---- A4+A5: fit + FFT Coulomb for the factored shard q in [q0, q1) (fftisdf.py:97-121)
  * Needs fisdf_factor_x4 on the same range.  W_q = zeta_q z_q^H computed as
