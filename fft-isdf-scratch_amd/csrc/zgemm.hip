@@ -70,6 +70,75 @@ struct Stage {
   }
 };
 
+// Epilogue shared by both kernels: split-K partials, the fused y-square epilogue, or
+// C = alpha acc + beta C; HERK blocks strictly below the diagonal are mirrored.
+template <bool HERK>
+__device__ __forceinline__ void zgemm_epilogue(int M, int N, cplx alpha, cplx beta,
+                                               cplx* __restrict__ C, long ldc, long sC, int ksplit,
+                                               int split, int bz, cplx* __restrict__ work, int epi,
+                                               unsigned long long* __restrict__ mon, int m0, int n0,
+                                               int wm, int wn, int lane, int mask,
+                                               const f64x4 (&accR)[2][2], const f64x4 (&accI)[2][2]) {
+  if (ksplit > 1) {
+    cplx* Wp = work + ((long)bz * ksplit + split) * (long)M * N;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
+          int col = n0 + wn + ni * 16 + (lane & 15);
+          const bool mirror = HERK && (m0 + wm + mi * 16 > n0 + wn + ni * 16);
+          if (((mask >> (mi * 2 + ni)) & 1) && row < M && col < N) {
+            Wp[(long)row * N + col] = cmk(accR[mi][ni][r], accI[mi][ni][r]);
+            if (mirror) Wp[(long)col * N + row] = cmk(accR[mi][ni][r], -accI[mi][ni][r]);
+          }
+        }
+    return;
+  }
+  C += (long)bz * sC;
+  if (epi == EPI_SQUARE_RE) {
+    // y_s = Re(alpha acc)^2 + 0i, fused (fftisdf.py:83); monitor max|Im| (fftisdf.py:81)
+    double mi_ = 0.0;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
+          int col = n0 + wn + ni * 16 + (lane & 15);
+          if (row < M && col < N) {
+            cplx v = cmul(alpha, cmk(accR[mi][ni][r], accI[mi][ni][r]));
+            C[(long)row * ldc + col] = cmk(v.x * v.x, 0.0);
+            mi_ = fmax(mi_, fabs(v.y));
+          }
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mi_ = fmax(mi_, __shfl_xor(mi_, o, 64));
+    if (lane == 0 && mon) atomicMax(mon, (unsigned long long)__double_as_longlong(mi_));
+    return;
+  }
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
+        int col = n0 + wn + ni * 16 + (lane & 15);
+        const bool mirror = HERK && (m0 + wm + mi * 16 > n0 + wn + ni * 16);
+        if (((mask >> (mi * 2 + ni)) & 1) && row < M && col < N) {
+          cplx v = cmul(alpha, cmk(accR[mi][ni][r], accI[mi][ni][r]));
+          cplx* cp = C + (long)row * ldc + col;
+          if (beta.x != 0.0 || beta.y != 0.0) v = cadd(v, cmul(beta, *cp));
+          *cp = v;
+          if (mirror) C[(long)col * ldc + row] = cconj(v);
+        }
+      }
+}
+
 // HERK=true: C = alpha A A^H (OPA = N, OPB = C, B == A, M == N); only lower-triangle tiles
 // (ti >= tj) are launched and the epilogue mirrors the conjugate into the upper triangle —
 // half the MFMA work of the GEMM.
@@ -202,63 +271,214 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx al
     }
   }
 
-  // epilogue
-  if (ksplit > 1) {
-    cplx* Wp = work + ((long)bz * ksplit + split) * (long)M * N;
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
-          int col = n0 + wn + ni * 16 + (lane & 15);
-          if (row < M && col < N) {
-            Wp[(long)row * N + col] = cmk(accR[mi][ni][r], accI[mi][ni][r]);
-            if (HERK && ti != tj) Wp[(long)col * N + row] = cmk(accR[mi][ni][r], -accI[mi][ni][r]);
-          }
-        }
-    return;
-  }
-  C += (long)bz * sC;
-  if (epi == EPI_SQUARE_RE) {
-    // y_s = Re(alpha acc)^2 + 0i, fused (fftisdf.py:83); monitor max|Im| (fftisdf.py:81)
-    double mi_ = 0.0;
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
-          int col = n0 + wn + ni * 16 + (lane & 15);
-          if (row < M && col < N) {
-            cplx v = cmul(alpha, cmk(accR[mi][ni][r], accI[mi][ni][r]));
-            C[(long)row * ldc + col] = cmk(v.x * v.x, 0.0);
-            mi_ = fmax(mi_, fabs(v.y));
-          }
-        }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mi_ = fmax(mi_, __shfl_xor(mi_, o, 64));
-    if (lane == 0 && mon) atomicMax(mon, (unsigned long long)__double_as_longlong(mi_));
-    return;
-  }
+  // every block was computed; strictly-upper HERK blocks are written as mirrors instead
+  int mask = 0;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
+    for (int ni = 0; ni < 2; ++ni) {
+      const int r0 = m0 + wm + mi * 16, c0 = n0 + wn + ni * 16;
+      mask |= (r0 < M && c0 < N && !(HERK && c0 > r0) ? 1 : 0) << (mi * 2 + ni);
+    }
+  zgemm_epilogue<HERK>(M, N, alpha, beta, C, ldc, sC, ksplit, split, bz, work, epi, mon, m0, n0, wm,
+                       wn, lane, mask, accR, accI);
+}
+
+// ---- LDS-DMA variant -------------------------------------------------------------------
+// Same tile, tile order, masks and epilogue as zgemm_kernel, but the operand tiles go
+// global -> LDS directly (global_load_lds_dwordx4, no staging registers) through a THREE-deep
+// LDS ring: the loads of K-step s+2 are issued at step s, so each has two full steps to land
+// (the register-staged kernel waited on its loads one step after issue: at 3 workgroups/CU
+// its per-step time was set by L2/HBM latency, not by the MFMA pipe).  The LDS image is
+// lane-linear per wave-instruction (dest = base + lane*16); the K-contiguous operands keep
+// their XOR swizzle by permuting the per-lane SOURCE address instead.  Out-of-range lanes
+// read a zero page; conjugation is folded into the MFMA operand signs.
+constexpr int NST = 3;
+constexpr int LPW = TILE / (64 * 4);  // glds wave-instructions per operand per step per wave
+__device__ cplx g_zero_page[64];      // zero-initialised device global
+
+template <int OPA, int OPB, bool HERK>
+__global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cplx alpha,
+                                                         const cplx* __restrict__ A, long lda, long sA,
+                                                         const cplx* __restrict__ B, long ldb, long sB,
+                                                         cplx beta, cplx* __restrict__ C, long ldc, long sC,
+                                                         int ksplit, int kchunk, cplx* __restrict__ work,
+                                                         int epi, unsigned long long* __restrict__ mon,
+                                                         int nMt, int ntile, int ntot) {
+  constexpr bool AK = !(OPA & 1);  // A stored [m][k]
+  constexpr bool BKc = (OPB & 1);  // B stored [n][k]
+  constexpr bool CA = (OPA & 2) != 0, CB = (OPB & 2) != 0;
+  typedef Stage<AK> SA;
+  typedef Stage<BKc> SB;
+  __shared__ cplx sm[NST * 2 * TILE];  // [stage][A|B][TILE], one object (48 KB at BK = 8)
+
+  const int per = (int)(gridDim.x >> 3);
+  const int order = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (order >= ntot) return;
+  const int zz = order / ntile, t = order - zz * ntile;
+  const int split = zz % ksplit;
+  const int bz = zz / ksplit;
+  A += (long)bz * sA;
+  B += (long)bz * sB;
+  int ti = t % nMt, tj = t / nMt;
+  if (HERK) {
+    ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+    while (ti * (ti + 1) / 2 > t) --ti;
+    tj = t - ti * (ti + 1) / 2;
+  }
+  const int m0 = ti * BM, n0 = tj * BN;
+  const int kbeg = split * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wave = (w + ti + tj) & 3;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+
+  // per-lane source of each glds: slot s = (w*LPW + j)*64 + lane of the operand tile
+  const cplx* srcA[LPW];
+  const cplx* srcB[LPW];
+  int kA[LPW], kB[LPW];
+  bool rowA[LPW], rowB[LPW];
+  long stepA, stepB;  // element advance of the source per K-step
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
-        int col = n0 + wn + ni * 16 + (lane & 15);
-        if (row < M && col < N) {
-          cplx v = cmul(alpha, cmk(accR[mi][ni][r], accI[mi][ni][r]));
-          cplx* cp = C + (long)row * ldc + col;
-          if (beta.x != 0.0 || beta.y != 0.0) v = cadd(v, cmul(beta, *cp));
-          *cp = v;
-          if (HERK && ti != tj) C[(long)col * ldc + row] = cconj(v);
+  for (int j = 0; j < LPW; ++j) {
+    const int sl = (w * LPW + j) * 64 + lane;
+    int x, k;
+    if (AK) { x = sl / BK; k = (sl % BK) ^ (x & (BK - 1)); }
+    else { x = sl % 64; k = sl / 64; }
+    rowA[j] = m0 + x < M;
+    kA[j] = k;
+    srcA[j] = A + (AK ? (long)(m0 + x) * lda + (kbeg + k) : (long)(kbeg + k) * lda + (m0 + x));
+    if (BKc) { x = sl / BK; k = (sl % BK) ^ (x & (BK - 1)); }
+    else { x = sl % 64; k = sl / 64; }
+    rowB[j] = n0 + x < N;
+    kB[j] = k;
+    srcB[j] = B + (BKc ? (long)(n0 + x) * ldb + (kbeg + k) : (long)(kbeg + k) * ldb + (n0 + x));
+  }
+  stepA = AK ? (long)BK : (long)BK * lda;
+  stepB = BKc ? (long)BK : (long)BK * ldb;
+
+  // The LDS-DMA is issued from inline asm so that hipcc's waitcnt pass does not see it (it
+  // would drain vmcnt(0) before the next ds_read); its completion is counted by hand below.
+  const cplx* zp = g_zero_page;
+  const unsigned lds0 = (unsigned)(uintptr_t)sm;
+  auto glds = [&](const cplx* src, unsigned lds_byte) {
+    unsigned keep;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_byte);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+  };
+  auto issue = [&](int st) {  // K-step st -> ring slot st % NST
+    const int buf = st % NST;
+    const int k0 = kbeg + st * BK;
+    const unsigned la = lds0 + (unsigned)((buf * 2 + 0) * TILE) * 16u;
+    const unsigned lb = lds0 + (unsigned)((buf * 2 + 1) * TILE) * 16u;
+#pragma unroll
+    for (int j = 0; j < LPW; ++j) {
+      const cplx* pa = (rowA[j] && k0 + kA[j] < kend) ? srcA[j] + st * stepA : zp;
+      glds(pa, la + (unsigned)((w * LPW + j) * 64) * 16u);
+      const cplx* pb = (rowB[j] && k0 + kB[j] < kend) ? srcB[j] + st * stepB : zp;
+      glds(pb, lb + (unsigned)((w * LPW + j) * 64) * 16u);
+    }
+  };
+
+  f64x4 accR[2][2], accI[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      accR[i][j] = f64x4{0, 0, 0, 0};
+      accI[i][j] = f64x4{0, 0, 0, 0};
+    }
+
+  int mask = 0;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int r0 = m0 + wm + mi * 16, c0 = n0 + wn + ni * 16;
+      const bool live = r0 < M && c0 < N && !(HERK && c0 > r0);
+      mask |= (live ? 1 : 0) << (mi * 2 + ni);
+    }
+
+  const int nsteps = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nsteps > 0) {
+    issue(0);
+    issue(1);
+  }
+  const int i16 = lane & 15, kq = lane >> 4;
+  auto mainloop = [&](auto maskc) {
+    constexpr int MASK = decltype(maskc)::value;
+    for (int s = 0; s < nsteps; ++s) {
+      // own loads of step s retired (step s+1's 2*LPW stay in flight), then every wave's:
+      // the barrier also retires all reads of the slot step s+2 is about to overwrite
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * LPW) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      issue(s + 2);
+      const int cur = s % NST;
+      const cplx* as = sm + (long)(cur * 2 + 0) * TILE;
+      const cplx* bs = sm + (long)(cur * 2 + 1) * TILE;
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 4) {
+        const int k = kk + kq;
+        cplx a[2], b[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          a[u] = as[SA::slot(wm + u * 16 + i16, k)];
+          b[u] = bs[SB::slot(wn + u * 16 + i16, k)];
         }
+        // op(A) = a (or conj a), op(B) = b (or conj b):
+        //   Re += ar br - ai' bi' ;  Im += ar bi' + ai' br   (ai' = +-ai, bi' = +-bi)
+        double ar[2], ai[2], nai[2], br[2], bi[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          ar[u] = a[u].x;
+          ai[u] = CA ? -a[u].y : a[u].y;
+          nai[u] = -ai[u];
+          br[u] = b[u].x;
+          bi[u] = CB ? -b[u].y : b[u].y;
+        }
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            if ((MASK >> (mi * 2 + ni)) & 1)
+              accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], accR[mi][ni], 0, 0, 0);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            if ((MASK >> (mi * 2 + ni)) & 1)
+              accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], bi[ni], accI[mi][ni], 0, 0, 0);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            if ((MASK >> (mi * 2 + ni)) & 1)
+              accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[mi], bi[ni], accR[mi][ni], 0, 0, 0);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            if ((MASK >> (mi * 2 + ni)) & 1)
+              accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], br[ni], accI[mi][ni], 0, 0, 0);
       }
+    }
+  };
+  switch (mask) {
+    case 13: mainloop(std::integral_constant<int, 13>{}); break;
+    case 5: mainloop(std::integral_constant<int, 5>{}); break;
+    case 3: mainloop(std::integral_constant<int, 3>{}); break;
+    case 1: mainloop(std::integral_constant<int, 1>{}); break;
+    case 0: mainloop(std::integral_constant<int, 0>{}); break;
+    default: mainloop(std::integral_constant<int, 15>{}); break;
+  }
+  // drain the (zero-page / unused) loads still in flight before the workgroup exits
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  zgemm_epilogue<HERK>(M, N, alpha, beta, C, ldc, sC, ksplit, split, bz, work, epi, mon, m0, n0, wm,
+                       wn, lane, mask, accR, accI);
 }
 
 // C = alpha * sum_s work[s] + beta * C  (deterministic split-K reduction)
@@ -277,6 +497,15 @@ __global__ void ksplit_reduce(int M, int N, int ksplit, const cplx* __restrict__
   }
 }
 
+// 0 = register-staged kernel, 1 = LDS-DMA kernel (default; FISDF_GEMM=reg selects 0)
+int gemm_variant() {
+  static int v = [] {
+    const char* e = getenv("FISDF_GEMM");
+    return (e && std::string(e) == "reg") ? 0 : 1;
+  }();
+  return v;
+}
+
 template <int OPA, int OPB, bool HERK = false>
 void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cplx* A, long lda,
             long sA, const cplx* B, long ldb, long sB, cplx beta, cplx* C, long ldc, long sC,
@@ -286,9 +515,14 @@ void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cpl
   const int ntile = (int)(grid.x * (HERK ? 1 : grid.y));
   const long ntot = (long)ntile * grid.z;
   const long per = (ntot + 7) / 8;
-  hipLaunchKernelGGL((zgemm_kernel<OPA, OPB, HERK>), dim3((unsigned)(8 * per)), dim3(256), 0, s, M,
-                     N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work,
-                     epi, mon, nMt, ntile, (int)ntot);
+  if (gemm_variant() == 1)
+    hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK>), dim3((unsigned)(8 * per)), dim3(256), 0,
+                       s, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk,
+                       work, epi, mon, nMt, ntile, (int)ntot);
+  else
+    hipLaunchKernelGGL((zgemm_kernel<OPA, OPB, HERK>), dim3((unsigned)(8 * per)), dim3(256), 0, s, M,
+                       N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work,
+                       epi, mon, nMt, ntile, (int)ntot);
 }
 
 }  // namespace
