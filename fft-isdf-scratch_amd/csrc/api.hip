@@ -4,6 +4,7 @@
 #include "../../include/fisdf.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -625,9 +626,14 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
   const cplx* f = (const cplx*)fv;
   const cplx* X = (const cplx*)Xv;
   cplx* yT = (cplx*)yTv;
-  // sub-block so that the temporaries stay ~<= 1 GB
+  // grid sub-blocks sized so the FX temporary (nk x nip x gb) stays resident in the 256 MB
+  // Infinity Cache between the GEMM that writes it and the k-mesh DFT that reads it
+  static const long yblk_bytes = [] {
+    const char* e = getenv("FISDF_YBLK_MB");
+    return (e ? atol(e) : 96L) << 20;
+  }();
   const long per_g = (long)nk * nip * sizeof(cplx);
-  int gb = (int)std::max(64L, std::min<long>(nblk, (1L << 30) / std::max(per_g, 1L)));
+  int gb = (int)std::max(64L, std::min<long>(nblk, yblk_bytes / std::max(per_g, 1L)));
   gb = std::min(gb, std::max(nblk, 1));
   Carver cv;
   size_t o1 = cv.take((size_t)per_g * gb);

@@ -12,6 +12,8 @@
 // between two LDS buffers, and writes the tile back.  The first pass (axis 2)
 // fuses the row gather (interpolation-point pivots) and the exp(-i k.r) phase,
 // the last pass (axis 0) fuses the Coulomb weight.
+#include <type_traits>
+
 #include "common.h"
 
 #include <map>
@@ -282,6 +284,221 @@ __global__ __launch_bounds__(256) void fft_plane_kernel(
   for (int e = tid; e < P; e += nthr) dstp[e] = a[e];
 }
 
+// ---- register FFT kernels for the common meshes (compile-time line length) -------------
+// A line of N points lives in one lane's registers and is transformed by a fully unrolled
+// mixed-radix Cooley-Tukey recursion (radix 4/2/3/5, prime lengths by direct DFT) with
+// compile-time twiddle indices: trivial twiddles (+-1, +-i) cost nothing and the rest are
+// wave-uniform loads from the n-th-root table.  The plane kernel does axes 2 and 1 of one
+// (i0) plane per wave through a padded LDS image; the axis-0 kernel needs no LDS at all:
+// lane = consecutive (i1, i2) column, so every one of its N0 loads/stores is a contiguous
+// 16*64-byte wave access.
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+constexpr int first_factor(int n) {
+  return (n % 4 == 0 && n > 4) ? 4 : (n % 2 == 0 && n > 2) ? 2 : (n % 3 == 0 && n > 3) ? 3
+       : (n % 5 == 0 && n > 5) ? 5 : n;
+}
+
+// v * W_NT^E (W_NT^t = exp(-2 pi i t / NT) = W[t])
+template <int NT, int E>
+__device__ __forceinline__ cplx twmul(cplx v, const cplx* __restrict__ W) {
+  constexpr int e = E % NT;
+  if constexpr (e == 0) return v;
+  else if constexpr (4 * e == NT) return cmk(v.y, -v.x);       // * (-i)
+  else if constexpr (2 * e == NT) return cmk(-v.x, -v.y);      // * (-1)
+  else if constexpr (4 * e == 3 * NT) return cmk(-v.y, v.x);   // * (+i)
+  else return cmul(v, W[e]);
+}
+
+template <int N, int NT>
+__device__ __forceinline__ void fft_rec(cplx* x, const cplx* __restrict__ W) {
+  if constexpr (N == 1) {
+  } else if constexpr (N == 2) {
+    const cplx a = x[0], b = x[1];
+    x[0] = cadd(a, b);
+    x[1] = csub(a, b);
+  } else if constexpr (N == 4) {
+    const cplx a0 = cadd(x[0], x[2]), a1 = csub(x[0], x[2]);
+    const cplx b0 = cadd(x[1], x[3]), b1 = csub(x[1], x[3]);
+    const cplx b1m = cmk(b1.y, -b1.x);  // b1 * (-i)
+    x[0] = cadd(a0, b0);
+    x[2] = csub(a0, b0);
+    x[1] = cadd(a1, b1m);
+    x[3] = csub(a1, b1m);
+  } else if constexpr (first_factor(N) == N) {  // prime: direct DFT
+    cplx o[N];
+    static_for<0, N>([&](auto kc) {
+      constexpr int K = decltype(kc)::value;
+      cplx acc = x[0];
+      static_for<1, N>([&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        acc = cadd(acc, twmul<NT, ((J * K) % N) * (NT / N)>(x[J], W));
+      });
+      o[K] = acc;
+    });
+    static_for<0, N>([&](auto kc) { x[decltype(kc)::value] = o[decltype(kc)::value]; });
+  } else {
+    // n = B n1 + n2, k = k1 + A k2:  X = DFT_B_n2[ W_N^(n2 k1) DFT_A_n1[x] ]
+    constexpr int A = first_factor(N), B = N / A;
+    cplx y[N];
+    static_for<0, B>([&](auto n2c) {
+      constexpr int N2 = decltype(n2c)::value;
+      cplx t[A];
+      static_for<0, A>([&](auto c) { t[decltype(c)::value] = x[B * decltype(c)::value + N2]; });
+      fft_rec<A, NT>(t, W);
+      static_for<0, A>([&](auto c) {
+        constexpr int K1 = decltype(c)::value;
+        y[K1 * B + N2] = twmul<NT, (N2 * K1) * (NT / N)>(t[K1], W);
+      });
+    });
+    static_for<0, A>([&](auto k1c) {
+      constexpr int K1 = decltype(k1c)::value;
+      cplx t[B];
+      static_for<0, B>([&](auto c) { t[decltype(c)::value] = y[K1 * B + decltype(c)::value]; });
+      fft_rec<B, NT>(t, W);
+      static_for<0, B>([&](auto c) { x[K1 + A * decltype(c)::value] = t[decltype(c)::value]; });
+    });
+  }
+}
+
+// axes 2 and 1 of one (row, i0) plane per 64-lane workgroup; fuses the row gather and the
+// separable phase exp(-i k.r) = e0(i0) e1(i1) e2(i2)
+template <int NN>
+__global__ __launch_bounds__(64) void fft_plane_reg(const cplx* __restrict__ in, long in_ld,
+                                                    const int* __restrict__ rowidx, cplx* out,
+                                                    long out_ld, int rows, int n0,
+                                                    const cplx* __restrict__ W, double kd0,
+                                                    double kd1, double kd2, int use_phase) {
+  constexpr int P = NN * NN, LD = NN + 1;
+  __shared__ cplx img[NN * LD];
+  __shared__ cplx ph1[NN], ph2[NN];
+  const int lane = threadIdx.x;
+  const int row = blockIdx.x / n0, i0 = blockIdx.x % n0;
+  if (row >= rows) return;
+  const cplx* src = in + (long)(rowidx ? rowidx[row] : row) * in_ld + (long)i0 * P;
+  cplx* dst = out + (long)row * out_ld + (long)i0 * P;
+  constexpr int U = (P + 63) / 64;
+  cplx v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = lane + 64 * u;
+    v[u] = src[e < P ? e : 0];
+  }
+  if (use_phase && lane < NN) {
+    double s0, c0, s, c;
+    sincos(-fftfreq(i0, n0) * kd0, &s0, &c0);
+    sincos(-fftfreq(lane, NN) * kd1, &s, &c);
+    ph1[lane] = cmul(cmk(c, s), cmk(c0, s0));
+    sincos(-fftfreq(lane, NN) * kd2, &s, &c);
+    ph2[lane] = cmk(c, s);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = lane + 64 * u;
+    if (e < P) {
+      const int i1 = e / NN, i2 = e - i1 * NN;
+      cplx x = v[u];
+      if (use_phase) x = cmul(x, cmul(ph1[i1], ph2[i2]));
+      img[i1 * LD + i2] = x;
+    }
+  }
+  __syncthreads();
+  if (lane < NN) {  // axis 2: line i1 = lane
+    cplx x[NN];
+#pragma unroll
+    for (int p = 0; p < NN; ++p) x[p] = img[lane * LD + p];
+    fft_rec<NN, NN>(x, W);
+#pragma unroll
+    for (int p = 0; p < NN; ++p) img[lane * LD + p] = x[p];
+  }
+  __syncthreads();
+  if (lane < NN) {  // axis 1: line i2 = lane
+    cplx x[NN];
+#pragma unroll
+    for (int p = 0; p < NN; ++p) x[p] = img[p * LD + lane];
+    fft_rec<NN, NN>(x, W);
+#pragma unroll
+    for (int p = 0; p < NN; ++p) img[p * LD + lane] = x[p];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = lane + 64 * u;
+    if (e < P) {
+      const int i1 = e / NN, i2 = e - i1 * NN;
+      dst[e] = img[i1 * LD + i2];
+    }
+  }
+}
+
+// axis 0: one line (row, column l = i1*n1n2... ) per lane, N0 strided loads, in registers
+template <int N0>
+__global__ __launch_bounds__(256) void fft_axis0_reg(const cplx* in, long in_ld, cplx* out,
+                                                     long out_ld, int rows, int P,
+                                                     const cplx* __restrict__ W,
+                                                     const double* __restrict__ weight) {
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (t >= (long)rows * P) return;
+  const int row = (int)(t / P), l = (int)(t - (long)row * P);
+  const cplx* src = in + (long)row * in_ld + l;
+  cplx* dst = out + (long)row * out_ld + l;
+  cplx x[N0];
+#pragma unroll
+  for (int p = 0; p < N0; ++p) x[p] = src[(long)p * P];
+  fft_rec<N0, N0>(x, W);
+  if (weight) {
+#pragma unroll
+    for (int p = 0; p < N0; ++p) x[p] = cscale(x[p], weight[(long)p * P + l]);
+  }
+#pragma unroll
+  for (int p = 0; p < N0; ++p) dst[(long)p * P] = x[p];
+}
+
+// meshes with register kernels (cubic n^3 for the plane kernel; any n0 for axis 0)
+#define FISDF_REG_SIZES(X) X(8) X(12) X(13) X(15) X(16) X(18) X(20) X(24) X(25) X(27) X(30) X(32) X(36) X(40) X(45) X(48)
+
+int fft_plane_reg_launch(hipStream_t s, int n, const cplx* in, long in_ld, const int* rowidx,
+                         cplx* out, long out_ld, int rows, int n0, const cplx* W, const double* kd,
+                         bool* done) {
+  *done = false;
+  const double k0 = kd ? kd[0] : 0, k1 = kd ? kd[1] : 0, k2 = kd ? kd[2] : 0;
+  const long planes = (long)rows * n0;
+#define FISDF_PL(N)                                                                            \
+  if (n == N) {                                                                                \
+    hipLaunchKernelGGL(fft_plane_reg<N>, dim3((unsigned)planes), dim3(64), 0, s, in, in_ld,     \
+                       rowidx, out, out_ld, rows, n0, W, k0, k1, k2, kd ? 1 : 0);               \
+    *done = true;                                                                              \
+  }
+  FISDF_REG_SIZES(FISDF_PL)
+#undef FISDF_PL
+  if (*done) FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int fft_axis0_reg_launch(hipStream_t s, int n0, const cplx* in, long in_ld, cplx* out, long out_ld,
+                         int rows, int P, const cplx* W, const double* weight, bool* done) {
+  *done = false;
+  const long threads = (long)rows * P;
+  const unsigned blocks = (unsigned)((threads + 255) / 256);
+#define FISDF_AX(N)                                                                            \
+  if (n0 == N) {                                                                               \
+    hipLaunchKernelGGL(fft_axis0_reg<N>, dim3(blocks), dim3(256), 0, s, in, in_ld, out, out_ld, \
+                       rows, P, W, weight);                                                    \
+    *done = true;                                                                              \
+  }
+  FISDF_REG_SIZES(FISDF_AX)
+#undef FISDF_AX
+  if (*done) FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
 bool needs_big(const Stages& st) {
   for (int i = 0; i < st.nst; ++i)
     if (st.radix[i] > 5) return true;
@@ -387,6 +604,27 @@ int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* ou
           int rows, int n0, int n1, int n2, const double* kd, const double* weight, cplx* /*work*/) {
   if (rows == 0) return 0;
   FISDF_CHECK(in != out || rowidx == nullptr, "fft: in-place pass cannot gather rows");
+  if (n1 == n2) {  // register kernels: square (i1, i2) planes of a listed size, listed n0
+    const cplx *W12 = nullptr, *W0 = nullptr;
+    FISDF_TRY(get_twiddles(n1, &W12));
+    FISDF_TRY(get_twiddles(n0, &W0));
+    bool ok1 = false, ok0 = false;
+    FISDF_CHECK((long)rows * n0 < (1L << 31) && (long)rows * n1 * n2 < (1L << 38), "fft: too large");
+    // probe both specialisations before launching anything
+    const int dims_ok = [&] {
+      int a = 0, b = 0;
+#define FISDF_HAS(N) if (n1 == N) a = 1; if (n0 == N) b = 1;
+      FISDF_REG_SIZES(FISDF_HAS)
+#undef FISDF_HAS
+      return a && b;
+    }();
+    if (dims_ok) {
+      FISDF_TRY(fft_plane_reg_launch(s, n1, in, in_ld, rowidx, out, out_ld, rows, n0, W12, kd, &ok1));
+      FISDF_TRY(fft_axis0_reg_launch(s, n0, out, out_ld, out, out_ld, rows, n1 * n2, W0, weight, &ok0));
+      FISDF_CHECK(ok1 && ok0, "fft: register kernel dispatch failed");
+      return 0;
+    }
+  }
   const size_t plane_lds = sizeof(cplx) * (4 * MAXN + 2 * (size_t)n1 * n2);
   if (plane_lds <= 96 * 1024) {
     // axes 2+1 fused per (i1,i2) plane, then axis 0 with the Coulomb weight: 2 HBM passes
