@@ -33,6 +33,10 @@ struct fisdf_ctx {
   std::map<std::vector<double>, cplx*> phase_cache;
   // per-q factors of x4_q (fisdf_factor_x4)
   std::vector<int> f_qs;  // the factored q (ascending), slot i <-> q = f_qs[i]
+  std::vector<char> f_real;  // slot factored as real (self-conjugate q, kmesh given)
+  // per (mesh, lattice, k_q): device list of G with asymmetric Coulomb weight (asym_list)
+  struct Asym { int* idx = nullptr; int n = 0; };
+  std::map<std::vector<double>, Asym> asym_cache;
   int f_nk = 0, f_nip = 0, f_nb = 64;
   cplx* f_L = nullptr;      // (nk, nip, nip) raw left-looking factor (row order)
   cplx* f_Lp = nullptr;     // (nk, nip*nip) pivot-order factor, ld = rank_q
@@ -207,6 +211,7 @@ int free_factors(fisdf_ctx* c) {
   c->f_piv = c->f_rank_dev = nullptr;
   c->f_rank.clear();
   c->f_qs.clear();
+  c->f_real.clear();
   c->f_nk = c->f_nip = 0;
   return 0;
 }
@@ -227,6 +232,39 @@ int select_gram(fisdf_ctx* c, const cplx* x0, int nk, int q0, int q1, int ng0, i
   FISDF_TRY(herk(c->stream, ng0, K, 1.0, tmp, K, x2, ng0, ks, work));
   if (work) FISDF_HIP(hipFreeAsync(work, c->stream));
   (void)nk;
+  return 0;
+}
+
+// q is its own time-reversal partner (2 k_q in the reciprocal lattice): Phi[:, q] is real, so
+// x4_q, y_q and z_q are real and W_q = Zhat diag(c) Zhat^H is real (Hermitian-symmetric
+// spectrum) — the fit runs with a real factor (GEMM_A_REAL) and a real-part HERK
+bool self_conjugate(const int kmesh[3], int q) {
+  const int i2 = q % kmesh[2], i1 = (q / kmesh[2]) % kmesh[1], i0 = q / (kmesh[1] * kmesh[2]);
+  return (2 * i0) % kmesh[0] == 0 && (2 * i1) % kmesh[1] == 0 && (2 * i2) % kmesh[2] == 0;
+}
+
+// cached asym_list of a self-conjugate q (one synchronous count read the first time)
+int get_asym(fisdf_ctx* c, const int mesh[3], const int kmesh[3], const double a[9], int q,
+             const double* wt, const fisdf_ctx::Asym** out) {
+  std::vector<double> key = {(double)mesh[0], (double)mesh[1], (double)mesh[2], (double)kmesh[0],
+                             (double)kmesh[1], (double)kmesh[2], (double)q};
+  for (int i = 0; i < 9; ++i) key.push_back(a[i]);
+  auto it = c->asym_cache.find(key);
+  if (it == c->asym_cache.end()) {
+    const int i2 = q % kmesh[2], i1 = (q / kmesh[2]) % kmesh[1], i0 = q / (kmesh[1] * kmesh[2]);
+    const int m[3] = {2 * i0 / kmesh[0], 2 * i1 / kmesh[1], 2 * i2 / kmesh[2]};
+    const long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
+    fisdf_ctx::Asym as;
+    int* cnt = nullptr;
+    FISDF_HIP(hipMalloc(&as.idx, sizeof(int) * (ngrid + 1)));
+    cnt = as.idx + ngrid;
+    FISDF_TRY(asym_list(c->stream, wt, mesh, m, as.idx, cnt));
+    FISDF_HIP(hipMemcpyAsync(&as.n, cnt, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    FISDF_HIP(hipStreamSynchronize(c->stream));
+    if (getenv("FISDF_VERBOSE")) fprintf(stderr, "fisdf: q %d: %d of %ld G with asymmetric weight\n", q, as.n, ngrid);
+    it = c->asym_cache.emplace(key, as).first;
+  }
+  *out = &it->second;
   return 0;
 }
 
@@ -312,6 +350,7 @@ int fisdf_destroy(fisdf_ctx* c) {
   FISDF_HIP(hipStreamSynchronize(c->stream));
   for (auto& e : c->events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto& kv : c->phase_cache) (void)hipFree(kv.second);
+  for (auto& kv : c->asym_cache) (void)hipFree(kv.second.idx);
   if (c->f_pending) (void)hipEventSynchronize(c->ev_fac);
   free_factors(c);
   if (c->f_scratch) (void)hipFree(c->f_scratch);
@@ -626,11 +665,12 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
   const cplx* f = (const cplx*)fv;
   const cplx* X = (const cplx*)Xv;
   cplx* yT = (cplx*)yTv;
-  // grid sub-blocks sized so the FX temporary (nk x nip x gb) stays resident in the 256 MB
-  // Infinity Cache between the GEMM that writes it and the k-mesh DFT that reads it
+  // grid sub-blocks of ~1 GB of FX temporary (swept on MI355X at C3: 1 GB 168.6 ms/step,
+  // 256 MB 170.7, 128 MB 172.2, 64 MB 176.8 — cache-sized blocks lose more to the smaller
+  // GEMM/DFT launches than they gain from Infinity-Cache residency)
   static const long yblk_bytes = [] {
     const char* e = getenv("FISDF_YBLK_MB");
-    return (e ? atol(e) : 96L) << 20;
+    return (e ? atol(e) : 1024L) << 20;
   }();
   const long per_g = (long)nk * nip * sizeof(cplx);
   int gb = (int)std::max(64L, std::min<long>(nblk, yblk_bytes / std::max(per_g, 1L)));
@@ -669,7 +709,7 @@ int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk
 
 // ---- A4 ---------------------------------------------------------------------
 int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int nq, int nip,
-                          double tol_rel) {
+                          double tol_rel, const int* kmesh) {
   FISDF_TRY(device_guard(c));
   const int nk = nq;
   FISDF_CHECK(nk > 0 && nip > 0, "factor_x4: bad sizes");
@@ -684,7 +724,9 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   const int nb = c->f_nb;
   const int nblk = (nip + nb - 1) / nb;
   const long nn = (long)nip * nip;
-  const bool contiguous = h_qs[nq - 1] - h_qs[0] == nq - 1;
+  bool any_real = false;
+  for (int i = 0; kmesh && i < nq; ++i) any_real |= self_conjugate(kmesh, h_qs[i]);
+  const bool contiguous = h_qs[nq - 1] - h_qs[0] == nq - 1 && !any_real;
   const void* x4v = (const cplx*)x4all + (long)h_qs[0] * nn;
   FISDF_HIP(hipMalloc(&c->f_L, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_Lp, sizeof(cplx) * nk * nn));
@@ -710,12 +752,17 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   StageTimer tm(c, FISDF_ST_FACTOR, c->side);
   hipStream_t s = c->side;
   if (!contiguous) {  // gather the listed x4_q (f_Lp is overwritten by gather_lp only later)
-    for (int i = 0; i < nq; ++i)
+    for (int i = 0; i < nq; ++i) {
       FISDF_HIP(hipMemcpyAsync(c->f_Lp + i * nn, (const cplx*)x4all + (long)h_qs[i] * nn,
                                sizeof(cplx) * nn, hipMemcpyDeviceToDevice, s));
+      // self-conjugate q: x4_q = Phi[:,q]^H x4_s is real up to rounding; factor it as real
+      if (kmesh && self_conjugate(kmesh, h_qs[i])) FISDF_TRY(zero_imag(s, c->f_Lp + i * nn, nn));
+    }
     x4v = c->f_Lp;
   }
   c->f_qs.assign(h_qs, h_qs + nq);
+  c->f_real.assign(nq, 0);
+  for (int i = 0; kmesh && i < nq; ++i) c->f_real[i] = self_conjugate(kmesh, h_qs[i]) ? 1 : 0;
   c->f_nk = nk;
   c->f_nip = nip;
   FISDF_TRY(pchol(s, (const cplx*)x4v, nip, nn, nip, nk, nip, tol_rel, 0.0, c->f_L, c->f_piv,
@@ -745,8 +792,8 @@ int fisdf_factor_x4_wait(fisdf_ctx* c, int* h_ranks) {
 }
 
 int fisdf_factor_x4_qs(fisdf_ctx* c, const void* x4all, const int* h_qs, int nq, int nip,
-                       double tol_rel, int* h_ranks) {
-  FISDF_TRY(fisdf_factor_x4_async(c, x4all, h_qs, nq, nip, tol_rel));
+                       double tol_rel, const int* kmesh, int* h_ranks) {
+  FISDF_TRY(fisdf_factor_x4_async(c, x4all, h_qs, nq, nip, tol_rel, kmesh));
   return fisdf_factor_x4_wait(c, h_ranks);
 }
 
@@ -754,7 +801,7 @@ int fisdf_factor_x4(fisdf_ctx* c, const void* x4v, int q0, int q1, int nip, doub
                     int* h_ranks) {
   FISDF_CHECK(q0 >= 0 && q1 > q0, "factor_x4: bad sizes");
   std::vector<int> qs = q_range(q0, q1);
-  return fisdf_factor_x4_qs(c, x4v, qs.data(), (int)qs.size(), nip, tol_rel, h_ranks);
+  return fisdf_factor_x4_qs(c, x4v, qs.data(), (int)qs.size(), nip, tol_rel, nullptr, h_ranks);
 }
 
 // ---- A4 + A5 ------------------------------------------------------------------
@@ -810,6 +857,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     if (r == 0) continue;
     const int* piv = c->f_piv + (long)lq * nip;
     const cplx* Lp = c->f_Lp + (long)lq * nn;
+    const bool real_q = c->f_real[lq];
     const cplx* Linv = c->f_Linv + (long)lq * sLi;
     double kq[3], kd[3];
     kpoint(kmesh, g, q, kq);
@@ -826,12 +874,24 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       StageTimer tm(c, FISDF_ST_TRSM);
       // U = L^{-1} Yh   (fit, factored order; (x4_q)_PP = L L^H)
       FISDF_TRY(trsm_blocked(c->stream, 1, Lp, nip, 0, r, Linv, 0, nb, Yh, ngrid, 0, U, ngrid, 0,
-                             (int)ngrid, 1));
+                             (int)ngrid, 1, real_q ? 1 : 0));
     }
     {
       StageTimer tm(c, FISDF_ST_HERK);
       // G = U U^H  (:121 by Parseval)
-      FISDF_TRY(herk(c->stream, r, (int)ngrid, 1.0, U, ngrid, G + lq * rr, rmax, ks, kw));
+      FISDF_TRY(herk(c->stream, r, (int)ngrid, 1.0, U, ngrid, G + lq * rr, rmax, ks, kw,
+                     real_q ? GEMM_RE_ONLY : GEMM_FULL));
+      if (real_q) {
+        // Im(G) = Im(sum over the weight-asymmetric G only): every other (G, G') pair cancels
+        const fisdf_ctx::Asym* as = nullptr;
+        FISDF_TRY(get_asym(c, mesh, kmesh, a, q, wt, &as));
+        if (as->n > 0) {
+          FISDF_TRY(gather_cols(c->stream, U, ngrid, r, as->idx, as->n, Yh));  // Yh is free
+          FISDF_TRY(herk(c->stream, r, as->n, 1.0, Yh, as->n, T, rmax,
+                         std::min(ks, std::max(1, as->n / 256)), kw));
+          FISDF_TRY(add_imag(c->stream, G + lq * rr, rmax, T, rmax, r));
+        }
+      }
     }
   }
   {

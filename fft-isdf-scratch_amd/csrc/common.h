@@ -54,14 +54,18 @@ enum Op { OP_N = 0, OP_T = 1, OP_R = 2 /*conj only*/, OP_C = 3 /*conj-transpose*
 // strides sA/sB/sC per batch in complex elements. ksplit>1 uses `work` (ksplit*M*N cplx).
 // epilogues: EPI_SQUARE_RE writes Re(alpha*acc)^2 + 0i and records max|Im| into *mon
 enum Epi { EPI_NONE = 0, EPI_SQUARE_RE = 1 };
+// arithmetic modes (MFMA work skipped): GEMM_A_REAL: Im(op(A)) is taken as zero (2 of the 4
+// real MFMAs per complex block); GEMM_RE_ONLY: only Re(C) is formed (Im(C) written as 0).
+// Supported for (N,N), (C,N) and the HERK; other op pairs require mode 0.
+enum GemmMode { GEMM_FULL = 0, GEMM_A_REAL = 1, GEMM_RE_ONLY = 2 };
 int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha,
           const cplx* A, long lda, long sA, const cplx* B, long ldb, long sB, cplx beta,
           cplx* C, long ldc, long sC, int batch, int ksplit = 1, cplx* work = nullptr,
-          int epi = EPI_NONE, unsigned long long* mon = nullptr);
+          int epi = EPI_NONE, unsigned long long* mon = nullptr, int mode = GEMM_FULL);
 
 // C = alpha A A^H (Hermitian rank-K update; lower tiles computed, upper mirrored)
 int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cplx* C, long ldc,
-         int ksplit = 1, cplx* work = nullptr);
+         int ksplit = 1, cplx* work = nullptr, int mode = GEMM_FULL);
 
 // batched pivoted Cholesky of Hermitian PSD matrices (fftisdf.py:381-382, A4 factorisation)
 int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int rmax,

@@ -14,7 +14,14 @@ int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int ldl, long sL, int nb,
                  cplx* Linv, int batch);
 int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, long ldl, long sL, int r,
                  const cplx* Linv, long sLi, int nb, cplx* B, long ldb, long sB, cplx* X, long ldx,
-                 long sX, int ncol, int batch);
+                 long sX, int ncol, int batch, int a_real = 0);
+// G indices whose Coulomb weight differs from that of G' = -G - m.b (ascending) -> idx, *count
+int asym_list(hipStream_t s, const double* w, const int mesh[3], const int m[3], int* idx,
+              int* count);
+int gather_cols(hipStream_t s, const cplx* A, long ld, int r, const int* idx, int n, cplx* out);
+int add_imag(hipStream_t s, cplx* G, int ldg, const cplx* H, int ldh, int n);
+// zero the imaginary parts of n complex elements
+int zero_imag(hipStream_t s, cplx* a, long n);
 int scatter_w(hipStream_t s, const cplx* Wpp, int ldw, long sW, int rmax, const int* piv,
               const int* rank, cplx* W, int nip, int batch);
 int conj_transpose(hipStream_t s, const cplx* A, int n, long sA, cplx* B, int batch);

@@ -499,8 +499,10 @@ int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int ldl, long sL, int nb,
 // ZGEMM with the block inverse per 64-row block (factored order, never an explicit inverse).
 int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, long ldl, long sL, int r,
                  const cplx* Linv, long sLi, int nb, cplx* B, long ldb, long sB, cplx* X, long ldx,
-                 long sX, int ncol, int batch) {
+                 long sX, int ncol, int batch, int a_real) {
   const cplx one = cmk(1, 0), mone = cmk(-1, 0), zero = cmk(0, 0);
+  // a_real: L (and hence its diagonal-block inverses) is real -> half the MFMA work
+  const int md = a_real ? GEMM_A_REAL : GEMM_FULL;
   int nblk = (r + nb - 1) / nb;
   for (int bi = 0; bi < nblk; ++bi) {
     int blk = lower ? bi : nblk - 1 - bi;
@@ -508,17 +510,122 @@ int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, long ldl, long sL, in
     if (lower) {
       if (b0 > 0)  // B_b -= L[b, :b] X[:b]
         FISDF_TRY(zgemm(s, OP_N, OP_N, m, ncol, b0, mone, Lp + (long)b0 * ldl, ldl, sL, X, ldx,
-                        sX, one, B + (long)b0 * ldb, ldb, sB, batch));
+                        sX, one, B + (long)b0 * ldb, ldb, sB, batch, 1, nullptr, EPI_NONE, nullptr,
+                        md));
       FISDF_TRY(zgemm(s, OP_N, OP_N, m, ncol, m, one, Linv + (long)blk * nb * nb, nb, sLi,
-                      B + (long)b0 * ldb, ldb, sB, zero, X + (long)b0 * ldx, ldx, sX, batch));
+                      B + (long)b0 * ldb, ldb, sB, zero, X + (long)b0 * ldx, ldx, sX, batch, 1,
+                      nullptr, EPI_NONE, nullptr, md));
     } else {
       if (b1 < r)  // B_b -= (L^H)[b, >b] X[>b] = conj(L[>b, b])^T X[>b]
         FISDF_TRY(zgemm(s, OP_C, OP_N, m, ncol, r - b1, mone, Lp + (long)b1 * ldl + b0, ldl, sL,
-                        X + (long)b1 * ldx, ldx, sX, one, B + (long)b0 * ldb, ldb, sB, batch));
+                        X + (long)b1 * ldx, ldx, sX, one, B + (long)b0 * ldb, ldb, sB, batch, 1,
+                        nullptr, EPI_NONE, nullptr, md));
       FISDF_TRY(zgemm(s, OP_C, OP_N, m, ncol, m, one, Linv + (long)blk * nb * nb, nb, sLi,
-                      B + (long)b0 * ldb, ldb, sB, zero, X + (long)b0 * ldx, ldx, sX, batch));
+                      B + (long)b0 * ldb, ldb, sB, zero, X + (long)b0 * ldx, ldx, sX, batch, 1,
+                      nullptr, EPI_NONE, nullptr, md));
     }
   }
+  return 0;
+}
+
+// Coulomb-weight asymmetry of a self-conjugate q (2 k_q = m . b): for real z_q,
+// Zhat(G') = conj(Zhat(G)) with G' = -G - 2 k_q, so W_q = sum_G c_G Zhat_G Zhat_G^H is real
+// except where c(k+G) != c(k+G') — the Nyquist planes of even meshes (fftfreq puts -N/2 in
+// both members of a pair) and the box-edge wrap of get_coulG.  One workgroup lists those G
+// (ascending, deterministic) so Im(W_q) can be formed from them alone.
+__global__ __launch_bounds__(1024) void asym_list_kernel(const double* __restrict__ w, int n0,
+                                                         int n1, int n2, int m0, int m1, int m2,
+                                                         int* __restrict__ idx,
+                                                         int* __restrict__ count) {
+  __shared__ int base;
+  __shared__ int warp_tot[16];
+  const long ngrid = (long)n0 * n1 * n2;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (long e0 = 0; e0 < ngrid; e0 += blockDim.x) {
+    const long e = e0 + threadIdx.x;
+    bool flag = false;
+    if (e < ngrid) {
+      const int i2 = (int)(e % n2), i1 = (int)((e / n2) % n1), i0 = (int)(e / ((long)n1 * n2));
+      const int p0 = ((-i0 - m0) % n0 + n0) % n0, p1 = ((-i1 - m1) % n1 + n1) % n1,
+                p2 = ((-i2 - m2) % n2 + n2) % n2;
+      const long pe = ((long)p0 * n1 + p1) * n2 + p2;
+      // pairs whose weights differ only by rounding (|k+G| and |k+G'| evaluated from
+      // different index vectors) contribute rounding-level Im parts: not listed
+      flag = fabs(w[e] - w[pe]) > 1e-13 * fmax(fabs(w[e]), fabs(w[pe]));
+    }
+    const unsigned long long bal = __ballot(flag);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) warp_tot[wv] = __popcll(bal);
+    __syncthreads();
+    int off = base;
+    for (int j = 0; j < wv; ++j) off += warp_tot[j];
+    if (flag) idx[off + before] = (int)e;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int j = 0; j < (int)(blockDim.x >> 6); ++j) t += warp_tot[j];
+      base += t;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *count = base;
+}
+
+// out[i][j] = A[i][idx[j]]  (r rows of ld, n listed columns)
+__global__ void gather_cols_kernel(const cplx* __restrict__ A, long ld, int r,
+                                   const int* __restrict__ idx, int n, cplx* __restrict__ out) {
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= (long)r * n) return;
+  const int i = (int)(e / n), j = (int)(e % n);
+  out[e] = A[(long)i * ld + idx[j]];
+}
+
+// G.y += H.y (n x n, leading dims ldg / ldh)
+__global__ void add_imag_kernel(cplx* __restrict__ G, int ldg, const cplx* __restrict__ H, int ldh,
+                                int n) {
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= (long)n * n) return;
+  const int i = (int)(e / n), j = (int)(e % n);
+  G[(long)i * ldg + j].y += H[(long)i * ldh + j].y;
+}
+
+__global__ void zero_imag_kernel(cplx* __restrict__ a, long n) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x)
+    a[e].y = 0.0;
+}
+
+int asym_list(hipStream_t s, const double* w, const int mesh[3], const int m[3], int* idx,
+              int* count) {
+  hipLaunchKernelGGL(asym_list_kernel, dim3(1), dim3(1024), 0, s, w, mesh[0], mesh[1], mesh[2],
+                     m[0], m[1], m[2], idx, count);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int gather_cols(hipStream_t s, const cplx* A, long ld, int r, const int* idx, int n, cplx* out) {
+  const long e = (long)r * n;
+  if (e == 0) return 0;
+  hipLaunchKernelGGL(gather_cols_kernel, dim3(nblocks(e, 256, 1L << 30)), dim3(256), 0, s, A, ld,
+                     r, idx, n, out);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int add_imag(hipStream_t s, cplx* G, int ldg, const cplx* H, int ldh, int n) {
+  const long e = (long)n * n;
+  if (e == 0) return 0;
+  hipLaunchKernelGGL(add_imag_kernel, dim3(nblocks(e, 256, 1L << 30)), dim3(256), 0, s, G, ldg, H,
+                     ldh, n);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int zero_imag(hipStream_t s, cplx* a, long n) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(zero_imag_kernel, dim3(nblocks(n, 256, 8192)), dim3(256), 0, s, a, n);
+  FISDF_HIP(hipGetLastError());
   return 0;
 }
 

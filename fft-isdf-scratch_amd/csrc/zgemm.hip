@@ -297,7 +297,7 @@ constexpr int NST = 3;
 constexpr int LPW = TILE / (64 * 4);  // glds wave-instructions per operand per step per wave
 __device__ cplx g_zero_page[64];      // zero-initialised device global
 
-template <int OPA, int OPB, bool HERK>
+template <int OPA, int OPB, bool HERK, int MODE>
 __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cplx alpha,
                                                          const cplx* __restrict__ A, long lda, long sA,
                                                          const cplx* __restrict__ B, long ldb, long sB,
@@ -439,30 +439,37 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
           br[u] = b[u].x;
           bi[u] = CB ? -b[u].y : b[u].y;
         }
+        constexpr bool AREAL = (MODE & GEMM_A_REAL) != 0, REONLY = (MODE & GEMM_RE_ONLY) != 0;
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
           for (int ni = 0; ni < 2; ++ni)
             if ((MASK >> (mi * 2 + ni)) & 1)
               accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], accR[mi][ni], 0, 0, 0);
+        if constexpr (!REONLY) {
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
+          for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
-            if ((MASK >> (mi * 2 + ni)) & 1)
-              accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], bi[ni], accI[mi][ni], 0, 0, 0);
+            for (int ni = 0; ni < 2; ++ni)
+              if ((MASK >> (mi * 2 + ni)) & 1)
+                accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], bi[ni], accI[mi][ni], 0, 0, 0);
+        }
+        if constexpr (!AREAL) {
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
+          for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
-            if ((MASK >> (mi * 2 + ni)) & 1)
-              accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[mi], bi[ni], accR[mi][ni], 0, 0, 0);
+            for (int ni = 0; ni < 2; ++ni)
+              if ((MASK >> (mi * 2 + ni)) & 1)
+                accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[mi], bi[ni], accR[mi][ni], 0, 0, 0);
+        }
+        if constexpr (!AREAL && !REONLY) {
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
+          for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
-            if ((MASK >> (mi * 2 + ni)) & 1)
-              accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], br[ni], accI[mi][ni], 0, 0, 0);
+            for (int ni = 0; ni < 2; ++ni)
+              if ((MASK >> (mi * 2 + ni)) & 1)
+                accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], br[ni], accI[mi][ni], 0, 0, 0);
+        }
       }
     }
   };
@@ -506,7 +513,7 @@ int gemm_variant() {
   return v;
 }
 
-template <int OPA, int OPB, bool HERK = false>
+template <int OPA, int OPB, bool HERK = false, int MODE = GEMM_FULL>
 void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cplx* A, long lda,
             long sA, const cplx* B, long ldb, long sB, cplx beta, cplx* C, long ldc, long sC,
             int ksplit, int kchunk, cplx* work, int epi, unsigned long long* mon) {
@@ -515,8 +522,8 @@ void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cpl
   const int ntile = (int)(grid.x * (HERK ? 1 : grid.y));
   const long ntot = (long)ntile * grid.z;
   const long per = (ntot + 7) / 8;
-  if (gemm_variant() == 1)
-    hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK>), dim3((unsigned)(8 * per)), dim3(256), 0,
+  if (gemm_variant() == 1 || MODE != GEMM_FULL)
+    hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE>), dim3((unsigned)(8 * per)), dim3(256), 0,
                        s, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk,
                        work, epi, mon, nMt, ntile, (int)ntot);
   else
@@ -529,9 +536,12 @@ void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cpl
 
 int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, const cplx* A,
           long lda, long sA, const cplx* B, long ldb, long sB, cplx beta, cplx* C, long ldc,
-          long sC, int batch, int ksplit, cplx* work, int epi, unsigned long long* mon) {
+          long sC, int batch, int ksplit, cplx* work, int epi, unsigned long long* mon, int mode) {
   FISDF_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 0, "zgemm: negative size");
   FISDF_CHECK(opA >= 0 && opA < 4 && opB >= 0 && opB < 4, "zgemm: bad op");
+  FISDF_CHECK(mode >= 0 && mode <= 3, "zgemm: bad mode");
+  FISDF_CHECK(mode == GEMM_FULL || (opB == OP_N && (opA == OP_N || opA == OP_C)),
+              "zgemm: real modes are implemented for (N,N) and (C,N) only");
   if (M == 0 || N == 0 || batch == 0) return 0;
   if (ksplit < 1) ksplit = 1;
   if (epi != EPI_NONE) ksplit = 1;
@@ -548,7 +558,15 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
     launch<a, b>(s, grid, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit,   \
                  kchunk, work, epi, mon);                                                     \
     break;
-  switch (opA * 4 + opB) {
+#define FISDF_MCASE(a, b, m)                                                                  \
+  if (opA == a && opB == b && mode == m) {                                                    \
+    launch<a, b, false, m>(s, grid, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, \
+                           ksplit, kchunk, work, epi, mon);                                   \
+  }
+  FISDF_MCASE(0, 0, 1) FISDF_MCASE(0, 0, 2) FISDF_MCASE(0, 0, 3)
+  FISDF_MCASE(3, 0, 1) FISDF_MCASE(3, 0, 2) FISDF_MCASE(3, 0, 3)
+#undef FISDF_MCASE
+  if (mode == GEMM_FULL) switch (opA * 4 + opB) {
     FISDF_CASE(0, 0) FISDF_CASE(0, 1) FISDF_CASE(0, 2) FISDF_CASE(0, 3)
     FISDF_CASE(1, 0) FISDF_CASE(1, 1) FISDF_CASE(1, 2) FISDF_CASE(1, 3)
     FISDF_CASE(2, 0) FISDF_CASE(2, 1) FISDF_CASE(2, 2) FISDF_CASE(2, 3)
@@ -568,7 +586,8 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
 
 // C = alpha A A^H, A: n x K (row-major, lda), C: n x n (ldc) Hermitian, lower tiles + mirror.
 int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cplx* C, long ldc,
-         int ksplit, cplx* work) {
+         int ksplit, cplx* work, int mode) {
+  FISDF_CHECK(mode == GEMM_FULL || mode == GEMM_RE_ONLY, "herk: mode must be FULL or RE_ONLY");
   FISDF_CHECK(n >= 0 && K >= 0, "herk: negative size");
   if (n == 0) return 0;
   if (ksplit < 1) ksplit = 1;
@@ -578,8 +597,13 @@ int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cpl
   ksplit = std::max(1, (K + kchunk - 1) / kchunk);
   const int nt = (n + BM - 1) / BM;
   dim3 grid(nt * (nt + 1) / 2, 1, ksplit);
-  launch<OP_N, OP_C, true>(s, grid, n, n, K, cmk(alpha, 0), A, lda, 0, A, lda, 0, cmk(0, 0), C,
-                           ldc, 0, ksplit, kchunk, work, EPI_NONE, nullptr);
+  if (mode == GEMM_RE_ONLY)  // C = Re(A A^H): 2 of the 4 MFMAs per complex block
+    launch<OP_N, OP_C, true, GEMM_RE_ONLY>(s, grid, n, n, K, cmk(alpha, 0), A, lda, 0, A, lda, 0,
+                                           cmk(0, 0), C, ldc, 0, ksplit, kchunk, work, EPI_NONE,
+                                           nullptr);
+  else
+    launch<OP_N, OP_C, true>(s, grid, n, n, K, cmk(alpha, 0), A, lda, 0, A, lda, 0, cmk(0, 0), C,
+                             ldc, 0, ksplit, kchunk, work, EPI_NONE, nullptr);
   FISDF_HIP(hipGetLastError());
   if (ksplit > 1) {
     long MN = (long)n * n;

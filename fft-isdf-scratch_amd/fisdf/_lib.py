@@ -49,8 +49,8 @@ _SIGS = {
     "fisdf_fit_coulomb": ([_vp, _i, _i, _vp, _i, _ip, _ip, _dp, _vp], _i),
     "fisdf_build_ws": ([_vp, _vp, _i, _i, _i, _ip, _dp, _vp], _i),
     "fisdf_build_y_qs": ([_vp, _vp, _l, _i, _i, _i, _vp, _i, _i, _ip, _dp, _ip, _i, _vp], _i),
-    "fisdf_factor_x4_qs": ([_vp, _vp, _ip, _i, _i, _d, _ip], _i),
-    "fisdf_factor_x4_async": ([_vp, _vp, _ip, _i, _i, _d], _i),
+    "fisdf_factor_x4_qs": ([_vp, _vp, _ip, _i, _i, _d, _ip, _ip], _i),
+    "fisdf_factor_x4_async": ([_vp, _vp, _ip, _i, _i, _d, _ip], _i),
     "fisdf_factor_x4_wait": ([_vp, _ip], _i),
     "fisdf_fit_coulomb_qs": ([_vp, _ip, _i, _vp, _i, _ip, _ip, _dp, _vp], _i),
     "fisdf_build_ws_qs": ([_vp, _vp, _ip, _dp, _i, _i, _ip, _dp, _vp], _i),

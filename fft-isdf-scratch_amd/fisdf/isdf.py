@@ -100,6 +100,9 @@ class InterpolativeSeparableDensityFitting:
     select_tol = -1.0       # dpstrf default tolerance (ng0*eps*max diag)
     # fit one q of each (q, -q) pair and take W_{-q} = conj(W_q) (y_s, x4_s real: :43,:81)
     time_reversal = True
+    # q with 2 k_q in the reciprocal lattice (Gamma, all q of a 2x2x2 mesh): real x4_q and
+    # W_q, fitted with real-factor / real-part GEMMs (half the MFMA work)
+    real_self_conjugate = True
 
     def __init__(self, cell, kpts, m0=None, c0=20.0, device=None, comm=None):
         self.cell = cell
@@ -389,7 +392,8 @@ def build(df_obj):
     # x4_q factorisation (replaces zgelsy's QRCP, :108) on the library's side stream,
     # overlapped with the y build enqueued next on the main stream
     if nq:
-        d.ctx.call("fisdf_factor_x4_async", _lib.ptr(x4), qs_c, nq, nip, float(df_obj.fit_tol))
+        d.ctx.call("fisdf_factor_x4_async", _lib.ptr(x4), qs_c, nq, nip, float(df_obj.fit_tol),
+                   km_p if df_obj.real_self_conjugate else None)
     yT = d.empty((nq, nip, ngrid))
     if d.size == 1:
         d.ctx.call("fisdf_build_y_qs", _lib.ptr(f), ngrid * nao, 0, ngrid, ngrid, _lib.ptr(X),

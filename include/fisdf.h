@@ -116,15 +116,18 @@ int fisdf_build_y_qs(fisdf_ctx* ctx, const void* d_f, long f_kstride, int g0, in
  * the numerical ranks (logged at fftisdf.py:122). */
 int fisdf_factor_x4(fisdf_ctx* ctx, const void* d_x4, int q0, int q1, int nip, double tol_rel,
                     int* h_ranks);
-/* q-list form: factors x4_q for q = h_qs[i] (ascending); h_ranks (nq). */
+/* q-list form: factors x4_q for q = h_qs[i] (ascending); h_ranks (nq).  kmesh (may be NULL):
+ * q that are their own time-reversal partner (2 k_q a reciprocal-lattice vector) have real
+ * x4_q, y_q, z_q and W_q; with kmesh given they are factored as real and fitted with real-
+ * factor / real-part GEMMs (half the MFMA work). */
 int fisdf_factor_x4_qs(fisdf_ctx* ctx, const void* d_x4, const int* h_qs, int nq, int nip,
-                       double tol_rel, int* h_ranks);
+                       double tol_rel, const int* kmesh, int* h_ranks);
 /* Asynchronous form: enqueues the factorisation on the context's side stream (after the work
  * already enqueued on the main stream, i.e. x4) and returns at once, so the y build enqueued
  * next overlaps it.  fisdf_factor_x4_wait (synchronous on the side stream) returns the ranks;
  * fisdf_fit_coulomb_qs waits by itself. */
 int fisdf_factor_x4_async(fisdf_ctx* ctx, const void* d_x4, const int* h_qs, int nq, int nip,
-                          double tol_rel);
+                          double tol_rel, const int* kmesh);
 int fisdf_factor_x4_wait(fisdf_ctx* ctx, int* h_ranks /* nq, may be NULL */);
 
 /* ---- A4+A5: fit + FFT Coulomb for the factored shard q in [q0, q1) (fftisdf.py:97-121)

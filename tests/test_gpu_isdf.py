@@ -20,13 +20,14 @@ JK_TOL = 1e-8   # Ha, north_star
 JK_TOL_RANK_DEFICIENT_TR = 1.5e-8
 
 
-def make_df(name, inject=True, time_reversal=True):
+def make_df(name, inject=True, time_reversal=True, real_sc=True):
     from fisdf import ISDF
     cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
     o = oracle(name)
     kpts = cell.get_kpts(kmesh)
     df = ISDF(cell, kpts, m0=list(m0), c0=c0)
     df.time_reversal = time_reversal
+    df.real_self_conjugate = real_sc
     d = df.device
     df._kmesh()
     df._ao_parent = d.to_dev(x0)
@@ -76,6 +77,28 @@ def test_jk_parity_without_time_reversal(name):
         res[tr] = (vj, vk)
     d = max(abs(res[True][0] - res[False][0]).max(), abs(res[True][1] - res[False][1]).max())
     print(f"{name}: |JK(tr) - JK(all q)| = {d:.2e}")
+    assert d < JK_TOL
+
+
+@pytest.mark.parametrize("name", ["toy222", "toy331_fr", "diamond_szv_gamma", "si_small"])
+def test_real_self_conjugate_path(name):
+    """q with 2 k_q in the reciprocal lattice (all q of 2x2x2, Gamma) are fitted with a real
+    factor (half-MFMA TRSM) and a real-part HERK; J/K agree with the all-complex fit."""
+    res = {}
+    for real_sc in (False, True):
+        df, o, dm = make_df(name, real_sc=real_sc)
+        df.build()
+        vj, vk = df.get_jk(dm)
+        full_rank = min(df.ranks) == df.nip
+        tol = JK_TOL if full_rank or len(df.fit_qs) == int(np.prod(df.kmesh)) \
+            else JK_TOL_RANK_DEFICIENT_TR
+        ej, ek = abs(vj - o["vj"]).max(), abs(vk - o["vk"]).max()
+        print(f"{name} real_sc={real_sc}: |dJ|={ej:.2e} |dK|={ek:.2e}")
+        assert ej < tol and ek < tol
+        res[real_sc] = (vj, vk, df._wq)
+    dw = abs(res[True][2] - res[False][2]).max() / abs(res[False][2]).max()
+    d = max(abs(res[True][0] - res[False][0]).max(), abs(res[True][1] - res[False][1]).max())
+    print(f"{name}: |JK(real) - JK(complex)| = {d:.2e}, rel |dW| = {dw:.2e}")
     assert d < JK_TOL
 
 
