@@ -41,6 +41,7 @@ struct fisdf_ctx {
   cplx* f_L = nullptr;      // (nk, nip, nip) raw left-looking factor (row order)
   cplx* f_Lp = nullptr;     // (nk, nip*nip) pivot-order factor, ld = rank_q
   cplx* f_Linv = nullptr;   // (nk, nblk*nb*nb)
+  cplx* f_Q = nullptr;      // (nk, nip, nip) block-row operator of trsm_merged (build_trsm_q)
   int* f_piv = nullptr;     // (nk, nip)
   int* f_rank_dev = nullptr;
   std::vector<int> f_rank;  // host copy
@@ -203,6 +204,8 @@ int free_factors(fisdf_ctx* c) {
   if (c->f_L) FISDF_HIP(hipFree(c->f_L));
   if (c->f_Lp) FISDF_HIP(hipFree(c->f_Lp));
   if (c->f_Linv) FISDF_HIP(hipFree(c->f_Linv));
+  if (c->f_Q) FISDF_HIP(hipFree(c->f_Q));
+  c->f_Q = nullptr;
   if (c->f_piv) FISDF_HIP(hipFree(c->f_piv));
   if (c->f_rank_dev) FISDF_HIP(hipFree(c->f_rank_dev));
   if (c->f_rank_pinned) FISDF_HIP(hipHostFree(c->f_rank_pinned));
@@ -773,6 +776,9 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   // back-substitutions of all q can run as one batch
   FISDF_TRY(gather_lp(s, c->f_L, nip, nip, c->f_piv, c->f_rank_dev, nip, c->f_Lp, nk));
   FISDF_TRY(trinv_blocks(s, c->f_Lp, nip, nip, nn, nb, (long)nblk * nb * nb, c->f_Linv, nk));
+  // merged forward-substitution operator (used for the q whose rank is nip)
+  FISDF_HIP(hipMalloc(&c->f_Q, sizeof(cplx) * nk * nn));
+  FISDF_TRY(build_trsm_q(s, c->f_Lp, nip, nn, c->f_Q, nk, GEMM_FULL));
   FISDF_HIP(hipEventRecord(c->ev_fac, s));
   c->f_pending = true;
   return 0;
@@ -870,24 +876,32 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       FISDF_TRY(fft3d(c->stream, yT + (long)lq * nip * ngrid, ngrid, piv, Yh, ngrid, r, mesh[0],
                       mesh[1], mesh[2], kd, wt, nullptr));
     }
+    cplx* Uq = U;  // where L^{-1} Yh lands
     {
       StageTimer tm(c, FISDF_ST_TRSM);
       // U = L^{-1} Yh   (fit, factored order; (x4_q)_PP = L L^H)
-      FISDF_TRY(trsm_blocked(c->stream, 1, Lp, nip, 0, r, Linv, 0, nb, Yh, ngrid, 0, U, ngrid, 0,
-                             (int)ngrid, 1, real_q ? 1 : 0));
+      if (r == nip) {  // merged block-row substitution, in place
+        FISDF_TRY(trsm_merged(c->stream, c->f_Q + (long)lq * nn, nip, Yh, ngrid, (int)ngrid,
+                              real_q ? GEMM_A_REAL : GEMM_FULL));
+        Uq = Yh;
+      } else {
+        FISDF_TRY(trsm_blocked(c->stream, 1, Lp, nip, 0, r, Linv, 0, nb, Yh, ngrid, 0, U, ngrid,
+                               0, (int)ngrid, 1, real_q ? 1 : 0));
+      }
     }
+    cplx* scratch = Uq == U ? Yh : U;
     {
       StageTimer tm(c, FISDF_ST_HERK);
       // G = U U^H  (:121 by Parseval)
-      FISDF_TRY(herk(c->stream, r, (int)ngrid, 1.0, U, ngrid, G + lq * rr, rmax, ks, kw,
+      FISDF_TRY(herk(c->stream, r, (int)ngrid, 1.0, Uq, ngrid, G + lq * rr, rmax, ks, kw,
                      real_q ? GEMM_RE_ONLY : GEMM_FULL));
       if (real_q) {
         // Im(G) = Im(sum over the weight-asymmetric G only): every other (G, G') pair cancels
         const fisdf_ctx::Asym* as = nullptr;
         FISDF_TRY(get_asym(c, mesh, kmesh, a, q, wt, &as));
         if (as->n > 0) {
-          FISDF_TRY(gather_cols(c->stream, U, ngrid, r, as->idx, as->n, Yh));  // Yh is free
-          FISDF_TRY(herk(c->stream, r, as->n, 1.0, Yh, as->n, T, rmax,
+          FISDF_TRY(gather_cols(c->stream, Uq, ngrid, r, as->idx, as->n, scratch));
+          FISDF_TRY(herk(c->stream, r, as->n, 1.0, scratch, as->n, T, rmax,
                          std::min(ks, std::max(1, as->n / 256)), kw));
           FISDF_TRY(add_imag(c->stream, G + lq * rr, rmax, T, rmax, r));
         }

@@ -63,6 +63,37 @@ __global__ __launch_bounds__(64) void trinv_blocks_kernel(const cplx* __restrict
     if (j < nb) out[i * nb + j] = (i < m && j < m) ? Xs[i][j] : cmk(i == j ? 1.0 : 0.0, 0.0);
 }
 
+// Same inverses for the partition [0, s0), [s0, s0+64), ... written straight into the
+// diagonal blocks of Q (ld = ldq) — the block-row operator of trsm_merged.
+__global__ __launch_bounds__(64) void trinv_into_kernel(const cplx* __restrict__ Lp, int r,
+                                                        int ldl, long sL, int s0,
+                                                        cplx* __restrict__ Q, int ldq, long sQ) {
+  __shared__ cplx Ls[64][65];
+  __shared__ cplx Xs[64][65];
+  Lp += blockIdx.y * sL;
+  Q += blockIdx.y * sQ;
+  const int blk = blockIdx.x;
+  const int b0 = blk == 0 ? 0 : s0 + (blk - 1) * 64;
+  const int m = blk == 0 ? s0 : min(64, r - b0);
+  const int j = threadIdx.x;
+  for (int i = 0; i < m; ++i)
+    if (j < m) Ls[i][j] = Lp[(long)(b0 + i) * ldl + b0 + j];
+  __syncthreads();
+  if (j < m) {
+    for (int i = 0; i < m; ++i) {
+      cplx sacc = cmk(i == j ? 1.0 : 0.0, 0.0);
+      for (int t = j; t < i; ++t) sacc = csub(sacc, cmul(Ls[i][t], Xs[t][j]));
+      cplx d = Ls[i][i];
+      double den = d.x * d.x + d.y * d.y;
+      Xs[i][j] = i < j ? cmk(0, 0)
+                       : cmk((sacc.x * d.x + sacc.y * d.y) / den, (sacc.y * d.x - sacc.x * d.y) / den);
+    }
+  }
+  __syncthreads();
+  for (int i = 0; i < m; ++i)
+    if (j < m) Q[(long)(b0 + i) * ldq + b0 + j] = Xs[i][j];
+}
+
 // W[b][piv[b][s]][piv[b][t]] = Wpp[b][s][t] for s,t < rank[b]   (W zeroed beforehand)
 __global__ void scatter_w_kernel(const cplx* __restrict__ Wpp, int ldw, long sW,
                                  const int* __restrict__ piv, const int* __restrict__ rank,
@@ -479,6 +510,44 @@ int gather_lp(hipStream_t s, const cplx* L, int n, int rmax, const int* piv, con
   hipLaunchKernelGGL(gather_lp_kernel, dim3(nblocks(e, 256, 1L << 30), batch), dim3(256), 0, s, L,
                      n, rmax, piv, rank, rpad, Lp);
   FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+// Q (r x r, ld = r per batch entry): block rows of the merged forward substitution,
+//   Q[b, b] = L_bb^{-1},  Q[b, :b0] = -L_bb^{-1} L[b, :b0]
+// over the partition [0, s0), [s0, s0+64), ..., s0 = r - 64 (nblk - 1) (the partial block
+// first, so every large-K step of trsm_merged has a full 64-row tile).
+int build_trsm_q(hipStream_t s, const cplx* Lp, int r, long sL, cplx* Q, int batch, int mode) {
+  const int nblk = (r + 63) / 64;
+  if (nblk == 0 || batch == 0) return 0;
+  const int s0 = r - 64 * (nblk - 1);
+  const long rr = (long)r * r;
+  hipLaunchKernelGGL(trinv_into_kernel, dim3(nblk, batch), dim3(64), 0, s, Lp, r, r, sL, s0, Q, r,
+                     rr);
+  FISDF_HIP(hipGetLastError());
+  const cplx mone = cmk(-1, 0), zero = cmk(0, 0);
+  for (int b = 1; b < nblk; ++b) {
+    const int b0 = s0 + (b - 1) * 64;
+    FISDF_TRY(zgemm(s, OP_N, OP_N, 64, b0, 64, mone, Q + (long)b0 * r + b0, r, rr,
+                    Lp + (long)b0 * r, r, sL, zero, Q + (long)b0 * r, r, rr, batch, 1, nullptr,
+                    EPI_NONE, nullptr, mode));
+  }
+  return 0;
+}
+
+// X = L^{-1} X in place for X (r x ncol, ld): one GEMM per block row with the Q of
+// build_trsm_q, X[b] = Q[b, :b1] X[:b1] — each workgroup owns whole columns (M <= 64), so
+// it reads all of X[:b1] for its columns before its epilogue overwrites X[b].
+int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol, int mode) {
+  const int nblk = (r + 63) / 64;
+  if (nblk == 0) return 0;
+  const int s0 = r - 64 * (nblk - 1);
+  const cplx one = cmk(1, 0), zero = cmk(0, 0);
+  for (int b = 0; b < nblk; ++b) {
+    const int b0 = b == 0 ? 0 : s0 + (b - 1) * 64, m = b == 0 ? s0 : 64, b1 = b0 + m;
+    FISDF_TRY(zgemm(s, OP_N, OP_N, m, ncol, b1, one, Q + (long)b0 * r, r, 0, X, ld, 0, zero,
+                    X + (long)b0 * ld, ld, 0, 1, 1, nullptr, EPI_NONE, nullptr, mode));
+  }
   return 0;
 }
 
