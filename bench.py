@@ -179,17 +179,26 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = nk / (dt / args.steps)
 
-    # roofline of the dominant kernel: the Coulomb HERK W_q = Zhat Zhat^H (one launch per q)
+    # roofline of the dominant kernel: the Coulomb HERK W_q = Zhat Zhat^H (one launch per fitted
+    # q; HIP events around each launch on the library's stream).  Algorithmic flop per launch:
+    # 4 r^2 N (complex HERK), 2 r^2 N for a self-conjugate q (real-part HERK).
     ngrid = int(np.prod(cell.mesh))
-    ranks = np.asarray(df.ranks, dtype=np.int64)
+    ranks = np.asarray(df.ranks, dtype=np.float64)
+    real = np.array([bool(df.real_self_conjugate and df.q_partner[q] == q) for q in df.my_qs])
+    flop_step = float(np.sum(np.where(real, 2.0, 4.0) * ranks ** 2) * ngrid)
     herk_ms, herk_calls = stages["herk"]
-    herk_flop = 4.0 * float(np.sum(ranks.astype(np.float64) ** 2)) * ngrid * args.steps
-    achieved = herk_flop / (herk_ms * 1e-3) / 1e12 if herk_ms > 0 else 0.0
-    roof = {"bound": "mfma", "kernel": "zgemm_kernel<0,3,true> (HERK W_q, split-K) + reduce",
+    achieved = flop_step * args.steps / (herk_ms * 1e-3) / 1e12 if herk_ms > 0 else 0.0
+    roof = {"bound": "mfma", "kernel": "zgemm_glds_kernel<0,3,true,*> (HERK W_q, split-K) + reduce",
             "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP64_TFLOPS, 4), "traffic": None,
-            "flop_per_launch": 4.0 * float(np.mean(ranks.astype(np.float64) ** 2)) * ngrid,
-            "avg_launch_ms": herk_ms / max(herk_calls, 1)}
+            "flop_per_launch": flop_step / max(len(ranks), 1),
+            "avg_launch_ms": herk_ms / max(herk_calls, 1), "launches": int(herk_calls)}
+    tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(tfile):
+        t = json.load(open(tfile))
+        if "herk" in t:  # rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes, tools/prof_round.sh
+            roof["traffic"] = t["herk"]["hbm_bytes_per_launch"]
+            roof["traffic_unit"] = "bytes/launch (measured, " + t.get("source", "profiles") + ")"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

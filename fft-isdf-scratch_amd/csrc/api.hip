@@ -895,7 +895,10 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       // G = U U^H  (:121 by Parseval)
       FISDF_TRY(herk(c->stream, r, (int)ngrid, 1.0, Uq, ngrid, G + lq * rr, rmax, ks, kw,
                      real_q ? GEMM_RE_ONLY : GEMM_FULL));
-      if (real_q) {
+    }
+    if (real_q) {
+      StageTimer tm(c, FISDF_ST_SMALL);
+      {
         // Im(G) = Im(sum over the weight-asymmetric G only): every other (G, G') pair cancels
         const fisdf_ctx::Asym* as = nullptr;
         FISDF_TRY(get_asym(c, mesh, kmesh, a, q, wt, &as));

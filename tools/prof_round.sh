@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round profile of the C3 bench on one MI355X: default bench line (with CPU baseline),
+# rocprofv3 kernel stats, and FETCH_SIZE / WRITE_SIZE passes (separate runs) for the
+# roofline kernel's HBM traffic.  Usage: bash tools/prof_round.sh TAG
+set -o pipefail
+TAG=${1:-prof}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo BENCH FAILED; tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > $OUT/trace.json 2> $OUT/trace.err || { echo TRACE FAILED; tail -20 $OUT/trace.err; exit 1; }
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 > $OUT/fetch.json 2> $OUT/fetch.err || { echo FETCH FAILED; tail -20 $OUT/fetch.err; exit 1; }
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 > $OUT/write.json 2> $OUT/write.err || { echo WRITE FAILED; tail -20 $OUT/write.err; exit 1; }
+python3 tools/traffic.py $OUT > $OUT/traffic.json && cat $OUT/traffic.json
