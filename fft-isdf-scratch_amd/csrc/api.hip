@@ -536,12 +536,17 @@ int fisdf_select_points(fisdf_ctx* c, const void* x0v, int nk, int ng0, int nao,
   // x2 = sum_q conj(x0_q) x0_q^T   (fftisdf.py:376-378; real part taken below) as one
   // K = nk*nao Hermitian rank-K update of the permuted x0
   FISDF_TRY(select_gram(c, x0, nk, 0, nk, ng0, nao, X2, (cplx*)(b + oPm)));
-  // x4 = Re(x2)^2 / nk  (:379)
-  FISDF_TRY(square_scale(c->stream, X2, 1.0 / nk, X4, (long)ng0 * ng0));
-  // greedy pivoted Cholesky (:381-384), first nip_max pivots
-  FISDF_TRY(pchol(c->stream, X4, ng0, 0, ng0, 1, nip_max, tol, 0.0, (cplx*)(b + oL),
-                  (int*)(b + oP), (int*)(b + oR), (double*)(b + oD), (int*)(b + oF),
-                  (double*)(b + oW)));
+  // x4 = Re(x2)^2 / nk (:379) and the greedy pivoted Cholesky (:381-384), first nip_max
+  // pivots: real blocked panels (X4's storage holds the real trailing matrix)
+  bool handled = false;
+  FISDF_TRY(pchol_select_real(c->stream, X2, 1.0 / nk, ng0, nip_max, tol, (int*)(b + oP),
+                              (int*)(b + oR), (double*)X4, (int*)(b + oF), &handled));
+  if (!handled) {
+    FISDF_TRY(square_scale(c->stream, X2, 1.0 / nk, X4, (long)ng0 * ng0));
+    FISDF_TRY(pchol(c->stream, X4, ng0, 0, ng0, 1, nip_max, tol, 0.0, (cplx*)(b + oL),
+                    (int*)(b + oP), (int*)(b + oR), (double*)(b + oD), (int*)(b + oF),
+                    (double*)(b + oW)));
+  }
   int rank = 0;
   FISDF_HIP(hipMemcpyAsync(&rank, b + oR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   FISDF_HIP(hipMemcpyAsync(h_perm, b + oP, sizeof(int) * nip_max, hipMemcpyDeviceToHost, c->stream));
@@ -583,10 +588,16 @@ int fisdf_select_pivots(fisdf_ctx* c, const void* x2, int nk, int ng0, int nip_m
   FISDF_TRY(arena_get(c, cv.off, &base));
   char* b = (char*)base;
   cplx* X4 = (cplx*)(b + oX4);
-  FISDF_TRY(square_scale(c->stream, (const cplx*)x2, 1.0 / nk, X4, (long)ng0 * ng0));  // :379
-  FISDF_TRY(pchol(c->stream, X4, ng0, 0, ng0, 1, nip_max, tol, 0.0, (cplx*)(b + oL),
-                  (int*)(b + oP), (int*)(b + oR), (double*)(b + oD), (int*)(b + oF),
-                  (double*)(b + oW)));                                                // :381-384
+  bool handled = false;  // x4 = Re(x2)^2/nk (:379) + pivoted Cholesky (:381-384)
+  FISDF_TRY(pchol_select_real(c->stream, (const cplx*)x2, 1.0 / nk, ng0, nip_max, tol,
+                              (int*)(b + oP), (int*)(b + oR), (double*)X4, (int*)(b + oF),
+                              &handled));
+  if (!handled) {
+    FISDF_TRY(square_scale(c->stream, (const cplx*)x2, 1.0 / nk, X4, (long)ng0 * ng0));
+    FISDF_TRY(pchol(c->stream, X4, ng0, 0, ng0, 1, nip_max, tol, 0.0, (cplx*)(b + oL),
+                    (int*)(b + oP), (int*)(b + oR), (double*)(b + oD), (int*)(b + oF),
+                    (double*)(b + oW)));
+  }
   int rank = 0;
   FISDF_HIP(hipMemcpyAsync(&rank, b + oR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   FISDF_HIP(hipMemcpyAsync(h_perm, b + oP, sizeof(int) * nip_max, hipMemcpyDeviceToHost, c->stream));

@@ -73,6 +73,11 @@ int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int
           int* rank /*batch, device*/, double* d /*batch,n*/, int* flags /*batch*/,
           double* work /*batch*(1+rmax)*/);
 
+// selection pivots from the real Gram Re(X2)^2*scale (blocked, real; n <= 4096): *handled=false
+// otherwise.  work: n*n + 17*n + 1 doubles; piv (rmax), rank (1), flags (1) device.
+int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rmax, double tol,
+                      int* piv, int* rank, double* work, int* flags, bool* handled);
+
 // 3-D FFT (unnormalised forward, numpy.fft.fftn sign) over `rows` rows of length n0*n1*n2.
 // in-row gather `rowidx` (may be null), pre-multiply by exp(-i (f.kd)) where f are the
 // fftfreq fractions (if kd != null), post-multiply by weight[G] (if weight != null).

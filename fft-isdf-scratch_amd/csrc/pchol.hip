@@ -275,6 +275,203 @@ __global__ __launch_bounds__(PB_THREADS) void pchol_panel(const cplx* __restrict
   }
 }
 
+// ---- real blocked variant for the interpolation-point selection --------------------------
+// The selection Gram x4 = Re(x2)^2 / nk is real (fftisdf.py:376-379).  Right-looking blocked
+// pivoted Cholesky (dpstrf structure) on a real n x n trailing matrix W: one 512-thread
+// workgroup factors a panel of NB pivots with its rows' panel entries in registers (RPT rows per
+// thread; the pivot row of W is one coalesced read per pivot), then a tiled real rank-NB
+// update W -= L_panel L_panel^T.  Same pivot choice as LAPACK: arg-max of the residual
+// diagonal, first index on ties; tol <= 0 -> n * eps * max(diag).
+constexpr int PR_THREADS = 512;
+
+template <int RPT, int NB>
+__global__ __launch_bounds__(PR_THREADS) void pchol_real_panel(const double* __restrict__ W, int n,
+                                                               int rmax, int j0, double tol,
+                                                               double* __restrict__ Lpan,
+                                                               int* __restrict__ piv,
+                                                               int* __restrict__ rank,
+                                                               double* __restrict__ d,
+                                                               int* __restrict__ flags,
+                                                               double* __restrict__ thr) {
+  if (flags[0]) return;
+  __shared__ double s_v[PR_THREADS / 64];
+  __shared__ int s_i[PR_THREADS / 64];
+  __shared__ double s_lp[NB];
+  __shared__ int s_p, s_stop;
+  __shared__ double s_dp, s_thr;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  double dd[RPT];
+  double lp[RPT][NB];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int i = tid + PR_THREADS * r;
+    dd[r] = i < n ? d[i] : -1e300;
+#pragma unroll
+    for (int c = 0; c < NB; ++c) lp[r][c] = 0.0;
+  }
+  // block arg-max of (value, index): larger value, then smaller index
+  auto argmax = [&](double v, int idx, double* ov, int* oi) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double v2 = __shfl_xor(v, o, 64);
+      const int i2 = __shfl_xor(idx, o, 64);
+      if (v2 > v || (v2 == v && i2 < idx)) { v = v2; idx = i2; }
+    }
+    if (lane == 0) { s_v[wid] = v; s_i[wid] = idx; }
+    __syncthreads();
+    v = lane < PR_THREADS / 64 ? s_v[lane] : -1e300;
+    idx = lane < PR_THREADS / 64 ? s_i[lane] : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double v2 = __shfl_xor(v, o, 64);
+      const int i2 = __shfl_xor(idx, o, 64);
+      if (v2 > v || (v2 == v && i2 < idx)) { v = v2; idx = i2; }
+    }
+    *ov = v;
+    *oi = idx;
+  };
+  if (j0 == 0) {  // stopping threshold from the initial diagonal
+    double bv = -1e300;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < RPT; ++r)
+      if (dd[r] > bv) { bv = dd[r]; bi = tid + PR_THREADS * r; }
+    double m;
+    int mi;
+    argmax(bv, bi, &m, &mi);
+    if (tid == 0) {
+      s_thr = tol > 0 ? tol * m : (double)n * 2.220446049250313e-16 * m;
+      thr[0] = s_thr;
+    }
+  } else if (tid == 0) {
+    s_thr = thr[0];
+  }
+  __syncthreads();
+  const double t = s_thr;
+  int jdone = j0;
+  bool stopped = false;
+#pragma unroll
+  for (int jj = 0; jj < NB; ++jj) {
+    const int j = j0 + jj;
+    if (stopped || j >= rmax) break;  // uniform over the workgroup
+    double bv = -1e300;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < RPT; ++r)
+      if (dd[r] > bv) { bv = dd[r]; bi = tid + PR_THREADS * r; }
+    double v;
+    int p;
+    argmax(bv, bi, &v, &p);
+    if (tid == 0) {
+      s_p = p;
+      s_dp = v;
+      s_stop = !(v > t);
+      if (!s_stop) piv[j] = p;
+    }
+    __syncthreads();
+    p = s_p;
+    const double dp = s_dp;
+    if (s_stop) {
+      stopped = true;
+      break;
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r)
+      if (tid + PR_THREADS * r == p) {
+#pragma unroll
+        for (int c = 0; c < NB; ++c) s_lp[c] = lp[r][c];
+      }
+    // row p of the trailing matrix (= column p), one coalesced read per row owned
+    double wrow[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      const int i = tid + PR_THREADS * r;
+      wrow[r] = i < n ? W[(long)p * n + i] : 0.0;
+    }
+    __syncthreads();
+    const double sq = sqrt(dp), inv = 1.0 / sq;
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      const int i = tid + PR_THREADS * r;
+      double l = 0.0;
+      if (i == p) {
+        l = sq;
+        dd[r] = -1e300;
+      } else if (i < n && dd[r] > -1e299) {
+        double w = wrow[r];
+#pragma unroll
+        for (int c = 0; c < NB; ++c) w -= lp[r][c] * s_lp[c];
+        l = w * inv;
+        dd[r] -= l * l;
+      }
+      lp[r][jj] = l;
+    }
+    jdone = j + 1;
+    __syncthreads();  // s_lp / s_p reused by the next pivot
+  }
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int i = tid + PR_THREADS * r;
+    if (i < n) {
+      d[i] = dd[r];
+#pragma unroll
+      for (int c = 0; c < NB; ++c) Lpan[(long)i * NB + c] = lp[r][c];
+    }
+  }
+  if (tid == 0) {
+    rank[0] = jdone;
+    if (stopped || jdone >= rmax) flags[0] = 1;
+  }
+}
+
+// W -= Lpan Lpan^T over the full n x n matrix (64 x 64 tile per 256-thread workgroup, 4 x 4
+// elements per thread, the two NB-wide panel slices in LDS)
+template <int NB>
+__global__ __launch_bounds__(256) void syrk_real_update(double* __restrict__ W, int n,
+                                                        const double* __restrict__ Lpan,
+                                                        const int* __restrict__ flags) {
+  if (flags[0]) return;
+  __shared__ double Li[64][NB + 1], Lj[64][NB + 1];
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 64 * NB; e += 256) {
+    const int r = e / NB, c = e % NB;
+    Li[r][c] = i0 + r < n ? Lpan[(long)(i0 + r) * NB + c] : 0.0;
+    Lj[r][c] = j0 + r < n ? Lpan[(long)(j0 + r) * NB + c] : 0.0;
+  }
+  __syncthreads();
+  const int ti = (tid >> 4) * 4, tj = (tid & 15) * 4;
+  double acc[4][4] = {};
+#pragma unroll 2
+  for (int c = 0; c < NB; ++c)
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] += Li[ti + a][c] * Lj[tj + b][c];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int i = i0 + ti + a;
+    if (i >= n) continue;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int j = j0 + tj + b;
+      if (j < n) W[(long)i * n + j] -= acc[a][b];
+    }
+  }
+}
+
+__global__ void real_square_scale_kernel(const cplx* __restrict__ in, double s,
+                                         double* __restrict__ out, double* __restrict__ d,
+                                         long n2, int n) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n2;
+       e += (long)gridDim.x * blockDim.x) {
+    const double r = in[e].x;
+    const double v = r * r * s;
+    out[e] = v;
+    if (e / n == e % n) d[e / n] = v;
+  }
+}
+
 }  // namespace
 
 // pivot values are kept in `dmax0 + batch` (caller allocates 2*batch + batch*rmax doubles: see api)
@@ -324,6 +521,36 @@ int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int
                        flags, thr);
   }
   FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+// selection: pivots of the real Gram x4 = Re(X2)^2 * scale (n x n, X2 complex); piv/rank
+// device; work = W (n*n doubles) + L panel (n*16) + d (n) + thr; flags (1 int).  Returns 1 in
+// *handled when n fits the register panel (n <= 4096), else 0 (caller uses pchol).
+int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rmax, double tol,
+                      int* piv, int* rank, double* work, int* flags, bool* handled) {
+  *handled = false;
+  if (n > 8 * PR_THREADS || rmax <= 0) return 0;
+  double* W = work;
+  double* Lpan = W + (long)n * n;
+  double* d = Lpan + (long)n * 16;
+  double* thr = d + n;
+  FISDF_HIP(hipMemsetAsync(flags, 0, sizeof(int), s));
+  FISDF_HIP(hipMemsetAsync(rank, 0, sizeof(int), s));
+  const long n2 = (long)n * n;
+  hipLaunchKernelGGL(real_square_scale_kernel, dim3((unsigned)std::min<long>((n2 + 255) / 256, 8192)),
+                     dim3(256), 0, s, X2, scale, W, d, n2, n);
+  FISDF_HIP(hipGetLastError());
+  const int rpt = (n + PR_THREADS - 1) / PR_THREADS;
+  const dim3 ug((n + 63) / 64, (n + 63) / 64);
+#define FISDF_PR(R, NBv)                                                                         for (int j0 = 0; j0 < rmax; j0 += NBv) {                                                          hipLaunchKernelGGL((pchol_real_panel<R, NBv>), dim3(1), dim3(PR_THREADS), 0, s, W, n, rmax,                        j0, tol, Lpan, piv, rank, d, flags, thr);                                   if (j0 + NBv < rmax)                                                                             hipLaunchKernelGGL((syrk_real_update<NBv>), ug, dim3(256), 0, s, W, n, Lpan, flags);        }
+  if (rpt <= 2) { FISDF_PR(2, 16) }
+  else if (rpt <= 4) { FISDF_PR(4, 16) }
+  else if (rpt <= 7) { FISDF_PR(7, 12) }
+  else { FISDF_PR(8, 8) }
+#undef FISDF_PR
+  FISDF_HIP(hipGetLastError());
+  *handled = true;
   return 0;
 }
 

@@ -160,7 +160,8 @@ def test_gpu_selection(name):
     perm_gpu = df.perm
     assert len(perm_gpu) == o["nip"]
     overlap = len(set(perm_gpu.tolist()) & set(o["perm"].tolist())) / o["nip"]
-    print(f"{name}: pivot-set overlap with dpstrf {overlap:.3f}")
+    first = int(np.argmax(perm_gpu != o["perm"])) if (perm_gpu != o["perm"]).any() else len(perm_gpu)
+    print(f"{name}: pivot-set overlap with dpstrf {overlap:.3f}, identical prefix {first}/{o['nip']}")
     # greedy order is tie-sensitive on a symmetric crystal: compare the resulting J/K
     vj, vk = df.get_jk(dm)
     assert abs(vj - o["vj"]).max() < 1e-7
