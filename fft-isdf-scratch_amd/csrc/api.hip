@@ -42,6 +42,11 @@ struct fisdf_ctx {
   cplx* f_Lp = nullptr;     // (nk, nip*nip) pivot-order factor, ld = rank_q
   cplx* f_Linv = nullptr;   // (nk, nblk*nb*nb)
   cplx* f_Q = nullptr;      // (nk, nip, nip) block-row operator of trsm_merged (build_trsm_q)
+  cplx* f_x4s = nullptr;    // (nk, nip, nip) staged x4_q of the factored slots
+  int* f_fail_pinned = nullptr;  // unpivoted path: per-slot failure flags (host, pinned)
+  double f_tol = 1e-14;
+  bool f_check_fail = false, f_used_pivoted = false;
+  int force_pivoted = -1;  // fisdf_set_pivoted_fit; -1: environment FISDF_PIVOTED_FIT
   int* f_piv = nullptr;     // (nk, nip)
   int* f_rank_dev = nullptr;
   std::vector<int> f_rank;  // host copy
@@ -206,6 +211,10 @@ int free_factors(fisdf_ctx* c) {
   if (c->f_Linv) FISDF_HIP(hipFree(c->f_Linv));
   if (c->f_Q) FISDF_HIP(hipFree(c->f_Q));
   c->f_Q = nullptr;
+  if (c->f_x4s) FISDF_HIP(hipFree(c->f_x4s));
+  c->f_x4s = nullptr;
+  if (c->f_fail_pinned) FISDF_HIP(hipHostFree(c->f_fail_pinned));
+  c->f_fail_pinned = nullptr;
   if (c->f_piv) FISDF_HIP(hipFree(c->f_piv));
   if (c->f_rank_dev) FISDF_HIP(hipFree(c->f_rank_dev));
   if (c->f_rank_pinned) FISDF_HIP(hipHostFree(c->f_rank_pinned));
@@ -722,6 +731,43 @@ int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk
 }
 
 // ---- A4 ---------------------------------------------------------------------
+// rank copies, pivot-order factor (identity-padded to nip so the small back-substitutions of
+// all q run as one batch), diagonal-block inverses and the merged TRSM operator, on stream s
+int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src) {
+  const int nk = c->f_nk, nip = c->f_nip, nb = c->f_nb, nblk = (nip + nb - 1) / nb;
+  const long nn = (long)nip * nip;
+  FISDF_HIP(hipMemcpyAsync(c->f_rank_pinned, rank_dev_src, sizeof(int) * nk, hipMemcpyDeviceToHost, s));
+  FISDF_HIP(hipMemcpyAsync(c->f_rank_dev, rank_dev_src, sizeof(int) * nk, hipMemcpyDeviceToDevice, s));
+  FISDF_TRY(gather_lp(s, c->f_L, nip, nip, c->f_piv, c->f_rank_dev, nip, c->f_Lp, nk));
+  FISDF_TRY(trinv_blocks(s, c->f_Lp, nip, nip, nn, nb, (long)nblk * nb * nb, c->f_Linv, nk));
+  FISDF_TRY(build_trsm_q(s, c->f_Lp, nip, nn, c->f_Q, nk, GEMM_FULL));
+  return 0;
+}
+
+bool pivoted_fit_forced() {
+  static const bool on = [] {
+    const char* e = getenv("FISDF_PIVOTED_FIT");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+// the greedy pivoted (rank-revealing) factorisation of the staged x4 (fallback / forced)
+int factor_pivoted(fisdf_ctx* c, hipStream_t s) {
+  const int nk = c->f_nk, nip = c->f_nip;
+  const long nn = (long)nip * nip;
+  char* b = (char*)c->f_scratch;
+  Carver cv;
+  size_t oR = cv.take(sizeof(int) * nk);
+  size_t oD = cv.take(sizeof(double) * (size_t)nk * nip);
+  size_t oF = cv.take(sizeof(int) * nk);
+  size_t oW = cv.take(sizeof(double) * (size_t)nk * (1 + nip));
+  FISDF_TRY(pchol(s, c->f_x4s, nip, nn, nip, nk, nip, c->f_tol, 0.0, c->f_L, c->f_piv,
+                  (int*)(b + oR), (double*)(b + oD), (int*)(b + oF), (double*)(b + oW)));
+  c->f_used_pivoted = true;
+  return factor_finish(c, s, (const int*)(b + oR));
+}
+
 int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int nq, int nip,
                           double tol_rel, const int* kmesh) {
   FISDF_TRY(device_guard(c));
@@ -738,60 +784,77 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   const int nb = c->f_nb;
   const int nblk = (nip + nb - 1) / nb;
   const long nn = (long)nip * nip;
-  bool any_real = false;
-  for (int i = 0; kmesh && i < nq; ++i) any_real |= self_conjugate(kmesh, h_qs[i]);
-  const bool contiguous = h_qs[nq - 1] - h_qs[0] == nq - 1 && !any_real;
-  const void* x4v = (const cplx*)x4all + (long)h_qs[0] * nn;
+  FISDF_HIP(hipMalloc(&c->f_x4s, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_L, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_Lp, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_Linv, sizeof(cplx) * (size_t)nk * nblk * nb * nb));
+  FISDF_HIP(hipMalloc(&c->f_Q, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_piv, sizeof(int) * (size_t)nk * nip));
   FISDF_HIP(hipMalloc(&c->f_rank_dev, sizeof(int) * nk));
   FISDF_HIP(hipHostMalloc((void**)&c->f_rank_pinned, sizeof(int) * nk, hipHostMallocDefault));
+  FISDF_HIP(hipHostMalloc((void**)&c->f_fail_pinned, sizeof(int) * nk, hipHostMallocDefault));
+  // scratch: pivoted pchol work, or the unpivoted path's rank/fail flags + block inverses
   Carver cv;
-  size_t oR = cv.take(sizeof(int) * nk);
-  size_t oD = cv.take(sizeof(double) * (size_t)nk * nip);
-  size_t oF = cv.take(sizeof(int) * nk);
-  size_t oW = cv.take(sizeof(double) * (size_t)nk * (1 + nip));
+  cv.take(sizeof(int) * nk);
+  cv.take(sizeof(double) * (size_t)nk * nip);
+  cv.take(sizeof(int) * nk);
+  cv.take(sizeof(double) * (size_t)nk * (1 + nip));
+  size_t oU = cv.take(sizeof(int) * nk);                                   // unpivoted rank
+  size_t oFl = cv.take(sizeof(int) * nk);                                  // unpivoted fail
+  size_t oWk = cv.take(sizeof(cplx) * (size_t)nk * 4096 + sizeof(double) * nk);
   if (cv.off > c->f_scratch_size) {
     if (c->f_scratch) FISDF_HIP(hipFree(c->f_scratch));
     FISDF_HIP(hipMalloc(&c->f_scratch, cv.off));
     c->f_scratch_size = cv.off;
   }
   char* b = (char*)c->f_scratch;
+  c->f_qs.assign(h_qs, h_qs + nq);
+  c->f_real.assign(nq, 0);
+  for (int i = 0; kmesh && i < nq; ++i) c->f_real[i] = self_conjugate(kmesh, h_qs[i]) ? 1 : 0;
+  c->f_nk = nk;
+  c->f_nip = nip;
+  c->f_tol = tol_rel;
+  c->f_used_pivoted = false;
   // the side stream starts once everything enqueued on `stream` so far (x4) is done; work
   // enqueued on `stream` after this call (the y build) runs concurrently
   FISDF_HIP(hipEventRecord(c->ev_x4, c->stream));
   FISDF_HIP(hipStreamWaitEvent(c->side, c->ev_x4, 0));
   StageTimer tm(c, FISDF_ST_FACTOR, c->side);
   hipStream_t s = c->side;
-  if (!contiguous) {  // gather the listed x4_q (f_Lp is overwritten by gather_lp only later)
-    for (int i = 0; i < nq; ++i) {
-      FISDF_HIP(hipMemcpyAsync(c->f_Lp + i * nn, (const cplx*)x4all + (long)h_qs[i] * nn,
-                               sizeof(cplx) * nn, hipMemcpyDeviceToDevice, s));
-      // self-conjugate q: x4_q = Phi[:,q]^H x4_s is real up to rounding; factor it as real
-      if (kmesh && self_conjugate(kmesh, h_qs[i])) FISDF_TRY(zero_imag(s, c->f_Lp + i * nn, nn));
-    }
-    x4v = c->f_Lp;
+  // stage the listed x4_q; self-conjugate q: x4_q = Phi[:,q]^H x4_s is real up to rounding
+  for (int i = 0; i < nq; ++i) {
+    FISDF_HIP(hipMemcpyAsync(c->f_x4s + i * nn, (const cplx*)x4all + (long)h_qs[i] * nn,
+                             sizeof(cplx) * nn, hipMemcpyDeviceToDevice, s));
+    if (c->f_real[i]) FISDF_TRY(zero_imag(s, c->f_x4s + i * nn, nn));
   }
-  c->f_qs.assign(h_qs, h_qs + nq);
-  c->f_real.assign(nq, 0);
-  for (int i = 0; kmesh && i < nq; ++i) c->f_real[i] = self_conjugate(kmesh, h_qs[i]) ? 1 : 0;
-  c->f_nk = nk;
-  c->f_nip = nip;
-  FISDF_TRY(pchol(s, (const cplx*)x4v, nip, nn, nip, nk, nip, tol_rel, 0.0, c->f_L, c->f_piv,
-                  (int*)(b + oR), (double*)(b + oD), (int*)(b + oF), (double*)(b + oW)));
-  FISDF_HIP(hipMemcpyAsync(c->f_rank_pinned, b + oR, sizeof(int) * nk, hipMemcpyDeviceToHost, s));
-  FISDF_HIP(hipMemcpyAsync(c->f_rank_dev, b + oR, sizeof(int) * nk, hipMemcpyDeviceToDevice, s));
-  // pivot-order factor padded to nip x nip (identity beyond the rank) so the small
-  // back-substitutions of all q can run as one batch
-  FISDF_TRY(gather_lp(s, c->f_L, nip, nip, c->f_piv, c->f_rank_dev, nip, c->f_Lp, nk));
-  FISDF_TRY(trinv_blocks(s, c->f_Lp, nip, nip, nn, nb, (long)nblk * nb * nb, c->f_Linv, nk));
-  // merged forward-substitution operator (used for the q whose rank is nip)
-  FISDF_HIP(hipMalloc(&c->f_Q, sizeof(cplx) * nk * nn));
-  FISDF_TRY(build_trsm_q(s, c->f_Lp, nip, nn, c->f_Q, nk, GEMM_FULL));
+  if (c->force_pivoted == 1 || (c->force_pivoted < 0 && pivoted_fit_forced())) {
+    FISDF_TRY(factor_pivoted(c, s));
+    c->f_check_fail = false;
+  } else {
+    // full-rank fast path: unpivoted blocked Cholesky (all pivots > tol_rel * max diag is the
+    // same full-rank verdict the rank-revealing pivoted factorisation gives); any matrix that
+    // fails it is redone by the pivoted pchol in fisdf_factor_x4_wait
+    FISDF_HIP(hipMemcpyAsync(c->f_L, c->f_x4s, sizeof(cplx) * nk * nn, hipMemcpyDeviceToDevice, s));
+    FISDF_TRY(chol_unpivoted(s, c->f_L, nip, nk, tol_rel, c->f_piv, (int*)(b + oU),
+                             (int*)(b + oFl), (cplx*)(b + oWk)));
+    FISDF_HIP(hipMemcpyAsync(c->f_fail_pinned, b + oFl, sizeof(int) * nk, hipMemcpyDeviceToHost, s));
+    FISDF_TRY(factor_finish(c, s, (const int*)(b + oU)));
+    c->f_check_fail = true;
+  }
   FISDF_HIP(hipEventRecord(c->ev_fac, s));
   c->f_pending = true;
+  return 0;
+}
+
+int fisdf_set_pivoted_fit(fisdf_ctx* c, int mode) {
+  FISDF_CHECK(c != nullptr && mode >= -1 && mode <= 1, "set_pivoted_fit: bad mode");
+  c->force_pivoted = mode;
+  return 0;
+}
+
+int fisdf_factor_info(fisdf_ctx* c, int* h_used_pivoted) {
+  FISDF_CHECK(c != nullptr, "null context");
+  if (h_used_pivoted) *h_used_pivoted = c->f_used_pivoted ? 1 : 0;
   return 0;
 }
 
@@ -799,6 +862,16 @@ int fisdf_factor_x4_wait(fisdf_ctx* c, int* h_ranks) {
   FISDF_TRY(device_guard(c));
   if (c->f_pending) {
     FISDF_HIP(hipEventSynchronize(c->ev_fac));
+    if (c->f_check_fail) {
+      bool any = false;
+      for (int q = 0; q < c->f_nk; ++q) any |= c->f_fail_pinned[q] != 0;
+      c->f_check_fail = false;
+      if (any) {  // not numerically full rank at tol: rank-revealing pivoted factorisation
+        FISDF_TRY(factor_pivoted(c, c->side));
+        FISDF_HIP(hipEventRecord(c->ev_fac, c->side));
+        FISDF_HIP(hipEventSynchronize(c->ev_fac));
+      }
+    }
     c->f_rank.assign(c->f_rank_pinned, c->f_rank_pinned + c->f_nk);
     FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_fac, 0));  // factors before any later use
     c->f_pending = false;

@@ -472,6 +472,85 @@ __global__ void real_square_scale_kernel(const cplx* __restrict__ in, double s,
   }
 }
 
+// ---- unpivoted blocked Cholesky (full-rank fast path of the x4_q factorisation) -----------
+// Right-looking, 64-column blocks, batched over q: the diagonal block is factored and inverted
+// in LDS by one workgroup per matrix, the panel below is multiplied by the block inverse^H
+// (in-place ZGEMM) and the trailing matrix gets a ZGEMM rank-64 update.  A matrix whose pivot
+// falls to <= tol_rel * max(initial diag) is flagged (the caller then uses the pivoted,
+// rank-revealing pchol for the batch).  Pivots = identity, rank = n on success.
+__global__ void diag_max_kernel(const cplx* __restrict__ A, int n, long sA, double tol_rel,
+                                double* __restrict__ thr, int* __restrict__ fail) {
+  A += blockIdx.x * sA;
+  __shared__ double sv[256];
+  double m = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmax(m, A[(long)i * n + i].x);
+  sv[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sv[threadIdx.x] = fmax(sv[threadIdx.x], sv[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    thr[blockIdx.x] = tol_rel * sv[0];
+    fail[blockIdx.x] = 0;
+  }
+}
+
+// factor + invert the m x m diagonal block at (b0, b0) of W (ld n); writes L_bb (lower) in
+// place and L_bb^{-1} to Linv (64 x 64, batch stride 4096)
+__global__ __launch_bounds__(64) void chol_diag_kernel(cplx* __restrict__ W, int n, long sW,
+                                                       int b0, int m,
+                                                       const double* __restrict__ thr,
+                                                       int* __restrict__ fail,
+                                                       cplx* __restrict__ Linv) {
+  const int b = blockIdx.x;
+  W += b * sW;
+  Linv += (long)b * 4096;
+  __shared__ cplx A[64][65];
+  __shared__ cplx X[64][65];
+  __shared__ int bad;
+  const int t = threadIdx.x;
+  if (t == 0) bad = 0;
+  for (int i = 0; i < m; ++i)
+    if (t < m) A[i][t] = W[(long)(b0 + i) * n + b0 + t];
+  __syncthreads();
+  const double th = thr[b];
+  for (int k = 0; k < m; ++k) {
+    const double dk = A[k][k].x;
+    if (t == 0 && !(dk > th)) bad = 1;
+    const double lk = sqrt(fmax(dk, 1e-300));
+    __syncthreads();
+    if (t > k && t < m) A[t][k] = cscale(A[t][k], 1.0 / lk);
+    if (t == k) A[k][k] = cmk(lk, 0.0);
+    __syncthreads();
+    if (t > k && t < m)  // row t: A[t][j] -= A[t][k] conj(A[j][k]), k < j <= t
+      for (int j = k + 1; j <= t; ++j) A[t][j] = csub(A[t][j], cmul(A[t][k], cconj(A[j][k])));
+    __syncthreads();
+  }
+  // inverse of the lower-triangular block, column t by forward substitution
+  if (t < m) {
+    for (int i = 0; i < m; ++i) {
+      cplx sacc = cmk(i == t ? 1.0 : 0.0, 0.0);
+      for (int q = t; q < i; ++q) sacc = csub(sacc, cmul(A[i][q], X[q][t]));
+      const double d = A[i][i].x;
+      X[i][t] = i < t ? cmk(0, 0) : cscale(sacc, 1.0 / d);
+    }
+  }
+  __syncthreads();
+  for (int i = 0; i < m; ++i)
+    if (t < m && t <= i) W[(long)(b0 + i) * n + b0 + t] = A[i][t];
+  for (int i = 0; i < 64; ++i)
+    if (t < 64) Linv[i * 64 + t] = (i < m && t < m) ? X[i][t] : cmk(i == t ? 1.0 : 0.0, 0.0);
+  if (t == 0 && bad) fail[b] = 1;
+}
+
+__global__ void chol_finish_kernel(int n, int* __restrict__ piv, int* __restrict__ rank,
+                                   const int* __restrict__ fail) {
+  const int b = blockIdx.x;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) piv[(long)b * n + i] = i;
+  if (threadIdx.x == 0) rank[b] = fail[b] ? 0 : n;
+}
+
 }  // namespace
 
 // pivot values are kept in `dmax0 + batch` (caller allocates 2*batch + batch*rmax doubles: see api)
@@ -520,6 +599,38 @@ int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int
     hipLaunchKernelGGL(pchol_pick, dim3(batch), dim3(nt), 0, s, n, rmax, j, piv, pval, rank, d,
                        flags, thr);
   }
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+// Unpivoted blocked Cholesky of batch n x n Hermitian matrices W (in place, ld n, batch stride
+// n*n; lower triangle = L on return).  fail[b] = 1 if a pivot <= tol_rel*max(diag) (the caller
+// falls back to pchol); piv = identity, rank = n (0 if failed).  work: batch*(4096 cplx) +
+// batch doubles.
+int chol_unpivoted(hipStream_t s, cplx* W, int n, int batch, double tol_rel, int* piv, int* rank,
+                   int* fail, cplx* work) {
+  FISDF_CHECK(n > 0 && batch > 0, "chol_unpivoted: bad sizes");
+  const long nn = (long)n * n;
+  cplx* Linv = work;
+  double* thr = (double*)(work + (long)batch * 4096);
+  hipLaunchKernelGGL(diag_max_kernel, dim3(batch), dim3(256), 0, s, W, n, nn, tol_rel, thr, fail);
+  FISDF_HIP(hipGetLastError());
+  const cplx one = cmk(1, 0), mone = cmk(-1, 0), zero = cmk(0, 0);
+  for (int b0 = 0; b0 < n; b0 += 64) {
+    const int m = std::min(64, n - b0), b1 = b0 + m;
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(batch), dim3(64), 0, s, W, n, nn, b0, m, thr, fail,
+                       Linv);
+    FISDF_HIP(hipGetLastError());
+    if (b1 < n) {
+      // panel: W[b1:, b0:b1] <- W[b1:, b0:b1] L_bb^{-H}  (in place: one N tile, rows per WG)
+      FISDF_TRY(zgemm(s, OP_N, OP_C, n - b1, m, m, one, W + (long)b1 * n + b0, n, nn, Linv, 64,
+                      4096, zero, W + (long)b1 * n + b0, n, nn, batch));
+      // trailing: W[b1:, b1:] -= P P^H
+      FISDF_TRY(zgemm(s, OP_N, OP_C, n - b1, n - b1, m, mone, W + (long)b1 * n + b0, n, nn,
+                      W + (long)b1 * n + b0, n, nn, one, W + (long)b1 * n + b1, n, nn, batch));
+    }
+  }
+  hipLaunchKernelGGL(chol_finish_kernel, dim3(batch), dim3(256), 0, s, n, piv, rank, fail);
   FISDF_HIP(hipGetLastError());
   return 0;
 }

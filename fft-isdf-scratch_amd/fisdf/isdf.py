@@ -103,6 +103,9 @@ class InterpolativeSeparableDensityFitting:
     # q with 2 k_q in the reciprocal lattice (Gamma, all q of a 2x2x2 mesh): real x4_q and
     # W_q, fitted with real-factor / real-part GEMMs (half the MFMA work)
     real_self_conjugate = True
+    # x4_q factorisation: None = library default (unpivoted blocked Cholesky when every x4_q
+    # is numerically full rank, else the greedy pivoted one); True forces the pivoted path
+    pivoted_fit = None
 
     def __init__(self, cell, kpts, m0=None, c0=20.0, device=None, comm=None):
         self.cell = cell
@@ -391,6 +394,8 @@ def build(df_obj):
     f = df_obj._ao_grid
     # x4_q factorisation (replaces zgelsy's QRCP, :108) on the library's side stream,
     # overlapped with the y build enqueued next on the main stream
+    d.ctx.call("fisdf_set_pivoted_fit", -1 if df_obj.pivoted_fit is None
+               else (1 if df_obj.pivoted_fit else 0))
     if nq:
         d.ctx.call("fisdf_factor_x4_async", _lib.ptr(x4), qs_c, nq, nip, float(df_obj.fit_tol),
                    km_p if df_obj.real_self_conjugate else None)
@@ -416,6 +421,9 @@ def build(df_obj):
     ranks = np.zeros(nq, np.int32)
     if nq:
         d.ctx.call("fisdf_factor_x4_wait", ranks.ctypes.data_as(_lib._ip))
+        used = C_int()
+        d.ctx.call("fisdf_factor_info", byref(used))
+        df_obj.used_pivoted_fit = bool(used.value)
     if d.size > 1:
         if work is not None:
             work.wait()

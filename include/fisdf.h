@@ -129,6 +129,13 @@ int fisdf_factor_x4_qs(fisdf_ctx* ctx, const void* d_x4, const int* h_qs, int nq
 int fisdf_factor_x4_async(fisdf_ctx* ctx, const void* d_x4, const int* h_qs, int nq, int nip,
                           double tol_rel, const int* kmesh);
 int fisdf_factor_x4_wait(fisdf_ctx* ctx, int* h_ranks /* nq, may be NULL */);
+/* Factorisation path.  Default (mode -1: unless FISDF_PIVOTED_FIT=1 in the environment): an
+ * unpivoted blocked Cholesky, kept when every pivot exceeds tol_rel * max(diag) (the full-rank
+ * verdict of the rank-revealing factorisation) and otherwise redone — for the whole batch —
+ * by the greedy pivoted Cholesky; mode 1 forces the pivoted one, mode 0 the default.
+ * fisdf_factor_info: 1 if the last factorisation used the pivoted path. */
+int fisdf_set_pivoted_fit(fisdf_ctx* ctx, int mode);
+int fisdf_factor_info(fisdf_ctx* ctx, int* h_used_pivoted);
 
 /* ---- A4+A5: fit + FFT Coulomb for the factored shard q in [q0, q1) (fftisdf.py:97-121)
  * Needs fisdf_factor_x4 on the same range.  W_q = zeta_q z_q^H computed as

@@ -20,7 +20,7 @@ JK_TOL = 1e-8   # Ha, north_star
 JK_TOL_RANK_DEFICIENT_TR = 1.5e-8
 
 
-def make_df(name, inject=True, time_reversal=True, real_sc=True):
+def make_df(name, inject=True, time_reversal=True, real_sc=True, pivoted=None):
     from fisdf import ISDF
     cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
     o = oracle(name)
@@ -28,6 +28,7 @@ def make_df(name, inject=True, time_reversal=True, real_sc=True):
     df = ISDF(cell, kpts, m0=list(m0), c0=c0)
     df.time_reversal = time_reversal
     df.real_self_conjugate = real_sc
+    df.pivoted_fit = pivoted
     d = df.device
     df._kmesh()
     df._ao_parent = d.to_dev(x0)
@@ -99,6 +100,28 @@ def test_real_self_conjugate_path(name):
     dw = abs(res[True][2] - res[False][2]).max() / abs(res[False][2]).max()
     d = max(abs(res[True][0] - res[False][0]).max(), abs(res[True][1] - res[False][1]).max())
     print(f"{name}: |JK(real) - JK(complex)| = {d:.2e}, rel |dW| = {dw:.2e}")
+    assert d < JK_TOL
+
+
+@pytest.mark.parametrize("name", ["toy331_fr", "toy333_fr", "nio_small", "toy331"])
+def test_unpivoted_fast_path(name):
+    """The full-rank fast path (unpivoted blocked Cholesky) gives the J/K of the pivoted
+    rank-revealing factorisation; rank-deficient x4_q fall back to the pivoted path."""
+    res = {}
+    for piv in (True, None):
+        df, o, dm = make_df(name, pivoted=piv)
+        df.build()
+        vj, vk = df.get_jk(dm)
+        full_rank = min(df.ranks) == df.nip
+        print(f"{name} pivoted={piv}: used_pivoted={df.used_pivoted_fit} ranks "
+              f"{min(df.ranks)}-{max(df.ranks)} |dK|={abs(vk - o['vk']).max():.2e}")
+        if piv is None:
+            assert df.used_pivoted_fit == (not full_rank)
+        tol = JK_TOL if full_rank else JK_TOL_RANK_DEFICIENT_TR
+        assert abs(vj - o["vj"]).max() < tol and abs(vk - o["vk"]).max() < tol
+        res[piv] = (vj, vk)
+    d = max(abs(res[True][0] - res[None][0]).max(), abs(res[True][1] - res[None][1]).max())
+    print(f"{name}: |JK(unpivoted) - JK(pivoted)| = {d:.2e}")
     assert d < JK_TOL
 
 
