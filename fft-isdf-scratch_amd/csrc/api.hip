@@ -900,9 +900,14 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   FISDF_TRY(device_guard(c));
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
   FISDF_TRY(check_qlist(h_qs, nq, nk, "fit_coulomb"));
-  FISDF_CHECK(c->f_nk == nq && c->f_nip == nip &&
-                  std::equal(c->f_qs.begin(), c->f_qs.end(), h_qs),
-              "fit_coulomb: call fisdf_factor_x4 on the same q-list first");
+  // the listed q must be a contiguous run of the factored q-list (slots s0 .. s0+nq-1): the
+  // whole shard at once, or one q at a time as its y arrives (overlapped all-to-all)
+  FISDF_CHECK(c->f_nip == nip && nq >= 1, "fit_coulomb: call fisdf_factor_x4 first");
+  const auto it0 = std::find(c->f_qs.begin(), c->f_qs.end(), h_qs[0]);
+  FISDF_CHECK(it0 != c->f_qs.end() && (it0 - c->f_qs.begin()) + nq <= (long)c->f_qs.size() &&
+                  std::equal(h_qs, h_qs + nq, it0),
+              "fit_coulomb: the q-list must be a contiguous run of the factored q-list");
+  const int s0 = (int)(it0 - c->f_qs.begin());
   FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
   const long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
   const long nn = (long)nip * nip;
@@ -914,7 +919,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   const cplx* yT = (const cplx*)yTv;
   cplx* Wq = (cplx*)Wqv;
   int rmax = 0;
-  for (int lq = 0; lq < nq; ++lq) rmax = std::max(rmax, c->f_rank[lq]);
+  for (int lq = 0; lq < nq; ++lq) rmax = std::max(rmax, c->f_rank[s0 + lq]);
   const int ks = pick_ksplit_herk(rmax, (int)ngrid, num_cus(c->device));
   const long rr = (long)rmax * rmax;
   const long sLi = (long)nblk * nb * nb;
@@ -943,12 +948,13 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   FISDF_HIP(hipMemsetAsync(G, 0, sizeof(cplx) * nq * rr, c->stream));
   for (int lq = 0; lq < nq; ++lq) {
     const int q = h_qs[lq];
-    const int r = c->f_rank[lq];
+    const int sl = s0 + lq;  // factor slot
+    const int r = c->f_rank[sl];
     if (r == 0) continue;
-    const int* piv = c->f_piv + (long)lq * nip;
-    const cplx* Lp = c->f_Lp + (long)lq * nn;
-    const bool real_q = c->f_real[lq];
-    const cplx* Linv = c->f_Linv + (long)lq * sLi;
+    const int* piv = c->f_piv + (long)sl * nip;
+    const cplx* Lp = c->f_Lp + (long)sl * nn;
+    const bool real_q = c->f_real[sl];
+    const cplx* Linv = c->f_Linv + (long)sl * sLi;
     double kq[3], kd[3];
     kpoint(kmesh, g, q, kq);
     for (int i = 0; i < 3; ++i) kd[i] = g.a[i][0] * kq[0] + g.a[i][1] * kq[1] + g.a[i][2] * kq[2];
@@ -965,7 +971,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       StageTimer tm(c, FISDF_ST_TRSM);
       // U = L^{-1} Yh   (fit, factored order; (x4_q)_PP = L L^H)
       if (r == nip) {  // merged block-row substitution, in place
-        FISDF_TRY(trsm_merged(c->stream, c->f_Q + (long)lq * nn, nip, Yh, ngrid, (int)ngrid,
+        FISDF_TRY(trsm_merged(c->stream, c->f_Q + (long)sl * nn, nip, Yh, ngrid, (int)ngrid,
                               real_q ? GEMM_A_REAL : GEMM_FULL));
         Uq = Yh;
       } else {
@@ -999,13 +1005,16 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     StageTimer tm(c, FISDF_ST_SMALL);
     // W_PP = L^{-H} G L^{-1} for all q of the shard at once (L padded with identity, G with
     // zeros beyond each rank):  T = L^{-H} G ; S = L^{-H} T^H ; W_PP = S^H ; scatter by pivots
-    FISDF_TRY(trsm_blocked(c->stream, 0, c->f_Lp, nip, nn, rmax, c->f_Linv, sLi, nb, G, rmax, rr,
+    const cplx* Lp0 = c->f_Lp + (long)s0 * nn;
+    const cplx* Li0 = c->f_Linv + (long)s0 * sLi;
+    FISDF_TRY(trsm_blocked(c->stream, 0, Lp0, nip, nn, rmax, Li0, sLi, nb, G, rmax, rr,
                            T, rmax, rr, rmax, nq));
     FISDF_TRY(conj_transpose(c->stream, T, rmax, rr, G, nq));
-    FISDF_TRY(trsm_blocked(c->stream, 0, c->f_Lp, nip, nn, rmax, c->f_Linv, sLi, nb, G, rmax, rr,
+    FISDF_TRY(trsm_blocked(c->stream, 0, Lp0, nip, nn, rmax, Li0, sLi, nb, G, rmax, rr,
                            S, rmax, rr, rmax, nq));
     FISDF_TRY(conj_transpose(c->stream, S, rmax, rr, T, nq));
-    FISDF_TRY(scatter_w(c->stream, T, rmax, rr, rmax, c->f_piv, c->f_rank_dev, Wq, nip, nq));
+    FISDF_TRY(scatter_w(c->stream, T, rmax, rr, rmax, c->f_piv + (long)s0 * nip,
+                        c->f_rank_dev + s0, Wq, nip, nq));
   }
   return 0;
 }

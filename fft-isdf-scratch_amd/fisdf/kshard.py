@@ -51,6 +51,37 @@ def shard_list(items, rank: int, size: int):
     return items[a:b]
 
 
+def balanced_chunks(costs, size: int):
+    """Split items (in order) into `size` contiguous chunks minimising the largest chunk cost
+    (linear partition by binary search on the bound).  Returns [(a, b)] per rank."""
+    import numpy as np
+    c = np.asarray(costs, dtype=float)
+    n = len(c)
+    if size <= 1 or n == 0:
+        return [(0, n)] + [(n, n)] * (size - 1)
+
+    def split(bound):
+        out, a, acc = [], 0, 0.0
+        for i in range(n):
+            if acc + c[i] > bound + 1e-12 and i > a:
+                out.append((a, i))
+                a, acc = i, 0.0
+            acc += c[i]
+        out.append((a, n))
+        return out
+
+    lo, hi = float(c.max()), float(c.sum())
+    for _ in range(60):
+        mid = 0.5 * (lo + hi)
+        if len(split(mid)) <= size:
+            hi = mid
+        else:
+            lo = mid
+    out = split(hi)
+    out += [(n, n)] * (size - len(out))
+    return out
+
+
 def owner_of(q: int, nk: int, size: int) -> int:
     for r in range(size):
         q0, q1 = shard_range(nk, r, size)
@@ -99,6 +130,54 @@ def exchange_y(send, nk: int, nip: int, slices, rank: int, size: int, group=None
         work = dist.all_to_all_single(recv, flat, out_splits, in_splits, group=group,
                                       async_op=async_op)
     return (recv, work) if async_op else recv
+
+
+def exchange_y_chunked(send, nip: int, slices, rank: int, size: int, group, counts):
+    """The all-to-all of exchange_y split per local q index j, so the fit of a rank's j-th q
+    can start as soon as its own piece has arrived (the later pieces move over xGMI while
+    the earlier q are fitted).  `send` is (nq_all, nip, ng_rank) in rank-chunk order with
+    counts[r] q per rank.  Returns [(recv_j, work_j)] for j < counts[rank]; recv_j is
+    concat_p (nip, ng_p); call work_j.wait() (may be None) before reading recv_j."""
+    import torch
+    import torch.distributed as dist
+    starts = [sum(counts[:r]) for r in range(size)]
+    ng_self = slices[rank][1]
+    nmax = max(counts) if counts else 0
+    out = []
+    host = _host_staged(group, send)
+    for j in range(nmax):
+        dst = [r for r in range(size) if j < counts[r]]
+        idx = torch.tensor([starts[r] + j for r in dst], dtype=torch.long, device=send.device)
+        sj = send.index_select(0, idx).reshape(-1) if len(dst) else send.new_empty(0)
+        in_splits = [nip * ng_self if j < counts[r] else 0 for r in range(size)]
+        mine = j < counts[rank]
+        out_splits = [nip * slices[p][1] if mine else 0 for p in range(size)]
+        rj = torch.empty(sum(out_splits), dtype=send.dtype, device=send.device)
+        if host:
+            hr = rj.cpu()
+            dist.all_to_all_single(torch.view_as_real(hr), torch.view_as_real(sj.cpu()),
+                                   out_splits, in_splits, group=group)
+            rj.copy_(hr)
+            work = None
+        else:
+            work = dist.all_to_all_single(torch.view_as_real(rj), torch.view_as_real(sj),
+                                          out_splits, in_splits, group=group, async_op=True)
+        if mine:
+            out.append((rj, work))
+        elif work is not None:
+            work.wait()
+    return out
+
+
+def allreduce_real_part(t, group=None):
+    """In-place sum over ranks of a complex tensor whose imaginary part is zero (W_s,
+    fftisdf.py:207 keeps only Re): only the real parts travel (half the bytes)."""
+    import torch
+    re = torch.view_as_real(t)[..., 0]
+    buf = re.contiguous()
+    allreduce_sum(buf, group)
+    re.copy_(buf)
+    return t
 
 
 def _host_staged(group, *tensors):

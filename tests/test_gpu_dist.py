@@ -23,7 +23,7 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("name,world", [("toy222", 2), ("toy331", 3)])
+@pytest.mark.parametrize("name,world", [("toy222", 2), ("toy331", 3), ("toy333_fr", 4)])
 def test_sharded_build_matches_oracle(name, world):
     port = _port()
     with tempfile.TemporaryDirectory() as tmp:

@@ -78,6 +78,19 @@ def test_time_reversal_reps():
         assert covered == set(range(nk))
 
 
+def test_balanced_chunks():
+    from fisdf.kshard import balanced_chunks
+    for costs, size in [([1.0] * 36, 8), ([0.6] * 8 + [1.0] * 28, 8), ([1.0] * 3, 8),
+                        ([0.6, 1.0, 1.0, 0.6, 1.0], 2), ([], 3)]:
+        ch = balanced_chunks(costs, size)
+        assert len(ch) == size
+        assert ch[0][0] == 0 and ch[-1][1] == len(costs)
+        assert all(a <= b for a, b in ch) and all(ch[i][1] == ch[i + 1][0] for i in range(size - 1))
+        if costs:
+            worst = max(sum(costs[a:b]) for a, b in ch)
+            assert worst <= max(max(costs), sum(costs) / size) + max(costs) + 1e-9
+
+
 def test_shard_ranges():
     from fisdf.kshard import shard_range, owner_of
     for nk in (1, 7, 8, 64):
@@ -184,7 +197,32 @@ def _worker_y(rank, size, port, result):
     kshard.allreduce_sum(t, None)
     full = sum(x0[q].conj() @ x0[q].T for q in range(nk))
     err_g = abs(t.numpy() - full).max() / abs(full).max()
-    result.put((rank, err_y, err_g))
+    # chunked exchange of the time-reversal representatives over cost-balanced chunks
+    reps, partner, _ = kshard.time_reversal_reps(kmesh)
+    costs = [0.6 if partner[q] == q else 1.0 for q in reps]
+    chunks = kshard.balanced_chunks(costs, size)
+    counts = [b - a for a, b in chunks]
+    send = torch.from_numpy(np.ascontiguousarray(yb[reps]))
+    pieces = kshard.exchange_y_chunked(send, nip, slices, rank, size, None, counts)
+    a0, a1 = chunks[rank]
+    assert len(pieces) == a1 - a0
+    err_c = 0.0
+    for j, (rj, work) in enumerate(pieces):
+        if work is not None:
+            work.wait()
+        rj = rj.numpy()
+        yq = np.zeros((nip, ngrid), complex)
+        off = 0
+        for (p0, npg) in slices:
+            yq[:, p0:p0 + npg] = rj[off:off + nip * npg].reshape(nip, npg)
+            off += nip * npg
+        err_c = max(err_c, abs(yq - o["y"][reps[a0 + j]].T).max() / abs(o["y"]).max())
+    # real-part all-reduce of W_s-like data (imaginary part zero)
+    w = torch.from_numpy((np.arange(12.0) * (rank + 1)).astype(complex))
+    kshard.allreduce_real_part(w, None)
+    err_r = abs(w.numpy() - np.arange(12.0) * sum(range(1, size + 1))).max()
+    err_g = max(err_g, err_r)
+    result.put((rank, max(err_y, err_c), err_g))
     dist.destroy_process_group()
 
 
