@@ -47,6 +47,9 @@ struct fisdf_ctx {
   double f_tol = 1e-14;
   bool f_check_fail = false, f_used_pivoted = false;
   int force_pivoted = -1;  // fisdf_set_pivoted_fit; -1: environment FISDF_PIVOTED_FIT
+  // extra streams of the fit lanes (fisdf_fit_coulomb_qs)
+  hipStream_t aux[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
   int* f_piv = nullptr;     // (nk, nip)
   int* f_rank_dev = nullptr;
   std::vector<int> f_rank;  // host copy
@@ -256,8 +259,8 @@ bool self_conjugate(const int kmesh[3], int q) {
 }
 
 // cached asym_list of a self-conjugate q (one synchronous count read the first time)
-int get_asym(fisdf_ctx* c, const int mesh[3], const int kmesh[3], const double a[9], int q,
-             const double* wt, const fisdf_ctx::Asym** out) {
+int get_asym(fisdf_ctx* c, hipStream_t st, const int mesh[3], const int kmesh[3],
+             const double a[9], int q, const double* wt, const fisdf_ctx::Asym** out) {
   std::vector<double> key = {(double)mesh[0], (double)mesh[1], (double)mesh[2], (double)kmesh[0],
                              (double)kmesh[1], (double)kmesh[2], (double)q};
   for (int i = 0; i < 9; ++i) key.push_back(a[i]);
@@ -270,13 +273,32 @@ int get_asym(fisdf_ctx* c, const int mesh[3], const int kmesh[3], const double a
     int* cnt = nullptr;
     FISDF_HIP(hipMalloc(&as.idx, sizeof(int) * (ngrid + 1)));
     cnt = as.idx + ngrid;
-    FISDF_TRY(asym_list(c->stream, wt, mesh, m, as.idx, cnt));
-    FISDF_HIP(hipMemcpyAsync(&as.n, cnt, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    FISDF_HIP(hipStreamSynchronize(c->stream));
+    FISDF_TRY(asym_list(st, wt, mesh, m, as.idx, cnt));
+    FISDF_HIP(hipMemcpyAsync(&as.n, cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+    FISDF_HIP(hipStreamSynchronize(st));
     if (getenv("FISDF_VERBOSE")) fprintf(stderr, "fisdf: q %d: %d of %ld G with asymmetric weight\n", q, as.n, ngrid);
     it = c->asym_cache.emplace(key, as).first;
   }
   *out = &it->second;
+  return 0;
+}
+
+int fit_lanes() {
+  static const int n = [] {
+    const char* e = getenv("FISDF_FIT_LANES");
+    const int v = e ? atoi(e) : 2;
+    return std::max(1, std::min(4, v));
+  }();
+  return n;
+}
+
+int ensure_aux(fisdf_ctx* c) {
+  if (c->ev_fork) return 0;
+  FISDF_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+  for (int l = 0; l < 3; ++l) {
+    FISDF_HIP(hipStreamCreateWithFlags(&c->aux[l], hipStreamNonBlocking));
+    FISDF_HIP(hipEventCreateWithFlags(&c->ev_join[l], hipEventDisableTiming));
+  }
   return 0;
 }
 
@@ -371,6 +393,14 @@ int fisdf_destroy(fisdf_ctx* c) {
     (void)hipStreamDestroy(c->side);
     (void)hipEventDestroy(c->ev_x4);
     (void)hipEventDestroy(c->ev_fac);
+  }
+  if (c->ev_fork) {
+    (void)hipEventDestroy(c->ev_fork);
+    for (int l = 0; l < 3; ++l) {
+      (void)hipStreamSynchronize(c->aux[l]);
+      (void)hipStreamDestroy(c->aux[l]);
+      (void)hipEventDestroy(c->ev_join[l]);
+    }
   }
   if (c->arena) (void)hipFree(c->arena);
   if (c->ev_stage) (void)hipEventSynchronize(c->ev_stage), (void)hipEventDestroy(c->ev_stage);
@@ -923,30 +953,50 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   const int ks = pick_ksplit_herk(rmax, (int)ngrid, num_cus(c->device));
   const long rr = (long)rmax * rmax;
   const long sLi = (long)nblk * nb * nb;
+  // q are processed on NL "lanes" (the main stream and aux streams), each with its own
+  // workspaces, so one q's HBM-bound FFT and memory-stalled HERK overlap another q's
+  // MFMA-bound TRSM on the same CUs
+  const int NL = std::min(nq, fit_lanes());
   Carver cv;
-  size_t oY = cv.take(sizeof(cplx) * rmax * ngrid);
-  size_t oU = cv.take(sizeof(cplx) * rmax * ngrid);
-  size_t oWt = cv.take(sizeof(double) * ngrid);
+  size_t oY[4], oU[4], oWt[4], oK[4], oTc[4];
+  for (int l = 0; l < NL; ++l) {
+    oY[l] = cv.take(sizeof(cplx) * rmax * ngrid);
+    oU[l] = cv.take(sizeof(cplx) * rmax * ngrid);
+    oWt[l] = cv.take(sizeof(double) * ngrid);
+    oK[l] = cv.take(sizeof(cplx) * (size_t)ks * rmax * rmax);
+    oTc[l] = cv.take(sizeof(cplx) * rr);
+  }
   size_t oG = cv.take(sizeof(cplx) * nq * rr);
   size_t oT = cv.take(sizeof(cplx) * nq * rr);
   size_t oS = cv.take(sizeof(cplx) * nq * rr);
-  size_t oK = cv.take(sizeof(cplx) * (size_t)ks * rmax * rmax);
   void* base;
   FISDF_TRY(arena_get(c, cv.off, &base));
   char* b = (char*)base;
-  cplx* Yh = (cplx*)(b + oY);
-  cplx* U = (cplx*)(b + oU);
-  double* wt = (double*)(b + oWt);
   cplx* G = (cplx*)(b + oG);   // (nq, rmax, rmax): G_q in the leading r_q x r_q block, zero elsewhere
   cplx* T = (cplx*)(b + oT);
   cplx* S = (cplx*)(b + oS);
-  cplx* kw = (cplx*)(b + oK);
   if (rmax == 0) {
     FISDF_HIP(hipMemsetAsync(Wq, 0, sizeof(cplx) * nq * nn, c->stream));
     return 0;
   }
   FISDF_HIP(hipMemsetAsync(G, 0, sizeof(cplx) * nq * rr, c->stream));
+  hipStream_t lane_st[4] = {c->stream, nullptr, nullptr, nullptr};
+  if (NL > 1) {
+    FISDF_TRY(ensure_aux(c));
+    FISDF_HIP(hipEventRecord(c->ev_fork, c->stream));
+    for (int l = 1; l < NL; ++l) {
+      lane_st[l] = c->aux[l - 1];
+      FISDF_HIP(hipStreamWaitEvent(lane_st[l], c->ev_fork, 0));
+    }
+  }
   for (int lq = 0; lq < nq; ++lq) {
+    const int ln = lq % NL;
+    hipStream_t st = lane_st[ln];
+    cplx* Yh = (cplx*)(b + oY[ln]);
+    cplx* U = (cplx*)(b + oU[ln]);
+    double* wt = (double*)(b + oWt[ln]);
+    cplx* kw = (cplx*)(b + oK[ln]);
+    cplx* Tc = (cplx*)(b + oTc[ln]);
     const int q = h_qs[lq];
     const int sl = s0 + lq;  // factor slot
     const int r = c->f_rank[sl];
@@ -959,47 +1009,51 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     kpoint(kmesh, g, q, kq);
     for (int i = 0; i < 3; ++i) kd[i] = g.a[i][0] * kq[0] + g.a[i][1] * kq[1] + g.a[i][2] * kq[2];
     {
-      StageTimer tm(c, FISDF_ST_FFT);
+      StageTimer tm(c, FISDF_ST_FFT, st);
       // sqrt(coulG(k_q+G) vol/N^2)  (:114-115 and the Parseval 1/N of :118)
-      FISDF_TRY(coulg_weight(c->stream, mesh, g, kq, vol / ((double)ngrid * ngrid), 1, wt));
+      FISDF_TRY(coulg_weight(st, mesh, g, kq, vol / ((double)ngrid * ngrid), 1, wt));
       // Yh = FFT(y_q[:, piv] * f_q) * w   (:99, :113; rows in pivot order)
-      FISDF_TRY(fft3d(c->stream, yT + (long)lq * nip * ngrid, ngrid, piv, Yh, ngrid, r, mesh[0],
+      FISDF_TRY(fft3d(st, yT + (long)lq * nip * ngrid, ngrid, piv, Yh, ngrid, r, mesh[0],
                       mesh[1], mesh[2], kd, wt, nullptr));
     }
     cplx* Uq = U;  // where L^{-1} Yh lands
     {
-      StageTimer tm(c, FISDF_ST_TRSM);
+      StageTimer tm(c, FISDF_ST_TRSM, st);
       // U = L^{-1} Yh   (fit, factored order; (x4_q)_PP = L L^H)
       if (r == nip) {  // merged block-row substitution, in place
-        FISDF_TRY(trsm_merged(c->stream, c->f_Q + (long)sl * nn, nip, Yh, ngrid, (int)ngrid,
+        FISDF_TRY(trsm_merged(st, c->f_Q + (long)sl * nn, nip, Yh, ngrid, (int)ngrid,
                               real_q ? GEMM_A_REAL : GEMM_FULL));
         Uq = Yh;
       } else {
-        FISDF_TRY(trsm_blocked(c->stream, 1, Lp, nip, 0, r, Linv, 0, nb, Yh, ngrid, 0, U, ngrid,
+        FISDF_TRY(trsm_blocked(st, 1, Lp, nip, 0, r, Linv, 0, nb, Yh, ngrid, 0, U, ngrid,
                                0, (int)ngrid, 1, real_q ? 1 : 0));
       }
     }
     cplx* scratch = Uq == U ? Yh : U;
     {
-      StageTimer tm(c, FISDF_ST_HERK);
+      StageTimer tm(c, FISDF_ST_HERK, st);
       // G = U U^H  (:121 by Parseval)
-      FISDF_TRY(herk(c->stream, r, (int)ngrid, 1.0, Uq, ngrid, G + lq * rr, rmax, ks, kw,
+      FISDF_TRY(herk(st, r, (int)ngrid, 1.0, Uq, ngrid, G + lq * rr, rmax, ks, kw,
                      real_q ? GEMM_RE_ONLY : GEMM_FULL));
     }
     if (real_q) {
-      StageTimer tm(c, FISDF_ST_SMALL);
+      StageTimer tm(c, FISDF_ST_SMALL, st);
       {
         // Im(G) = Im(sum over the weight-asymmetric G only): every other (G, G') pair cancels
         const fisdf_ctx::Asym* as = nullptr;
-        FISDF_TRY(get_asym(c, mesh, kmesh, a, q, wt, &as));
+        FISDF_TRY(get_asym(c, st, mesh, kmesh, a, q, wt, &as));
         if (as->n > 0) {
-          FISDF_TRY(gather_cols(c->stream, Uq, ngrid, r, as->idx, as->n, scratch));
-          FISDF_TRY(herk(c->stream, r, as->n, 1.0, scratch, as->n, T, rmax,
+          FISDF_TRY(gather_cols(st, Uq, ngrid, r, as->idx, as->n, scratch));
+          FISDF_TRY(herk(st, r, as->n, 1.0, scratch, as->n, Tc, rmax,
                          std::min(ks, std::max(1, as->n / 256)), kw));
-          FISDF_TRY(add_imag(c->stream, G + lq * rr, rmax, T, rmax, r));
+          FISDF_TRY(add_imag(st, G + lq * rr, rmax, Tc, rmax, r));
         }
       }
     }
+  }
+  for (int l = 1; l < NL; ++l) {  // join the lanes before the batched small stage
+    FISDF_HIP(hipEventRecord(c->ev_join[l - 1], lane_st[l]));
+    FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_join[l - 1], 0));
   }
   {
     StageTimer tm(c, FISDF_ST_SMALL);

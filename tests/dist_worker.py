@@ -31,7 +31,19 @@ def main():
     df._ao_grid = d.to_dev(chi)
     df.build()
     vj, vk = df.get_jk(dm)
-    np.savez(out, vj=vj, vk=vk, perm=df.perm, ranks=df.ranks, vj0=o["vj"], vk0=o["vk"],
+    vj0, vk0 = o["vj"], o["vk"]
+    if not np.array_equal(df.perm, o["perm"]):
+        # the sharded Gram sums in another order than dpstrf's input: a near-tie may pick an
+        # equally valid different point set; the reference value is then the oracle's build
+        # on THAT point set (the selection itself is checked against dpstrf elsewhere)
+        from oracle import isdf_ref as R
+        xip = x0[:, df.perm]
+        ob = R.build(xip, chi, coords, cell.a, kmesh, cell.mesh)
+        kpts = R.get_kpts(cell.a, kmesh)
+        phase = R.get_phase(cell.a, kpts, kmesh)
+        vj0 = R.get_j_kpts(xip, ob["w0"], dm, kpts_band_is_zero=bool(abs(kpts).max() < 1e-9))
+        vk0 = R.get_k_kpts(xip, ob["wq"], dm, phase)
+    np.savez(out, vj=vj, vk=vk, perm=df.perm, ranks=df.ranks, vj0=vj0, vk0=vk0,
              perm0=o["perm"])
     torch.cuda.synchronize()
     dist.destroy_process_group()

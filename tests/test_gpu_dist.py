@@ -42,9 +42,9 @@ def test_sharded_build_matches_oracle(name, world):
         ek = abs(o["vk"] - o["vk0"]).max()
         same = np.array_equal(o["perm"], o["perm0"])
         print(f"{name} rank {r}/{world}: |dJ|={ej:.2e} |dK|={ek:.2e} pivots==dpstrf: {same}")
-        # with dpstrf's pivots the bar is the north-star 1e-8; a tie flipped by the sharded
-        # Gram's summation order changes the (equally valid) point set: ISDF-error level
-        tol = 1e-8 if same else 1e-7
+        # vs the oracle on the same point set (dist_worker.py); toy331 is rank-deficient with
+        # time reversal (1.5e-8 bar, test_gpu_isdf.py)
+        tol = 1.5e-8 if name == "toy331" else 1e-8
         assert ej < tol and ek < tol
         # every rank returns the same J/K and the same pivots
         assert abs(o["vj"] - outs[0]["vj"]).max() == 0.0
