@@ -193,6 +193,22 @@ def main():
             "frac": round(achieved / PEAK_FP64_TFLOPS, 4), "traffic": None,
             "flop_per_launch": flop_step / max(len(ranks), 1),
             "avg_launch_ms": herk_ms / max(herk_calls, 1), "launches": int(herk_calls)}
+    # in the timed region the fit lanes share the CUs, so the per-launch HERK durations above
+    # include contention with the other lanes' TRSM/FFT; one extra untimed step with a single
+    # lane gives the kernel's own rate
+    d.ctx.call("fisdf_set_fit_lanes", 1)
+    d.ctx.call("fisdf_set_timing", 1)
+    d.ctx.timings()
+    step()
+    torch.cuda.synchronize()
+    iso_ms, iso_calls = d.ctx.timings()["herk"]
+    d.ctx.call("fisdf_set_timing", 0)
+    d.ctx.call("fisdf_set_fit_lanes", 0)
+    if iso_ms > 0:
+        iso = flop_step / (iso_ms * 1e-3) / 1e12
+        roof["isolated"] = {"achieved": round(iso, 3), "frac": round(iso / PEAK_FP64_TFLOPS, 4),
+                            "avg_launch_ms": iso_ms / max(iso_calls, 1),
+                            "note": "one untimed step after the timed region, 1 fit lane"}
     tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tfile):
         t = json.load(open(tfile))

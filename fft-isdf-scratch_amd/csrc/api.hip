@@ -47,6 +47,7 @@ struct fisdf_ctx {
   double f_tol = 1e-14;
   bool f_check_fail = false, f_used_pivoted = false;
   int force_pivoted = -1;  // fisdf_set_pivoted_fit; -1: environment FISDF_PIVOTED_FIT
+  int lanes = 0;           // fisdf_set_fit_lanes; 0: environment FISDF_FIT_LANES / default
   // extra streams of the fit lanes (fisdf_fit_coulomb_qs)
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
@@ -283,10 +284,10 @@ int get_asym(fisdf_ctx* c, hipStream_t st, const int mesh[3], const int kmesh[3]
   return 0;
 }
 
-int fit_lanes() {
+int env_fit_lanes() {
   static const int n = [] {
     const char* e = getenv("FISDF_FIT_LANES");
-    const int v = e ? atoi(e) : 2;
+    const int v = e ? atoi(e) : 3;
     return std::max(1, std::min(4, v));
   }();
   return n;
@@ -882,6 +883,12 @@ int fisdf_set_pivoted_fit(fisdf_ctx* c, int mode) {
   return 0;
 }
 
+int fisdf_set_fit_lanes(fisdf_ctx* c, int lanes) {
+  FISDF_CHECK(c != nullptr && lanes >= 0 && lanes <= 4, "set_fit_lanes: lanes must be 0..4");
+  c->lanes = lanes;
+  return 0;
+}
+
 int fisdf_factor_info(fisdf_ctx* c, int* h_used_pivoted) {
   FISDF_CHECK(c != nullptr, "null context");
   if (h_used_pivoted) *h_used_pivoted = c->f_used_pivoted ? 1 : 0;
@@ -950,13 +957,17 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   cplx* Wq = (cplx*)Wqv;
   int rmax = 0;
   for (int lq = 0; lq < nq; ++lq) rmax = std::max(rmax, c->f_rank[s0 + lq]);
-  const int ks = pick_ksplit_herk(rmax, (int)ngrid, num_cus(c->device));
+  static const int ks_env = [] {
+    const char* e = getenv("FISDF_HERK_KS");
+    return e ? atoi(e) : 0;
+  }();
+  const int ks = ks_env > 0 ? ks_env : pick_ksplit_herk(rmax, (int)ngrid, num_cus(c->device));
   const long rr = (long)rmax * rmax;
   const long sLi = (long)nblk * nb * nb;
   // q are processed on NL "lanes" (the main stream and aux streams), each with its own
   // workspaces, so one q's HBM-bound FFT and memory-stalled HERK overlap another q's
   // MFMA-bound TRSM on the same CUs
-  const int NL = std::min(nq, fit_lanes());
+  const int NL = std::min(nq, c->lanes > 0 ? c->lanes : env_fit_lanes());
   Carver cv;
   size_t oY[4], oU[4], oWt[4], oK[4], oTc[4];
   for (int l = 0; l < NL; ++l) {

@@ -149,6 +149,11 @@ int fisdf_fit_coulomb(fisdf_ctx* ctx, int q0, int q1, const void* d_yT, int nip,
  * callers may fit only one q of each (q, -q) pair and weight it 2 in fisdf_build_ws_qs. */
 int fisdf_fit_coulomb_qs(fisdf_ctx* ctx, const int* h_qs, int nq, const void* d_yT, int nip,
                          const int mesh[3], const int kmesh[3], const double a[9], void* d_Wq);
+/* Fit lanes: the q of one fisdf_fit_coulomb_qs call are spread round-robin over `lanes`
+ * streams with private workspaces (one q's memory-bound FFT/HERK overlaps another's
+ * MFMA-bound TRSM); 0 (default): FISDF_FIT_LANES from the environment, else 3.  Results do
+ * not depend on it (same kernels, same per-q arithmetic). */
+int fisdf_set_fit_lanes(fisdf_ctx* ctx, int lanes);
 
 /* ---- A8 prep: W_s[R] = sqrt(nk) Re(sum_{q in [q0,q1)} Phi[R,q] W_q) (fftisdf.py:204-207)
  * d_Wq: (q1-q0, nip, nip) shard; d_Ws: (nimg, nip, nip) c128 with zero imaginary part
