@@ -44,9 +44,12 @@ int square_scale(hipStream_t s, const cplx* in, double sc, cplx* out, long n);
 int permute_kgm(hipStream_t s, const cplx* x0, int nq, int ng, int nao, cplx* out);
 int pair_product(hipStream_t s, const cplx* A, int n1, const cplx* B, int n2, int nip, cplx* P);
 // y_q = Phi^T (Re(Phi FX))^2 for the ascending q-list (h_qs on the host; d_qs a device copy,
-// needed only when the k-mesh has more than 64 points), written to yT[slot][I][goff + g]
+// needed only when the k-mesh has more than 64 points), written to yT[slot][I][goff + g].
+// half: FX holds only the first kmesh_half_count(kmesh) k (planes a <= n0/2); the others are
+// conj(FX[-k]) (time reversal)
+int kmesh_half_count(const int kmesh[3]);
 int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const int* h_qs,
-            const int* d_qs, int nq, int m, cplx* yT, long qs, long Is, long goff,
+            const int* d_qs, int nq, int m, cplx* yT, long qs, long Is, long goff, bool half,
             unsigned long long* mon);
 
 }  // namespace fisdf

@@ -271,10 +271,16 @@ __device__ void kmesh_axis_dft(cplx* T, int CT, int ld, int nk, int na, int stri
   }
 }
 
+// index of -k on the k-mesh (k = (a*n1 + b)*n2 + c, ascending cartesian order)
+__host__ __device__ inline int kmesh_partner(int k, int n0, int n1, int n2) {
+  const int c = k % n2, b = (k / n2) % n1, a = k / (n1 * n2);
+  return (((n0 - a) % n0) * n1 + (n1 - b) % n1) * n2 + (n2 - c) % n2;
+}
+
 __global__ __launch_bounds__(256) void kmesh_y_kernel(
     const cplx* __restrict__ FX, long ncol, int nk, int n0, int n1, int n2,
     const int* __restrict__ qlist, int nq, int m, cplx* __restrict__ yT, long qs, long Is,
-    long goff, int CT,
+    long goff, int CT, int nks,
     unsigned long long* __restrict__ mon) {
   extern __shared__ cplx sm[];
   cplx* w0 = sm;
@@ -304,11 +310,15 @@ __global__ __launch_bounds__(256) void kmesh_y_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = e0 + u * nthr + tid;
-      const int k = e / CT, c = e % CT;
+      int k = e / CT;
+      const int c = e % CT;
       const long col = c0 + c;
       const bool ok = e < tot && col < ncol;
+      const bool mirror = k >= nks;  // time reversal: fx_{-k} = conj(fx_k), only k < nks stored
+      if (mirror) k = kmesh_partner(k, n0, n1, n2);
       v[u] = FX[ok ? (long)k * ncol + col : 0];
       if (!ok) v[u] = cmk(0, 0);
+      if (mirror) v[u] = cconj(v[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -394,7 +404,7 @@ __device__ __forceinline__ void reg_axis_dft(cplx* v, const cplx* tw) {
     }
 }
 
-template <int N0, int N1, int N2>
+template <int N0, int N1, int N2, bool HALF>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void kmesh_y_reg_kernel(
     const cplx* __restrict__ FX, int ncol, unsigned long long qmask, int m, cplx* __restrict__ yT,
     long qs, long Is, long goff, unsigned long long* __restrict__ mon) {
@@ -410,8 +420,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   double mi = 0.0;
   for (int col = blockIdx.x * blockDim.x + threadIdx.x; col < ncol; col += gridDim.x * blockDim.x) {
     cplx v[NK];
+    // HALF: only the k-planes a <= N0/2 are stored; fx_{-k} = conj(fx_k) (time reversal)
+    constexpr int NKS = HALF ? (N0 / 2 + 1) * N1 * N2 : NK;
 #pragma unroll
-    for (int k = 0; k < NK; ++k) v[k] = FX[(long)k * ncol + col];
+    for (int k = 0; k < NKS; ++k) v[k] = FX[(long)k * ncol + col];
+#pragma unroll
+    for (int k = NKS; k < NK; ++k) v[k] = cconj(v[kmesh_partner(k, N0, N1, N2)]);
     // fx_s = Phi fx_k (fftisdf.py:79)
     reg_axis_dft<N0, N1 * N2, NK>(v, tw0);
     reg_axis_dft<N1, N2, NK>(v, tw1);
@@ -780,10 +794,13 @@ int scale_rows(hipStream_t s, const cplx* X, const cplx* v, int nset, int nk, in
   return 0;
 }
 
+int kmesh_half_count(const int kmesh[3]) { return (kmesh[0] / 2 + 1) * kmesh[1] * kmesh[2]; }
+
 int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const int* h_qs,
             const int* d_qs, int nq, int m, cplx* yT, long qs, long Is, long goff,
-            unsigned long long* mon) {
+            bool half, unsigned long long* mon) {
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  const int nks = half ? kmesh_half_count(kmesh) : nk;
   for (int i = 0; i < nq; ++i)
     FISDF_CHECK(h_qs[i] >= 0 && h_qs[i] < nk && (i == 0 || h_qs[i] > h_qs[i - 1]),
                 "kmesh_y: q-list must be ascending and inside the k-mesh");
@@ -796,8 +813,12 @@ int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const 
     const unsigned grid = (unsigned)std::max<long>(1, std::min<long>((ncol + 63) / 64, 32768));
 #define FISDF_KM(a, b, c)                                                                      \
   if (kmesh[0] == a && kmesh[1] == b && kmesh[2] == c) {                                       \
-    hipLaunchKernelGGL((kmesh_y_reg_kernel<a, b, c>), dim3(grid), dim3(64), 0, s, FX, nc,       \
-                       qmask, m, yT, qs, Is, goff, mon);                                       \
+    if (half)                                                                                  \
+      hipLaunchKernelGGL((kmesh_y_reg_kernel<a, b, c, true>), dim3(grid), dim3(64), 0, s, FX,   \
+                         nc, qmask, m, yT, qs, Is, goff, mon);                                 \
+    else                                                                                       \
+      hipLaunchKernelGGL((kmesh_y_reg_kernel<a, b, c, false>), dim3(grid), dim3(64), 0, s, FX,  \
+                         nc, qmask, m, yT, qs, Is, goff, mon);                                 \
     FISDF_HIP(hipGetLastError());                                                              \
     return 0;                                                                                  \
   }
@@ -815,7 +836,7 @@ int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const 
   if (tiles == 0) return 0;
   const unsigned grid = (unsigned)std::min<long>(tiles, 4096);
   hipLaunchKernelGGL(kmesh_y_kernel, dim3(grid), dim3(256), lds, s, FX, ncol, nk,
-                     kmesh[0], kmesh[1], kmesh[2], d_qs, nq, m, yT, qs, Is, goff, CT, mon);
+                     kmesh[0], kmesh[1], kmesh[2], d_qs, nq, m, yT, qs, Is, goff, CT, nks, mon);
   FISDF_HIP(hipGetLastError());
   return 0;
 }

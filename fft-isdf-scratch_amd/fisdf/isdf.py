@@ -402,6 +402,8 @@ def build(df_obj):
     if nq:
         d.ctx.call("fisdf_factor_x4_async", _lib.ptr(x4), qs_c, nq, nip, float(df_obj.fit_tol),
                    km_p if df_obj.real_self_conjugate else None)
+    # fx_{-k} = conj(fx_k) for real AOs: fx_k computed for half the k-mesh (:76)
+    d.ctx.call("fisdf_set_time_reversal", 1 if df_obj.time_reversal else 0)
     yT = d.empty((nq, nip, ngrid))
     if d.size == 1:
         d.ctx.call("fisdf_build_y_qs", _lib.ptr(f), ngrid * nao, 0, ngrid, ngrid, _lib.ptr(X),

@@ -154,6 +154,10 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* ctx, const int* h_qs, int nq, const void* d_
  * MFMA-bound TRSM); 0 (default): FISDF_FIT_LANES from the environment, else 3.  Results do
  * not depend on it (same kernels, same per-q arithmetic). */
 int fisdf_set_fit_lanes(fisdf_ctx* ctx, int lanes);
+/* Time reversal of the inputs (real AOs, k-mesh closed under k -> -k): f_{-k} = conj(f_k)
+ * and x_{-k} = conj(x_k), so fx_{-k} = conj(fx_k) (fftisdf.py:76) and fisdf_build_y(_qs)
+ * computes fx_k only for the k-planes a <= kmesh[0]/2.  Default 0 (every k computed). */
+int fisdf_set_time_reversal(fisdf_ctx* ctx, int on);
 
 /* ---- A8 prep: W_s[R] = sqrt(nk) Re(sum_{q in [q0,q1)} Phi[R,q] W_q) (fftisdf.py:204-207)
  * d_Wq: (q1-q0, nip, nip) shard; d_Ws: (nimg, nip, nip) c128 with zero imaginary part

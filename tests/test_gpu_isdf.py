@@ -150,7 +150,7 @@ def test_build_y_qlist():
         assert abs(o["y"][part[q]] - o["y"][q].conj()).max() < 1e-12 * abs(o["y"]).max()
 
 
-@pytest.mark.parametrize("name", ["toy222", "toy331"])
+@pytest.mark.parametrize("name", ["toy222", "toy331", "toy333_fr"])
 def test_x4_and_y_parity(name):
     df, o, dm = make_df(name)
     df.build()
@@ -165,15 +165,20 @@ def test_x4_and_y_parity(name):
     yT = d.empty((nk, nip, ngrid))
     km, kmp = L.iarr(kmesh)
     a, ap = L.darr(cell.a.ravel())
-    # two blocks to exercise the g0 offset
+    # two blocks to exercise the g0 offset; every k computed, then fx_k for half the k-mesh
+    # with fx_{-k} = conj(fx_k) (fisdf_set_time_reversal)
     h = ngrid // 2
-    for g0, g1 in ((0, h), (h, ngrid)):
-        d.ctx.call("fisdf_build_y", L._vp(df._ao_grid.data_ptr() + g0 * nao * 16),
-                   ngrid * nao, g0, g1 - g0, ngrid,
-                   L.ptr(df._dev_state["X"]), nip, nao, kmp, ap, 0, nk, L.ptr(yT))
-    y = yT.cpu().numpy().transpose(0, 2, 1)
-    rel = abs(y - o["y"]).max() / abs(o["y"]).max()
-    assert rel < 1e-12
+    for tr in (0, 1):
+        d.ctx.call("fisdf_set_time_reversal", tr)
+        yT.zero_()
+        for g0, g1 in ((0, h), (h, ngrid)):
+            d.ctx.call("fisdf_build_y", L._vp(df._ao_grid.data_ptr() + g0 * nao * 16),
+                       ngrid * nao, g0, g1 - g0, ngrid,
+                       L.ptr(df._dev_state["X"]), nip, nao, kmp, ap, 0, nk, L.ptr(yT))
+        y = yT.cpu().numpy().transpose(0, 2, 1)
+        rel = abs(y - o["y"]).max() / abs(o["y"]).max()
+        print(f"{name} time_reversal={tr}: max rel |y - y_oracle| = {rel:.2e}")
+        assert rel < 1e-12
 
 
 @pytest.mark.parametrize("name", ["toy222", "diamond_szv_gamma"])
