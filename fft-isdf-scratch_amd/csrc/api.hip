@@ -246,7 +246,8 @@ int select_gram(fisdf_ctx* c, const cplx* x0, int nk, int q0, int q1, int ng0, i
   while (tiles * ks < 512 && K / (ks * 2) >= 256) ks *= 2;
   cplx* work = nullptr;
   if (ks > 1) FISDF_HIP(hipMallocAsync((void**)&work, sizeof(cplx) * (size_t)ks * ng0 * ng0, c->stream));
-  FISDF_TRY(herk(c->stream, ng0, K, 1.0, tmp, K, x2, ng0, ks, work));
+  // only Re(x2) enters the selection (fftisdf.py:379): real-part HERK, imaginary part zero
+  FISDF_TRY(herk(c->stream, ng0, K, 1.0, tmp, K, x2, ng0, ks, work, GEMM_RE_ONLY));
   if (work) FISDF_HIP(hipFreeAsync(work, c->stream));
   (void)nk;
   return 0;

@@ -13,6 +13,8 @@
 // (one wave per row, dot product over the j previous columns with a wave reduction),
 // updates the residual diagonal d, then a per-matrix arg-max picks pivot j+1
 // (first index on ties, as LAPACK's MAXLOC).  Chosen rows are marked d = -1.
+#include <cstdio>
+
 #include "common.h"
 
 namespace fisdf {
@@ -381,12 +383,13 @@ __global__ __launch_bounds__(PR_THREADS) void pchol_real_panel(const double* __r
 #pragma unroll
         for (int c = 0; c < NB; ++c) s_lp[c] = lp[r][c];
       }
-    // row p of the trailing matrix (= column p), one coalesced read per row owned
+    // column p of the trailing matrix from its lower triangle (the only part the rank-NB
+    // updates keep current): row p for i < p (coalesced), column p below the diagonal
     double wrow[RPT];
 #pragma unroll
     for (int r = 0; r < RPT; ++r) {
       const int i = tid + PR_THREADS * r;
-      wrow[r] = i < n ? W[(long)p * n + i] : 0.0;
+      wrow[r] = i < n ? W[i < p ? (long)p * n + i : (long)i * n + p] : 0.0;
     }
     __syncthreads();
     const double sq = sqrt(dp), inv = 1.0 / sq;
@@ -424,15 +427,21 @@ __global__ __launch_bounds__(PR_THREADS) void pchol_real_panel(const double* __r
   }
 }
 
-// W -= Lpan Lpan^T over the full n x n matrix (64 x 64 tile per 256-thread workgroup, 4 x 4
-// elements per thread, the two NB-wide panel slices in LDS)
+// W -= Lpan Lpan^T on the lower triangle of tiles (64 x 64 tile per 256-thread workgroup,
+// 4 x 4 elements per thread, the two NB-wide panel slices in LDS); 1-D grid over the
+// T(T+1)/2 tiles with row >= column
 template <int NB>
 __global__ __launch_bounds__(256) void syrk_real_update(double* __restrict__ W, int n,
                                                         const double* __restrict__ Lpan,
                                                         const int* __restrict__ flags) {
   if (flags[0]) return;
   __shared__ double Li[64][NB + 1], Lj[64][NB + 1];
-  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  const int t = blockIdx.x;
+  int bi = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+  while (bi * (bi + 1) / 2 > t) --bi;
+  const int bj = t - bi * (bi + 1) / 2;
+  const int i0 = bi * 64, j0 = bj * 64;
   const int tid = threadIdx.x;
   for (int e = tid; e < 64 * NB; e += 256) {
     const int r = e / NB, c = e % NB;
@@ -457,6 +466,189 @@ __global__ __launch_bounds__(256) void syrk_real_update(double* __restrict__ W, 
       const int j = j0 + tj + b;
       if (j < n) W[(long)i * n + j] -= acc[a][b];
     }
+  }
+}
+
+// ---- cooperative left-looking variant (default for the selection) ----------------------
+// One pivot per step over a co-resident grid (hipLaunchCooperativeKernel): workgroup w owns
+// rows [w*RW, w*RW+RW) with their L rows in LDS (and a copy in the row-major global L) and
+// their residual diagonal.  Step j:
+//   post: the local arg-max of the residual diagonal as one 16-byte record {value, row, step}
+//     (a single agent-coherent dwordx4 store);
+//   poll: thread g waits for workgroup g's record of step j; block arg-max (larger value,
+//     then smaller row: LAPACK's first index on ties) -> pivot p, d_p;
+//   gather: L[p, :j] from the global L and x4[p, owned rows] = Re(x2[p, rows])^2 * scale;
+//   column: L[rows, j] = (x4[rows, p] - L[rows, :j] L[p, :j]^T) / sqrt(d_p), 8 threads per row;
+//     d -= L^2; the new entries go to LDS and to the global L (completed before the next post,
+//     so a reader that sees step j+1's record sees row p's entries up to j).
+// No trailing matrix is formed or updated.  Exchange traffic uses agent-coherent (sc1) loads
+// and stores (no per-step L2 write-back/invalidate).  Records are double-buffered by step
+// parity (a workgroup runs at most one step ahead).  Every wait is bounded: a stalled step
+// sets *err and every workgroup exits (the caller then falls back to the blocked path).
+constexpr int SC_THREADS = 256;
+constexpr int SC_MAXRW = SC_THREADS / 8;  // 8 threads per owned row
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void sc_store_rec(u32x4* addr, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(addr), "v"(v) : "memory");
+}
+__device__ __forceinline__ u32x4 sc_load_rec(const u32x4* addr) {
+  u32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)"
+               : "=v"(r)
+               : "v"(addr)
+               : "memory");
+  return r;
+}
+__device__ __forceinline__ bool sc_better(double v2, int i2, double v, int i) {
+  return v2 > v || (v2 == v && i2 < i);
+}
+
+__global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
+    const cplx* __restrict__ X2, double scale, int n, int rmax, double tol, int RW,
+    int* __restrict__ piv, int* __restrict__ rank, u32x4* __restrict__ rec,
+    double* __restrict__ Lg, int* __restrict__ err) {
+  extern __shared__ double sm[];
+  double* Lr = sm;                    // RW x rmax, row-major
+  double* Lp = Lr + (long)RW * rmax;  // pivot row L[p, :j]
+  double* dd = Lp + rmax;             // residual diagonal of the owned rows
+  double* w0 = dd + RW;               // x4[p, owned rows]
+  __shared__ double s_v[SC_THREADS / 64];
+  __shared__ int s_i[SC_THREADS / 64];
+  __shared__ int s_p, s_stop;
+  __shared__ double s_dp, s_thr;
+  const int G = gridDim.x, w = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r0 = w * RW, nr = max(0, min(RW, n - r0));
+  if (tid < RW) {
+    double v = -1e300;
+    if (tid < nr) {
+      const double x = X2[(long)(r0 + tid) * n + r0 + tid].x;
+      v = x * x * scale;
+    }
+    dd[tid] = v;
+  }
+  if (tid == 0) s_stop = 0;
+  __syncthreads();
+  for (int j = 0;; ++j) {
+    // ---- post ----
+    if (wid == 0) {
+      double v = lane < nr ? dd[lane] : -1e300;
+      int i = lane < nr ? r0 + lane : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double v2 = __shfl_xor(v, o, 64);
+        const int i2 = __shfl_xor(i, o, 64);
+        if (sc_better(v2, i2, v, i)) { v = v2; i = i2; }
+      }
+      if (lane == 0) {
+        const unsigned long long vb = (unsigned long long)__double_as_longlong(v);
+        u32x4 r;
+        r.x = (unsigned)vb;
+        r.y = (unsigned)(vb >> 32);
+        r.z = (unsigned)i;
+        r.w = (unsigned)(j + 1);
+        sc_store_rec(rec + (j & 1) * G + w, r);
+      }
+    }
+    // ---- poll ----
+    {
+      double v = -1e300;
+      int i = 0x7fffffff;
+      bool bad = false;
+      for (int g = tid; g < G; g += SC_THREADS) {
+        u32x4 r;
+        long spins = 0;
+        for (;;) {
+          r = sc_load_rec(rec + (j & 1) * G + g);
+          if (r.w == (unsigned)(j + 1)) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1L << 22) ||
+              ((spins & 1023) == 0 &&
+               __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            bad = true;
+            break;
+          }
+        }
+        if (bad) break;
+        const double v2 =
+            __longlong_as_double((long long)(((unsigned long long)r.y << 32) | r.x));
+        const int i2 = (int)r.z;
+        if (sc_better(v2, i2, v, i)) { v = v2; i = i2; }
+      }
+      if (bad) {
+        atomicExch(err, 1);
+        s_stop = 1;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double v2 = __shfl_xor(v, o, 64);
+        const int i2 = __shfl_xor(i, o, 64);
+        if (sc_better(v2, i2, v, i)) { v = v2; i = i2; }
+      }
+      if (lane == 0) { s_v[wid] = v; s_i[wid] = i; }
+      __syncthreads();
+      if (s_stop) return;
+      if (tid == 0) {
+        for (int q = 1; q < SC_THREADS / 64; ++q)
+          if (sc_better(s_v[q], s_i[q], v, i)) { v = s_v[q]; i = s_i[q]; }
+        if (j == 0) s_thr = tol > 0 ? tol * v : (double)n * 2.220446049250313e-16 * v;
+        const bool stop = !(v > s_thr) || i == 0x7fffffff;
+        s_stop = stop;
+        s_p = i;
+        s_dp = v;
+        if (w == 0) {
+          if (!stop) piv[j] = i;
+          if (stop || j + 1 >= rmax) rank[0] = stop ? j : j + 1;
+        }
+      }
+      __syncthreads();
+      if (s_stop) return;
+    }
+    const int p = s_p;
+    const double dp = s_dp;
+    // ---- gather ----
+    for (int c = tid; c < j; c += SC_THREADS)
+      Lp[c] = __hip_atomic_load(&Lg[(long)p * rmax + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int r = tid; r < nr; r += SC_THREADS) {
+      const double x = X2[(long)p * n + r0 + r].x;
+      w0[r] = x * x * scale;
+    }
+    __syncthreads();
+    // ---- column j ----
+    {
+      const double sq = sqrt(dp), inv = 1.0 / sq;
+      const int r = tid >> 3, part = tid & 7;
+      if (r < nr) {
+        const double* lr = Lr + (long)r * rmax;
+        double a0 = 0.0, a1 = 0.0;
+        int c = part;
+        for (; c + 8 < j; c += 16) {
+          a0 += lr[c] * Lp[c];
+          a1 += lr[c + 8] * Lp[c + 8];
+        }
+        if (c < j) a0 += lr[c] * Lp[c];
+        double acc = a0 + a1;
+        acc += __shfl_xor(acc, 1, 64);
+        acc += __shfl_xor(acc, 2, 64);
+        acc += __shfl_xor(acc, 4, 64);
+        if (part == 0) {
+          const int i = r0 + r;
+          double l = 0.0;
+          if (i == p) {
+            l = sq;
+            dd[r] = -1e300;
+          } else if (dd[r] > -1e299) {
+            l = (w0[r] - acc) * inv;
+            dd[r] -= l * l;
+          }
+          Lr[(long)r * rmax + j] = l;
+          __hip_atomic_store(&Lg[(long)i * rmax + j], l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+    }
+    __syncthreads();
+    if (j + 1 >= rmax) return;
   }
 }
 
@@ -638,10 +830,77 @@ int chol_unpivoted(hipStream_t s, cplx* W, int n, int batch, double tol_rel, int
 // selection: pivots of the real Gram x4 = Re(X2)^2 * scale (n x n, X2 complex); piv/rank
 // device; work = W (n*n doubles) + L panel (n*16) + d (n) + thr; flags (1 int).  Returns 1 in
 // *handled when n fits the register panel (n <= 4096), else 0 (caller uses pchol).
+// FISDF_SEL_COOP=0 selects the blocked single-CU path (read per call: tests compare the two)
+bool select_coop_enabled() {
+  const char* e = getenv("FISDF_SEL_COOP");
+  return !(e && e[0] == '0');
+}
+
+// launches pchol_select_coop when the owned L rows fit the LDS of a co-resident grid;
+// *handled = false (nothing enqueued that matters) otherwise or if the launch is refused.
+// The cooperative launch synchronises the stream to read the barrier error flag.
+int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n, int rmax,
+                             double tol, int* piv, int* rank, double* work, bool* handled) {
+  *handled = false;
+  if (!select_coop_enabled() || n < 64) return 0;
+  static const int ncu = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return v;
+  }();
+  static const int wgs_env = [] {
+    const char* e = getenv("FISDF_SEL_WGS");
+    return e ? atoi(e) : 0;
+  }();
+  int G = wgs_env > 0 ? wgs_env : 128;
+  G = std::min({G, ncu, (n + 7) / 8});
+  if (G < 1) return 0;
+  const int RW = (n + G - 1) / G;
+  G = (n + RW - 1) / RW;
+  const size_t lds = sizeof(double) * ((size_t)RW * rmax + rmax + 2 * (size_t)RW);
+  if (lds > 150 * 1024 || RW > SC_MAXRW) return 0;
+  // scratch in the caller's work area (n*n doubles): records, global L, error flag
+  u32x4* rec = (u32x4*)work;
+  double* Lg = work + 4 * G;
+  int* err = (int*)(Lg + (long)n * rmax);
+  if ((long)(4 * G + (long)n * rmax + 2) > (long)n * n) return 0;
+  FISDF_HIP(hipMemsetAsync(rec, 0, 2 * G * sizeof(u32x4), s));
+  FISDF_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
+  FISDF_HIP(hipMemsetAsync(rank, 0, sizeof(int), s));
+  static bool attr = false;
+  if (!attr) {
+    FISDF_HIP(hipFuncSetAttribute((const void*)pchol_select_coop,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+    attr = true;
+  }
+  void* args[] = {(void*)&X2, (void*)&scale, (void*)&n,   (void*)&rmax, (void*)&tol, (void*)&RW,
+                  (void*)&piv, (void*)&rank, (void*)&rec, (void*)&Lg,   (void*)&err};
+  const hipError_t e = hipLaunchCooperativeKernel((const void*)pchol_select_coop, dim3(G),
+                                                  dim3(SC_THREADS), args, (unsigned)lds, s);
+  static const bool dbg = getenv("FISDF_SEL_DEBUG") != nullptr;
+  if (e != hipSuccess) {
+    if (dbg) fprintf(stderr, "[fisdf] cooperative selection refused: %s (G=%d RW=%d lds=%zu)\n",
+                     hipGetErrorString(e), G, RW, lds);
+    (void)hipGetLastError();
+    return 0;
+  }
+  int h_err = 0;
+  FISDF_HIP(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, s));
+  FISDF_HIP(hipStreamSynchronize(s));
+  if (dbg) fprintf(stderr, "[fisdf] cooperative selection G=%d RW=%d lds=%zu err=%d\n", G, RW, lds, h_err);
+  *handled = h_err == 0;
+  return 0;
+}
+
 int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rmax, double tol,
                       int* piv, int* rank, double* work, int* flags, bool* handled) {
   *handled = false;
-  if (n > 8 * PR_THREADS || rmax <= 0) return 0;
+  if (rmax <= 0) return 0;
+  FISDF_TRY(pchol_select_coop_launch(s, X2, scale, n, rmax, tol, piv, rank, work, handled));
+  if (*handled) return 0;
+  if (n > 8 * PR_THREADS) return 0;
   double* W = work;
   double* Lpan = W + (long)n * n;
   double* d = Lpan + (long)n * 16;
@@ -653,7 +912,8 @@ int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rm
                      dim3(256), 0, s, X2, scale, W, d, n2, n);
   FISDF_HIP(hipGetLastError());
   const int rpt = (n + PR_THREADS - 1) / PR_THREADS;
-  const dim3 ug((n + 63) / 64, (n + 63) / 64);
+  const int nt = (n + 63) / 64;
+  const dim3 ug(nt * (nt + 1) / 2);
 #define FISDF_PR(R, NBv)                                                                         for (int j0 = 0; j0 < rmax; j0 += NBv) {                                                          hipLaunchKernelGGL((pchol_real_panel<R, NBv>), dim3(1), dim3(PR_THREADS), 0, s, W, n, rmax,                        j0, tol, Lpan, piv, rank, d, flags, thr);                                   if (j0 + NBv < rmax)                                                                             hipLaunchKernelGGL((syrk_real_update<NBv>), ug, dim3(256), 0, s, W, n, Lpan, flags);        }
   if (rpt <= 2) { FISDF_PR(2, 16) }
   else if (rpt <= 4) { FISDF_PR(4, 16) }

@@ -197,7 +197,7 @@ class InterpolativeSeparableDensityFitting:
             q0, q1 = d.shard(nk)
             x2 = d.empty((ng0, ng0))
             d.ctx.call("fisdf_select_gram", _lib.ptr(x0), nk, q0, q1, ng0, nao, _lib.ptr(x2))
-            kshard.allreduce_sum(x2, d.comm)
+            kshard.allreduce_real_part(x2, d.comm)  # the Gram is Re(x2) + 0i
             d.ctx.call("fisdf_select_pivots", _lib.ptr(x2), nk, ng0, nip_max,
                        float(self.select_tol), perm.ctypes.data_as(_lib._ip), byref(npiv),
                        byref(full))

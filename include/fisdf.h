@@ -72,8 +72,9 @@ int fisdf_select_points(fisdf_ctx* ctx, const void* d_x0, int nk, int ng0, int n
                         double tol, int* h_perm, int* h_npiv, int* h_full_rank);
 
 /* The two halves of fisdf_select_points, for a k-point-sharded selection:
- * fisdf_select_gram: d_x2 (ng0, ng0) c128 = sum_{q in [q0,q1)} x0_q x0_q^H (its real part is
- *   fftisdf.py:376-378's x2; shards are summed with an all-reduce);
+ * fisdf_select_gram: d_x2 (ng0, ng0) c128 = Re(sum_{q in [q0,q1)} x0_q x0_q^H) + 0i (the real
+ *   part is fftisdf.py:376-378's x2, the only part :379 uses; shards are summed with an
+ *   all-reduce);
  * fisdf_select_pivots: x4 = Re(x2)^2/nk and the greedy pivoted Cholesky (fftisdf.py:379-384);
  *   synchronous. */
 int fisdf_select_gram(fisdf_ctx* ctx, const void* d_x0, int nk, int q0, int q1, int ng0, int nao,

@@ -181,6 +181,22 @@ def test_x4_and_y_parity(name):
         assert rel < 1e-12
 
 
+@pytest.mark.parametrize("name", ["toy222", "diamond_szv_gamma", "si_small"])
+def test_selection_paths_agree(name, monkeypatch):
+    """The cooperative left-looking selection (default) and the blocked right-looking one
+    (FISDF_SEL_COOP=0) pick the same pivots as dpstrf on these cases."""
+    perms = {}
+    for coop in ("1", "0"):
+        monkeypatch.setenv("FISDF_SEL_COOP", coop)
+        df, o, dm = make_df(name, inject=False)
+        df.build()
+        perms[coop] = df.perm.copy()
+    print(f"{name}: coop == blocked: {np.array_equal(perms['1'], perms['0'])}, "
+          f"coop == dpstrf: {np.array_equal(perms['1'], o['perm'])}")
+    assert np.array_equal(perms["1"], perms["0"])
+    assert np.array_equal(perms["1"], o["perm"])
+
+
 @pytest.mark.parametrize("name", ["toy222", "diamond_szv_gamma"])
 def test_gpu_selection(name):
     df, o, dm = make_df(name, inject=False)
