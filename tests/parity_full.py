@@ -1,7 +1,7 @@
 """Full-size parity: GPU ISDF build + get_jk vs the CPU oracle (gelsy restatement of
 fftisdf.py) on a bench config (default C2; C3 takes a few minutes of CPU).
 
-  python tools/parity_full.py [--config c2|c3|c4|c5] [--no-tr]
+  python tests/parity_full.py [--config c2|c3|c4|c5] [--no-tr]
 
 Prints one JSON line with max|dJ|, max|dK| (Ha), the ranks and the oracle's CPU time.
 The oracle runs with the GPU's interpolation points (SURVEY.md §7 hard part (b))."""
