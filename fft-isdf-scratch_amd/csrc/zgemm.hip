@@ -109,7 +109,7 @@ __device__ __forceinline__ void zgemm_epilogue(int M, int N, cplx alpha, cplx be
         for (int r = 0; r < 4; ++r) {
           int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
           int col = n0 + wn + ni * 16 + (lane & 15);
-          if (row < M && col < N) {
+          if (((mask >> (mi * 2 + ni)) & 1) && row < M && col < N) {
             cplx v = cmul(alpha, cmk(accR[mi][ni][r], accI[mi][ni][r]));
             C[(long)row * ldc + col] = cmk(v.x * v.x, 0.0);
             mi_ = fmax(mi_, fabs(v.y));
@@ -293,7 +293,10 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx al
 // lane-linear per wave-instruction (dest = base + lane*16); the K-contiguous operands keep
 // their XOR swizzle by permuting the per-lane SOURCE address instead.  Out-of-range lanes
 // read a zero page; conjugation is folded into the MFMA operand signs.
-constexpr int NST = 3;
+#ifndef FISDF_NST
+#define FISDF_NST 3
+#endif
+constexpr int NST = FISDF_NST;  // LDS ring depth; loads run NST-1 K-steps ahead
 constexpr int LPW = TILE / (64 * 4);  // glds wave-instructions per operand per step per wave
 __device__ cplx g_zero_page[64];      // zero-initialised device global
 
@@ -332,8 +335,26 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
   const int kend = min(K, kbeg + kchunk);
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wave = (w + ti + tj) & 3;
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  // wave -> sub-tile: the role rotates with the tile so idle roles spread over the SIMDs.
+  // Default 2x2 quadrants of 32x32; tiles whose valid 16x16 blocks would leave waves idle get
+  // another split so the 4 waves share the valid blocks: an edge row of tiles with <= 32
+  // valid rows splits by 16-column blocks (and an edge column by 16-row blocks), a full HERK
+  // diagonal tile gives its 10 lower blocks out as 3 + 3 + 2 + 2.  `own` = the blocks of the
+  // wave's nominal 2x2 (bit mi*2+ni) it is responsible for.
+  const int role = (w + ti + tj) & 3;
+  const int vr = min(4, max(0, (M - m0 + 15) / 16)), vc = min(4, max(0, (N - n0 + 15) / 16));
+  int wm, wn, own;
+  if (HERK && ti == tj && vr == 4) {
+    wm = role == 0 ? 0 : (role == 1 ? 32 : (role == 2 ? 32 : 48));
+    wn = role == 1 ? 32 : 0;
+    own = role < 2 ? 15 : 3;
+  } else if (vr <= 2 && vc > 2) {
+    wm = 0; wn = 16 * role; own = 5;
+  } else if (vc <= 2 && vr > 2) {
+    wm = 16 * role; wn = 0; own = 3;
+  } else {
+    wm = (role >> 1) * 32; wn = (role & 1) * 32; own = 15;
+  }
 
   // per-lane source of each glds: slot s = (w*LPW + j)*64 + lane of the operand tile
   const cplx* srcA[LPW];
@@ -398,14 +419,15 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
       const int r0 = m0 + wm + mi * 16, c0 = n0 + wn + ni * 16;
-      const bool live = r0 < M && c0 < N && !(HERK && c0 > r0);
+      const bool live = ((own >> (mi * 2 + ni)) & 1) && r0 < M && c0 < N && !(HERK && c0 > r0);
       mask |= (live ? 1 : 0) << (mi * 2 + ni);
     }
 
   const int nsteps = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  // (steps past the end load the zero page: the counted waits assume NST-1 steps in flight)
   if (nsteps > 0) {
-    issue(0);
-    issue(1);
+#pragma unroll
+    for (int st = 0; st < NST - 1; ++st) issue(st);
   }
   const int i16 = lane & 15, kq = lane >> 4;
   auto mainloop = [&](auto maskc) {
@@ -413,9 +435,9 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
     for (int s = 0; s < nsteps; ++s) {
       // own loads of step s retired (step s+1's 2*LPW stay in flight), then every wave's:
       // the barrier also retires all reads of the slot step s+2 is about to overwrite
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * LPW) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * LPW * (NST - 2)) : "memory");
       __builtin_amdgcn_sched_barrier(0);
-      issue(s + 2);
+      issue(s + NST - 1);
       const int cur = s % NST;
       const cplx* as = sm + (long)(cur * 2 + 0) * TILE;
       const cplx* bs = sm + (long)(cur * 2 + 1) * TILE;
@@ -424,9 +446,9 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
         const int k = kk + kq;
         cplx a[2], b[2];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          a[u] = as[SA::slot(wm + u * 16 + i16, k)];
-          b[u] = bs[SB::slot(wn + u * 16 + i16, k)];
+        for (int u = 0; u < 2; ++u) {  // & 63: a masked block past the tile reads in-tile rows
+          a[u] = as[SA::slot((wm + u * 16 + i16) & 63, k)];
+          b[u] = bs[SB::slot((wn + u * 16 + i16) & 63, k)];
         }
         // op(A) = a (or conj a), op(B) = b (or conj b):
         //   Re += ar br - ai' bi' ;  Im += ar bi' + ai' br   (ai' = +-ai, bi' = +-bi)

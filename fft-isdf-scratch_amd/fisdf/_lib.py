@@ -12,7 +12,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfisdf.so")
+# FISDF_LIB_VARIANT=x loads libfisdf_x.so from the same directory (A/B of build variants)
+LIB_PATH = os.path.join(_HERE, "libfisdf%s.so" % (
+    "_" + os.environ["FISDF_LIB_VARIANT"] if os.environ.get("FISDF_LIB_VARIANT") else ""))
 
 STAGES = ["select", "x4", "y", "factor", "fft", "trsm", "herk", "small", "get_j", "get_k", "ws"]
 

@@ -59,7 +59,11 @@ def test_zgemm_ops(env, opA, opB):
 
 
 @pytest.mark.parametrize("M,N,K,ks", [(1, 1, 1, 1), (64, 64, 16, 1), (129, 65, 17, 1),
-                                      (200, 200, 5000, 8), (600, 1, 600, 1)])
+                                      (200, 200, 5000, 8), (600, 1, 600, 1),
+                                      # edge tiles with <= 32 valid rows / columns (the waves
+                                      # split by 16-blocks there)
+                                      (24, 300, 50, 1), (88, 40, 33, 1), (40, 130, 70, 2),
+                                      (600, 600, 300, 3)])
 def test_zgemm_shapes_splitk(env, M, N, K, ks):
     torch, L, ctx = env
     rng = np.random.default_rng(M + N + K)
@@ -70,6 +74,21 @@ def test_zgemm_shapes_splitk(env, M, N, K, ks):
     ctx.call("fisdf_zgemm", 0, 0, M, N, K, one.ctypes.data_as(L._dp), L.ptr(dA), K, 0, L.ptr(dB),
              N, 0, zero.ctypes.data_as(L._dp), L.ptr(dC), N, 0, 1, ks)
     ref = A @ B
+    assert abs(dC.cpu().numpy() - ref).max() < 1e-12 * max(K, 16)
+
+
+@pytest.mark.parametrize("n,K,ks", [(1, 7, 1), (16, 40, 1), (24, 37, 1), (40, 100, 2),
+                                    (64, 64, 1), (88, 300, 4), (100, 33, 1), (600, 700, 3)])
+def test_herk_shapes(env, n, K, ks):
+    """C = A A^H through the lower-tile HERK (diagonal tiles split 3+3+2+2 over the waves,
+    edge tiles by 16-blocks), compared with NumPy on the full matrix (both triangles)."""
+    torch, L, ctx = env
+    rng = np.random.default_rng(n * 1000 + K)
+    A = rnd(rng, n, K)
+    dA = dev(torch, A)
+    dC = torch.full((n, n), complex(7.0, 7.0), dtype=torch.complex128, device="cuda")
+    ctx.call("fisdf_herk", n, K, 1.0, L.ptr(dA), K, L.ptr(dC), n, ks)
+    ref = A @ A.conj().T
     assert abs(dC.cpu().numpy() - ref).max() < 1e-12 * max(K, 16)
 
 

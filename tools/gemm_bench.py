@@ -51,3 +51,15 @@ for M, K in (((600, 600),) if QUICK else ((300, 300), (256, 256), (600, 600), (1
     ms = timeit(lambda: ctx.call("fisdf_zgemm", 0, 0, M, N, K, mone, L.ptr(Lm), r, 0, L.ptr(X), N, 0,
                                  one, L.ptr(Bm), N, 0, 1, 1))
     print(f"zgemm NN M={M} N={N} K={K}: {ms:.3f} ms  {8.0 * M * N * K / ms / 1e9:.1f} TF/s", flush=True)
+if "--herk-shapes" in sys.argv:
+    # tile-waste study: HERK at multiples of 64 vs 600, and the same product as a full GEMM
+    for n in (512, 576, 600, 640):
+        An = rnd(n, N)
+        Cn = rnd(n, n)
+        for ks in (13, 32):
+            ms = timeit(lambda: ctx.call("fisdf_herk", n, N, 1.0, L.ptr(An), N, L.ptr(Cn), n, ks))
+            print(f"herk n={n} ks={ks}: {ms:.3f} ms  {4.0 * n * n * N / ms / 1e9:.1f} TF/s (lower-half flops)", flush=True)
+        for ks in (4, 8):
+            ms = timeit(lambda: ctx.call("fisdf_zgemm", 0, 3, n, n, N, one, L.ptr(An), N, 0, L.ptr(An), N, 0,
+                                         zero, L.ptr(Cn), n, 0, 1, ks))
+            print(f"zgemm NC n={n} K={N} ks={ks}: {ms:.3f} ms  {8.0 * n * n * N / ms / 1e9:.1f} TF/s", flush=True)
