@@ -1204,18 +1204,24 @@ int fisdf_get_eri(fisdf_ctx* c, const void* Xv, int nip, int nao, const int kidx
 }
 
 // ---- A7 -----------------------------------------------------------------------
-int fisdf_get_j(fisdf_ctx* c, const void* Xv, const void* W0, const void* dmsv, int nset, int nk,
-                int nip, int nao, void* vjv) {
+int fisdf_get_j_rows(fisdf_ctx* c, const void* Xv, const void* W0, const void* dmsv, int nset,
+                     int nk, int nip, int nao, int i0, int i1, void* vjv) {
   FISDF_TRY(device_guard(c));
+  FISDF_CHECK(0 <= i0 && i0 <= i1 && i1 <= nip, "get_j: bad row range");
   StageTimer tm(c, FISDF_ST_J);
   const cplx* X = (const cplx*)Xv;
   const cplx* dms = (const cplx*)dmsv;
   cplx* vj = (cplx*)vjv;
+  const int nb = i1 - i0;
   const long xs = (long)nip * nao, ds = (long)nao * nao;
+  if (nb == 0) {
+    FISDF_HIP(hipMemsetAsync(vj, 0, sizeof(cplx) * nset * nk * ds, c->stream));
+    return 0;
+  }
   Carver cv;
   size_t oT = cv.take(sizeof(cplx) * nset * nk * xs);
   size_t oR = cv.take(sizeof(cplx) * nset * nip);
-  size_t oV = cv.take(sizeof(cplx) * nset * nip);
+  size_t oV = cv.take(sizeof(cplx) * nset * nb);
   void* base;
   FISDF_TRY(arena_get(c, cv.off, &base));
   cplx* T = (cplx*)((char*)base + oT);
@@ -1225,23 +1231,31 @@ int fisdf_get_j(fisdf_ctx* c, const void* Xv, const void* W0, const void* dmsv, 
   for (int x = 0; x < nset; ++x)
     FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nip, nao, nao, ONE, X, nao, xs, dms + (long)x * nk * ds,
                     nao, ds, ZERO, T + (long)x * nk * xs, nao, xs, nk));
-  // rho_I = sum_k X_k[I,m] D_k[m,n] X_k*[I,n] / nk  (:155-156)
+  // rho_I = sum_k X_k[I,m] D_k[m,n] X_k*[I,n] / nk  (:155-156), every I
   FISDF_TRY(rho_diag(c->stream, T, X, nset, nk, nip, nao, 1.0 / nk, rho));
-  // v = W0 rho  (:159)
-  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nip, 1, nip, ONE, (const cplx*)W0, nip, 0, rho, 1, nip,
-                  ZERO, v, 1, nip, nset));
-  // J_k = X_k^H diag(v) X_k  (:166)
-  FISDF_TRY(scale_rows(c->stream, X, v, nset, nk, nip, nao, T));
+  // v_I = (W0 rho)_I for the rows of the block  (:159)
+  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nb, 1, nip, ONE, (const cplx*)W0 + (long)i0 * nip, nip, 0,
+                  rho, 1, nip, ZERO, v, 1, nb, nset));
+  // J_k (block part) = X_k[I]^H diag(v_I) X_k[I]  (:166)
+  FISDF_TRY(scale_rows(c->stream, X, v, nset, nk, nip, i0, nb, nao, T));
   for (int x = 0; x < nset; ++x)
-    FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nao, nao, nip, ONE, X, nao, xs, T + (long)x * nk * xs,
-                    nao, xs, ZERO, vj + (long)x * nk * ds, nao, ds, nk));
+    FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nao, nao, nb, ONE, X + (long)i0 * nao, nao, xs,
+                    T + (long)x * nk * nb * nao, nao, (long)nb * nao, ZERO,
+                    vj + (long)x * nk * ds, nao, ds, nk));
   return 0;
 }
 
+int fisdf_get_j(fisdf_ctx* c, const void* Xv, const void* W0, const void* dmsv, int nset, int nk,
+                int nip, int nao, void* vjv) {
+  return fisdf_get_j_rows(c, Xv, W0, dmsv, nset, nk, nip, nao, 0, nip, vjv);
+}
+
 // ---- A8 -----------------------------------------------------------------------
-int fisdf_get_k(fisdf_ctx* c, const void* Xv, const void* Wsv, const void* dmsv, int nset, int nip,
-                int nao, const int kmesh[3], const double a[9], void* vkv) {
+int fisdf_get_k_rows(fisdf_ctx* c, const void* Xv, const void* Wsv, const void* dmsv, int nset,
+                     int nip, int nao, const int kmesh[3], const double a[9], int i0, int i1,
+                     void* vkv) {
   FISDF_TRY(device_guard(c));
+  FISDF_CHECK(0 <= i0 && i0 <= i1 && i1 <= nip, "get_k: bad row range");
   StageTimer tm(c, FISDF_ST_K);
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
   const cplx* phase;
@@ -1250,39 +1264,51 @@ int fisdf_get_k(fisdf_ctx* c, const void* Xv, const void* Wsv, const void* dmsv,
   const cplx* Ws = (const cplx*)Wsv;
   const cplx* dms = (const cplx*)dmsv;
   cplx* vk = (cplx*)vkv;
-  const long xs = (long)nip * nao, ds = (long)nao * nao, nn = (long)nip * nip;
+  const int nb = i1 - i0;
+  const long xs = (long)nip * nao, ds = (long)nao * nao, bn = (long)nb * nip, ba = (long)nb * nao;
+  if (nb == 0) {
+    FISDF_HIP(hipMemsetAsync(vk, 0, sizeof(cplx) * nset * nk * ds, c->stream));
+    return 0;
+  }
   Carver cv;
-  size_t oT = cv.take(sizeof(cplx) * nk * xs);
-  size_t o1 = cv.take(sizeof(cplx) * nk * nn);
-  size_t o2 = cv.take(sizeof(cplx) * nk * nn);
+  size_t oT = cv.take(sizeof(cplx) * nk * ba);
+  size_t o1 = cv.take(sizeof(cplx) * nk * bn);
+  size_t o2 = cv.take(sizeof(cplx) * nk * bn);
   void* base;
   FISDF_TRY(arena_get(c, cv.off, &base));
   cplx* T = (cplx*)((char*)base + oT);
   cplx* B1 = (cplx*)((char*)base + o1);
   cplx* B2 = (cplx*)((char*)base + o2);
+  const cplx* Xb = X + (long)i0 * nao;
   for (int x = 0; x < nset; ++x) {
     const cplx* dm = dms + (long)x * nk * ds;
-    // rho_k = X_k D_k X_k^H / nk  (:211-212)
-    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nip, nao, nao, ONE, X, nao, xs, dm, nao, ds, ZERO, T,
-                    nao, xs, nk));
-    FISDF_TRY(zgemm(c->stream, OP_N, OP_C, nip, nip, nao, cmk(1.0 / nk, 0), T, nao, xs, X, nao, xs,
-                    ZERO, B1, nip, nn, nk));
+    // rho_k^T[I, J] = rho_k[J, I] = (conj(X_k[I]) D_k^T X_k^T)[I, J] / nk for the block rows
+    // (:211-212, transposed at the source so :219's product is element-wise)
+    FISDF_TRY(zgemm(c->stream, OP_R, OP_T, nb, nao, nao, cmk(1.0 / nk, 0), Xb, nao, xs, dm, nao, ds,
+                    ZERO, T, nao, ba, nk));
+    FISDF_TRY(zgemm(c->stream, OP_N, OP_T, nb, nip, nao, ONE, T, nao, ba, X, nao, xs, ZERO, B1,
+                    nip, bn, nk));
     // rho_s = Phi rho_k (:215), real (:216)
-    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nn, nk, ONE, phase, nk, 0, B1, nn, 0, ZERO, B2, nn,
+    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, bn, nk, ONE, phase, nk, 0, B1, bn, 0, ZERO, B2, bn,
                     0, 1));
-    FISDF_TRY(real_part(c->stream, B2, 1.0, B2, nk * nn, c->maximag + 2));
-    // V_s = W_s * rho_s^T (:219)
-    FISDF_TRY(ws_times_rhoT(c->stream, Ws, B2, nk, nip, B1));
+    FISDF_TRY(real_part(c->stream, B2, 1.0, B2, nk * bn, c->maximag + 2));
+    // V_s = W_s * rho_s^T (:219), block rows
+    FISDF_TRY(ws_times_rho_rows(c->stream, Ws, B2, nk, nip, i0, nb, B1));
     // V_k = Phi^T V_s (:222)
-    FISDF_TRY(zgemm(c->stream, OP_T, OP_N, nk, nn, nk, ONE, phase, nk, 0, B1, nn, 0, ZERO, B2, nn,
+    FISDF_TRY(zgemm(c->stream, OP_T, OP_N, nk, bn, nk, ONE, phase, nk, 0, B1, bn, 0, ZERO, B2, bn,
                     0, 1));
-    // K_k = X_k^H V_k X_k (:225)
-    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nip, nao, nip, ONE, B2, nip, nn, X, nao, xs, ZERO, T,
-                    nao, xs, nk));
-    FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nao, nao, nip, ONE, X, nao, xs, T, nao, xs, ZERO,
+    // K_k (block part) = X_k[I]^H (V_k[I, :] X_k)  (:225)
+    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nb, nao, nip, ONE, B2, nip, bn, X, nao, xs, ZERO, T,
+                    nao, ba, nk));
+    FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nao, nao, nb, ONE, Xb, nao, xs, T, nao, ba, ZERO,
                     vk + (long)x * nk * ds, nao, ds, nk));
   }
   return 0;
+}
+
+int fisdf_get_k(fisdf_ctx* c, const void* Xv, const void* Wsv, const void* dmsv, int nset, int nip,
+                int nao, const int kmesh[3], const double a[9], void* vkv) {
+  return fisdf_get_k_rows(c, Xv, Wsv, dmsv, nset, nip, nao, kmesh, a, 0, nip, vkv);
 }
 
 }  // extern "C"

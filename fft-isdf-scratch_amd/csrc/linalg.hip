@@ -191,15 +191,15 @@ __global__ void real_part_kernel(const cplx* __restrict__ in, double scale, cplx
 }
 
 // V[R,I,J] = Ws[R,I,J] * Re(rho[R,J,I])   (fftisdf.py:219)
-__global__ void ws_times_rhoT_kernel(const cplx* __restrict__ ws, const cplx* __restrict__ rho,
-                                     int nimg, int nip, cplx* __restrict__ V) {
+// V[R][i][j] = Re(ws[R][i0+i][j]) * Re(rhoT[R][i][j]) for a block of nb rows (fftisdf.py:219
+// with rho_s transposed at its source, so the product is element-wise)
+__global__ void ws_times_rho_rows_kernel(const cplx* __restrict__ ws, const cplx* __restrict__ rhoT,
+                                         int nimg, int nip, int i0, int nb, cplx* __restrict__ V) {
   long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  long tot = (long)nimg * nip * nip;
-  if (e >= tot) return;
-  long R = e / ((long)nip * nip);
-  int I = (int)((e / nip) % nip), J = (int)(e % nip);
-  double r = rho[R * nip * nip + (long)J * nip + I].x;
-  V[e] = cmk(ws[e].x * r, 0.0);
+  const long per = (long)nb * nip;
+  if (e >= (long)nimg * per) return;
+  const long R = e / per, r = e % per;
+  V[e] = cmk(ws[R * nip * nip + (long)i0 * nip + r].x * rhoT[e].x, 0.0);
 }
 
 // rho[x,I] = scale * sum_k sum_n T[x,k,I,n] conj(X[k,I,n])
@@ -222,15 +222,17 @@ __global__ void rho_diag_kernel(const cplx* __restrict__ T, const cplx* __restri
 }
 
 // Xv[x,k,I,n] = v[x,I] * X[k,I,n]
+// Xv[x][k][I][m] = v[x][I] * X[k][i0+I][m] for I < nb (X: nip rows per k)
 __global__ void scale_rows_kernel(const cplx* __restrict__ X, const cplx* __restrict__ v, int nset,
-                                  int nk, int nip, int nao, cplx* __restrict__ Xv) {
+                                  int nk, int nip, int i0, int nb, int nao, cplx* __restrict__ Xv) {
   long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  long per = (long)nk * nip * nao;
+  long per = (long)nk * nb * nao;
   if (e >= (long)nset * per) return;
   int x = (int)(e / per);
   long r = e % per;
-  int I = (int)((r / nao) % nip);
-  Xv[e] = cmul(v[(long)x * nip + I], X[r]);
+  int k = (int)(r / ((long)nb * nao));
+  int I = (int)((r / nao) % nb), m = (int)(r % nao);
+  Xv[e] = cmul(v[(long)x * nb + I], X[((long)k * nip + i0 + I) * nao + m]);
 }
 
 // ---- y build, k-mesh part (fftisdf.py:79-85) -----------------------------------------
@@ -765,15 +767,6 @@ int csquare(hipStream_t s, cplx* a, long n, unsigned long long* maximag) {
   return 0;
 }
 
-int ws_times_rhoT(hipStream_t s, const cplx* ws, const cplx* rho, int nimg, int nip, cplx* V) {
-  long n = (long)nimg * nip * nip;
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(ws_times_rhoT_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, ws,
-                     rho, nimg, nip, V);
-  FISDF_HIP(hipGetLastError());
-  return 0;
-}
-
 int rho_diag(hipStream_t s, const cplx* T, const cplx* X, int nset, int nk, int nip, int nao,
              double scale, cplx* rho) {
   long n = (long)nset * nip;
@@ -784,12 +777,22 @@ int rho_diag(hipStream_t s, const cplx* T, const cplx* X, int nset, int nk, int 
   return 0;
 }
 
-int scale_rows(hipStream_t s, const cplx* X, const cplx* v, int nset, int nk, int nip, int nao,
-               cplx* Xv) {
-  long n = (long)nset * nk * nip * nao;
+int ws_times_rho_rows(hipStream_t s, const cplx* ws, const cplx* rhoT, int nimg, int nip, int i0,
+                      int nb, cplx* V) {
+  long n = (long)nimg * nb * nip;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ws_times_rho_rows_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s,
+                     ws, rhoT, nimg, nip, i0, nb, V);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int scale_rows(hipStream_t s, const cplx* X, const cplx* v, int nset, int nk, int nip, int i0,
+               int nb, int nao, cplx* Xv) {
+  long n = (long)nset * nk * nb * nao;
   if (n == 0) return 0;
   hipLaunchKernelGGL(scale_rows_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, X, v,
-                     nset, nk, nip, nao, Xv);
+                     nset, nk, nip, i0, nb, nao, Xv);
   FISDF_HIP(hipGetLastError());
   return 0;
 }

@@ -492,8 +492,12 @@ def get_j_kpts(df_obj, dm_kpts, hermi=1, kpts=np.zeros((1, 3)), kpts_band=None, 
     nset, nk, nao = dms.shape[:3]
     nip = st["X"].shape[1]
     vj = d.empty(dms.shape)
-    d.ctx.call("fisdf_get_j", _lib.ptr(st["X"]), _lib.ptr(st["W0"]), _lib.ptr(ddms), nset, nk,
-               nip, nao, _lib.ptr(vj))
+    # sharded: each rank contracts its block of interpolation points, one all-reduce (:166)
+    i0, i1 = d.shard(nip) if d.size > 1 else (0, nip)
+    d.ctx.call("fisdf_get_j_rows", _lib.ptr(st["X"]), _lib.ptr(st["W0"]), _lib.ptr(ddms), nset,
+               nk, nip, nao, i0, i1, _lib.ptr(vj))
+    if d.size > 1:  # the library runs on torch's current stream: the all-reduce is ordered
+        kshard.allreduce_sum(vj, d.comm)
     out = vj.cpu().numpy()
     band = np.asarray(kpts if kpts_band is None else kpts_band)
     if abs(band).max() < 1e-9:                                           # :169-170
@@ -513,6 +517,10 @@ def get_k_kpts(df_obj, dm_kpts, hermi=1, kpts=np.zeros((1, 3)), kpts_band=None, 
     km_c, km_p = _lib.iarr(df_obj.kmesh)
     a_c, a_p = _lib.darr(np.asarray(df_obj.cell.lattice_vectors(), float).ravel())
     vk = d.empty(dms.shape)
-    d.ctx.call("fisdf_get_k", _lib.ptr(st["X"]), _lib.ptr(st["Ws"]), _lib.ptr(ddms), nset, nip,
-               nao, km_p, a_p, _lib.ptr(vk))
+    # sharded: each rank contracts its block of interpolation points, one all-reduce (:225)
+    i0, i1 = d.shard(nip) if d.size > 1 else (0, nip)
+    d.ctx.call("fisdf_get_k_rows", _lib.ptr(st["X"]), _lib.ptr(st["Ws"]), _lib.ptr(ddms), nset,
+               nip, nao, km_p, a_p, i0, i1, _lib.ptr(vk))
+    if d.size > 1:
+        kshard.allreduce_sum(vk, d.comm)
     return _format_jks(vk.cpu().numpy(), dm_kpts)

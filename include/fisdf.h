@@ -179,6 +179,16 @@ int fisdf_get_j(fisdf_ctx* ctx, const void* d_X, const void* d_W0, const void* d
 int fisdf_get_k(fisdf_ctx* ctx, const void* d_X, const void* d_Ws, const void* d_dms, int nset,
                 int nip, int nao, const int kmesh[3], const double a[9], void* d_vk);
 
+/* Row-block forms: the contribution of the interpolation points I in [i0, i1) to J / K
+ * (J_k = sum_I X_k[I]^H v_I X_k[I], K_k = sum_I X_k[I]^H (V_k[I,:] X_k)); the full result is
+ * the sum over a partition of [0, nip) — a sharded caller all-reduces nset*nk*nao^2 values.
+ * fisdf_get_j / fisdf_get_k are the [0, nip) cases. */
+int fisdf_get_j_rows(fisdf_ctx* ctx, const void* d_X, const void* d_W0, const void* d_dms,
+                     int nset, int nk, int nip, int nao, int i0, int i1, void* d_vj);
+int fisdf_get_k_rows(fisdf_ctx* ctx, const void* d_X, const void* d_Ws, const void* d_dms,
+                     int nset, int nip, int nao, const int kmesh[3], const double a[9], int i0,
+                     int i1, void* d_vk);
+
 /* ---- ISDF 4-index integrals (get_eri / ao2mo surface) --------------------------
  * eri[i*n2+j][k*n4+l] = sum_IJ W_q[I,J] conj(A1[I,i]) A2[I,j] conj(A3[J,k]) A4[J,l] with
  * A_s = X_{kidx[s]} C_s, q = k2 - k1 (fftdf-with-k-lstsq.py:221-232).  d_Wq: the (nip,nip)
