@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <string>
 #include <vector>
 
 #include "common.h"
@@ -42,6 +43,7 @@ struct fisdf_ctx {
   cplx* f_Lp = nullptr;     // (nk, nip*nip) pivot-order factor, ld = rank_q
   cplx* f_Linv = nullptr;   // (nk, nblk*nb*nb)
   cplx* f_Q = nullptr;      // (nk, nip, nip) block-row operator of trsm_merged (build_trsm_q)
+  cplx* f_Li = nullptr;     // (nk, nip, nip) L^{-1} (pivot order) = trsm_merged on the identity
   cplx* f_x4s = nullptr;    // (nk, nip, nip) staged x4_q of the factored slots
   int* f_fail_pinned = nullptr;  // unpivoted path: per-slot failure flags (host, pinned)
   double f_tol = 1e-14;
@@ -216,6 +218,8 @@ int free_factors(fisdf_ctx* c) {
   if (c->f_Linv) FISDF_HIP(hipFree(c->f_Linv));
   if (c->f_Q) FISDF_HIP(hipFree(c->f_Q));
   c->f_Q = nullptr;
+  if (c->f_Li) FISDF_HIP(hipFree(c->f_Li));
+  c->f_Li = nullptr;
   if (c->f_x4s) FISDF_HIP(hipFree(c->f_x4s));
   c->f_x4s = nullptr;
   if (c->f_fail_pinned) FISDF_HIP(hipHostFree(c->f_fail_pinned));
@@ -779,6 +783,11 @@ int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src) {
   FISDF_TRY(gather_lp(s, c->f_L, nip, nip, c->f_piv, c->f_rank_dev, nip, c->f_Lp, nk));
   FISDF_TRY(trinv_blocks(s, c->f_Lp, nip, nip, nn, nb, (long)nblk * nb * nb, c->f_Linv, nk));
   FISDF_TRY(build_trsm_q(s, c->f_Lp, nip, nn, c->f_Q, nk, GEMM_FULL));
+  // L^{-1} by the same block-row substitution applied to the identity (the fit then applies it
+  // as one lower-triangular GEMM over the grid; J/K within 2-3x of the TRSM's rounding,
+  // tests/experiments/explicit_tri_inverse.py)
+  FISDF_TRY(set_identity(s, c->f_Li, nip, nk));
+  FISDF_TRY(trsm_merged_batched(s, c->f_Q, nn, nip, c->f_Li, nip, nn, nip, nk));
   return 0;
 }
 
@@ -827,6 +836,7 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   FISDF_HIP(hipMalloc(&c->f_Lp, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_Linv, sizeof(cplx) * (size_t)nk * nblk * nb * nb));
   FISDF_HIP(hipMalloc(&c->f_Q, sizeof(cplx) * nk * nn));
+  FISDF_HIP(hipMalloc(&c->f_Li, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_piv, sizeof(int) * (size_t)nk * nip));
   FISDF_HIP(hipMalloc(&c->f_rank_dev, sizeof(int) * nk));
   FISDF_HIP(hipHostMalloc((void**)&c->f_rank_pinned, sizeof(int) * nk, hipHostMallocDefault));
@@ -1044,7 +1054,16 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     {
       StageTimer tm(c, FISDF_ST_TRSM, st);
       // U = L^{-1} Yh   (fit, factored order; (x4_q)_PP = L L^H)
-      if (r == nip) {  // merged block-row substitution, in place
+      static const bool tri_gemm = [] {
+        const char* e = getenv("FISDF_TRSM");
+        return !(e && std::string(e) == "merged");
+      }();
+      if (r == nip && tri_gemm) {  // one lower-triangular GEMM with L^{-1}
+        FISDF_TRY(zgemm(st, OP_N, OP_N, nip, (int)ngrid, nip, ONE, c->f_Li + (long)sl * nn, nip, 0,
+                        Yh, ngrid, 0, ZERO, U, ngrid, 0, 1, 1, nullptr, EPI_NONE, nullptr,
+                        GEMM_A_LOWER | (real_q ? GEMM_A_REAL : GEMM_FULL)));
+        Uq = U;
+      } else if (r == nip) {  // merged block-row substitution, in place
         FISDF_TRY(trsm_merged(st, c->f_Q + (long)sl * nn, nip, Yh, ngrid, (int)ngrid,
                               real_q ? GEMM_A_REAL : GEMM_FULL));
         Uq = Yh;

@@ -57,7 +57,9 @@ enum Epi { EPI_NONE = 0, EPI_SQUARE_RE = 1 };
 // arithmetic modes (MFMA work skipped): GEMM_A_REAL: Im(op(A)) is taken as zero (2 of the 4
 // real MFMAs per complex block); GEMM_RE_ONLY: only Re(C) is formed (Im(C) written as 0).
 // Supported for (N,N), (C,N) and the HERK; other op pairs require mode 0.
-enum GemmMode { GEMM_FULL = 0, GEMM_A_REAL = 1, GEMM_RE_ONLY = 2 };
+// GEMM_A_LOWER: op(A) = A (OP_N) is lower triangular: each M-tile stops its K loop at the
+// tile's last row (the zero upper part is never read or multiplied).
+enum GemmMode { GEMM_FULL = 0, GEMM_A_REAL = 1, GEMM_RE_ONLY = 2, GEMM_A_LOWER = 4 };
 int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha,
           const cplx* A, long lda, long sA, const cplx* B, long ldb, long sB, cplx beta,
           cplx* C, long ldc, long sC, int batch, int ksplit = 1, cplx* work = nullptr,

@@ -567,6 +567,38 @@ int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol,
   return 0;
 }
 
+// trsm_merged over a batch (Q and X with batch strides sQ, sX): one launch per block row
+int trsm_merged_batched(hipStream_t s, const cplx* Q, long sQ, int r, cplx* X, long ld, long sX,
+                        int ncol, int batch) {
+  const int nblk = (r + 63) / 64;
+  if (nblk == 0 || batch == 0) return 0;
+  const int s0 = r - 64 * (nblk - 1);
+  const cplx one = cmk(1, 0), zero = cmk(0, 0);
+  for (int b = 0; b < nblk; ++b) {
+    const int b0 = b == 0 ? 0 : s0 + (b - 1) * 64, m = b == 0 ? s0 : 64, b1 = b0 + m;
+    FISDF_TRY(zgemm(s, OP_N, OP_N, m, ncol, b1, one, Q + (long)b0 * r, r, sQ, X, ld, sX, zero,
+                    X + (long)b0 * ld, ld, sX, batch, 1));
+  }
+  return 0;
+}
+
+__global__ void set_identity_kernel(cplx* __restrict__ X, int n, int batch) {
+  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long nn = (long)n * n;
+  if (e >= nn * batch) return;
+  const long r = e % nn;
+  X[e] = cmk(r / n == r % n ? 1.0 : 0.0, 0.0);
+}
+
+int set_identity(hipStream_t s, cplx* X, int n, int batch) {
+  const long tot = (long)n * n * batch;
+  if (tot == 0) return 0;
+  hipLaunchKernelGGL(set_identity_kernel, dim3(nblocks(tot, 256, 1L << 30)), dim3(256), 0, s, X, n,
+                     batch);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
 int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int ldl, long sL, int nb, long sLi,
                  cplx* Linv, int batch) {
   FISDF_CHECK(nb >= 1 && nb <= 64, "trinv_blocks: nb must be <= 64");

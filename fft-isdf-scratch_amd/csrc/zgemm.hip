@@ -332,7 +332,8 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
   }
   const int m0 = ti * BM, n0 = tj * BN;
   const int kbeg = split * kchunk;
-  const int kend = min(K, kbeg + kchunk);
+  int kend = min(K, kbeg + kchunk);
+  if constexpr ((MODE & GEMM_A_LOWER) != 0) kend = min(kend, m0 + BM);  // A[m][k] = 0 for k > m
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // wave -> sub-tile: the role rotates with the tile so idle roles spread over the SIMDs.
@@ -561,9 +562,11 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
           long sC, int batch, int ksplit, cplx* work, int epi, unsigned long long* mon, int mode) {
   FISDF_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 0, "zgemm: negative size");
   FISDF_CHECK(opA >= 0 && opA < 4 && opB >= 0 && opB < 4, "zgemm: bad op");
-  FISDF_CHECK(mode >= 0 && mode <= 3, "zgemm: bad mode");
+  FISDF_CHECK(mode >= 0 && mode <= 7, "zgemm: bad mode");
   FISDF_CHECK(mode == GEMM_FULL || (opB == OP_N && (opA == OP_N || opA == OP_C)),
               "zgemm: real modes are implemented for (N,N) and (C,N) only");
+  FISDF_CHECK(!(mode & GEMM_A_LOWER) || (opA == OP_N && opB == OP_N && !(mode & GEMM_RE_ONLY)),
+              "zgemm: GEMM_A_LOWER is implemented for (N,N), optionally with GEMM_A_REAL");
   if (M == 0 || N == 0 || batch == 0) return 0;
   if (ksplit < 1) ksplit = 1;
   if (epi != EPI_NONE) ksplit = 1;
@@ -586,6 +589,7 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
                            ksplit, kchunk, work, epi, mon);                                   \
   }
   FISDF_MCASE(0, 0, 1) FISDF_MCASE(0, 0, 2) FISDF_MCASE(0, 0, 3)
+  FISDF_MCASE(0, 0, 4) FISDF_MCASE(0, 0, 5)
   FISDF_MCASE(3, 0, 1) FISDF_MCASE(3, 0, 2) FISDF_MCASE(3, 0, 3)
 #undef FISDF_MCASE
   if (mode == GEMM_FULL) switch (opA * 4 + opB) {
