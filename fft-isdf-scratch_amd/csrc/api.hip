@@ -752,8 +752,11 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
     const int m = std::min(gb, nblk - s0);
     const long nm = (long)nip * m;
     // fx_k^T = X_k f_k^H  -> FX[k][I][g]   (:76, transposed layout)
+    static const int fx_epi = getenv("FISDF_FX_NT") && getenv("FISDF_FX_NT")[0] == '0'
+                                  ? EPI_NONE : EPI_STREAM;
     FISDF_TRY(zgemm(c->stream, OP_N, OP_C, nip, m, nao, ONE, X, nao, (long)nip * nao,
-                    f + (long)s0 * nao, nao, f_kstride, ZERO, FX, m, nm, nks));
+                    f + (long)s0 * nao, nao, f_kstride, ZERO, FX, m, nm, nks, 1, nullptr,
+                    fx_epi));
     // fx_s = Phi fx_k (:79, real :81), y_s = fx_s^2 (:83), y_k = Phi^T y_s (:84) for the
     // listed q, written into yT[slot][I][g0+s0+g] (:85): separable k-mesh DFTs
     FISDF_TRY(kmesh_y(c->stream, FX, nm, kmesh, h_qs, dq, nq, m, yT, (long)nip * ngrid, ngrid,

@@ -690,11 +690,14 @@ __global__ void diag_max_kernel(const cplx* __restrict__ A, int n, long sA, doub
 
 // factor + invert the m x m diagonal block at (b0, b0) of W (ld n); writes L_bb (lower) in
 // place and L_bb^{-1} to Linv (64 x 64, batch stride 4096)
-__global__ __launch_bounds__(64) void chol_diag_kernel(cplx* __restrict__ W, int n, long sW,
-                                                       int b0, int m,
-                                                       const double* __restrict__ thr,
-                                                       int* __restrict__ fail,
-                                                       cplx* __restrict__ Linv) {
+__global__ __launch_bounds__(256) void chol_diag_kernel(cplx* __restrict__ W, int n, long sW,
+                                                        int b0, int m,
+                                                        const double* __restrict__ thr,
+                                                        int* __restrict__ fail,
+                                                        cplx* __restrict__ Linv) {
+  // 256 threads: the block is loaded in one coalesced sweep (16 elements in flight per
+  // thread), every step's column scale / rank-1 update / substitution row is spread over the
+  // workgroup (the single-wave version spent ~1 ms per block on serial LDS chains)
   const int b = blockIdx.x;
   W += b * sW;
   Linv += (long)b * 4096;
@@ -703,36 +706,53 @@ __global__ __launch_bounds__(64) void chol_diag_kernel(cplx* __restrict__ W, int
   __shared__ int bad;
   const int t = threadIdx.x;
   if (t == 0) bad = 0;
-  for (int i = 0; i < m; ++i)
-    if (t < m) A[i][t] = W[(long)(b0 + i) * n + b0 + t];
+  {
+    cplx v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, i = e >> 6, j = e & 63;
+      v[u] = (i < m && j < m) ? W[(long)(b0 + i) * n + b0 + j] : cmk(0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, i = e >> 6, j = e & 63;
+      A[i][j] = v[u];
+      X[i][j] = cmk(i == j ? 1.0 : 0.0, 0.0);
+    }
+  }
   __syncthreads();
   const double th = thr[b];
   for (int k = 0; k < m; ++k) {
     const double dk = A[k][k].x;
-    if (t == 0 && !(dk > th)) bad = 1;
     const double lk = sqrt(fmax(dk, 1e-300));
-    __syncthreads();
+    __syncthreads();  // every thread has read A[k][k] before it is overwritten
     if (t > k && t < m) A[t][k] = cscale(A[t][k], 1.0 / lk);
     if (t == k) A[k][k] = cmk(lk, 0.0);
+    if (t == 0 && !(dk > th)) bad = 1;
     __syncthreads();
-    if (t > k && t < m)  // row t: A[t][j] -= A[t][k] conj(A[j][k]), k < j <= t
-      for (int j = k + 1; j <= t; ++j) A[t][j] = csub(A[t][j], cmul(A[t][k], cconj(A[j][k])));
-    __syncthreads();
-  }
-  // inverse of the lower-triangular block, column t by forward substitution
-  if (t < m) {
-    for (int i = 0; i < m; ++i) {
-      cplx sacc = cmk(i == t ? 1.0 : 0.0, 0.0);
-      for (int q = t; q < i; ++q) sacc = csub(sacc, cmul(A[i][q], X[q][t]));
-      const double d = A[i][i].x;
-      X[i][t] = i < t ? cmk(0, 0) : cscale(sacc, 1.0 / d);
+    // A[i][j] -= A[i][k] conj(A[j][k]),  k < j <= i < m
+    for (int e = t; e < 4096; e += 256) {
+      const int i = e >> 6, j = e & 63;
+      if (j > k && j <= i && i < m) A[i][j] = csub(A[i][j], cmul(A[i][k], cconj(A[j][k])));
     }
+    __syncthreads();  // the next step reads A[k+1][k+1] and column k+1
   }
-  __syncthreads();
-  for (int i = 0; i < m; ++i)
-    if (t < m && t <= i) W[(long)(b0 + i) * n + b0 + t] = A[i][t];
-  for (int i = 0; i < 64; ++i)
-    if (t < 64) Linv[i * 64 + t] = (i < m && t < m) ? X[i][t] : cmk(i == t ? 1.0 : 0.0, 0.0);
+  // inverse of the lower-triangular block: forward substitution on the identity, row k final
+  // once rows < k have been subtracted (same operation order as a per-column solve)
+  for (int k = 0; k < m; ++k) {
+    if (t < 64) X[k][t] = cscale(X[k][t], 1.0 / A[k][k].x);
+    __syncthreads();
+    for (int e = t; e < 4096; e += 256) {
+      const int i = e >> 6, c = e & 63;
+      if (i > k && i < m) X[i][c] = csub(X[i][c], cmul(A[i][k], X[k][c]));
+    }
+    __syncthreads();
+  }
+  for (int e = t; e < 4096; e += 256) {
+    const int i = e >> 6, j = e & 63;
+    if (i < m && j <= i) W[(long)(b0 + i) * n + b0 + j] = A[i][j];
+    Linv[e] = (i < m && j < m) ? X[i][j] : cmk(i == j ? 1.0 : 0.0, 0.0);
+  }
   if (t == 0 && bad) fail[b] = 1;
 }
 
@@ -810,7 +830,7 @@ int chol_unpivoted(hipStream_t s, cplx* W, int n, int batch, double tol_rel, int
   const cplx one = cmk(1, 0), mone = cmk(-1, 0), zero = cmk(0, 0);
   for (int b0 = 0; b0 < n; b0 += 64) {
     const int m = std::min(64, n - b0), b1 = b0 + m;
-    hipLaunchKernelGGL(chol_diag_kernel, dim3(batch), dim3(64), 0, s, W, n, nn, b0, m, thr, fail,
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(batch), dim3(256), 0, s, W, n, nn, b0, m, thr, fail,
                        Linv);
     FISDF_HIP(hipGetLastError());
     if (b1 < n) {

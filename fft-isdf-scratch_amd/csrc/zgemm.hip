@@ -98,6 +98,24 @@ __device__ __forceinline__ void zgemm_epilogue(int M, int N, cplx alpha, cplx be
     return;
   }
   C += (long)bz * sC;
+  if (epi == EPI_STREAM) {
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
+          int col = n0 + wn + ni * 16 + (lane & 15);
+          if (((mask >> (mi * 2 + ni)) & 1) && row < M && col < N) {
+            const cplx v = cmul(alpha, cmk(accR[mi][ni][r], accI[mi][ni][r]));
+            double* cp = (double*)(C + (long)row * ldc + col);
+            __builtin_nontemporal_store(v.x, cp);
+            __builtin_nontemporal_store(v.y, cp + 1);
+          }
+        }
+    return;
+  }
   if (epi == EPI_SQUARE_RE) {
     // y_s = Re(alpha acc)^2 + 0i, fused (fftisdf.py:83); monitor max|Im| (fftisdf.py:81)
     double mi_ = 0.0;
@@ -442,8 +460,10 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
       const int cur = s % NST;
       const cplx* as = sm + (long)(cur * 2 + 0) * TILE;
       const cplx* bs = sm + (long)(cur * 2 + 1) * TILE;
+      const int kleft = kend - kbeg - s * BK;  // K-substeps past the end hold only zeros
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 4) {
+        if (kk > 0 && kk >= kleft) break;
         const int k = kk + kq;
         cplx a[2], b[2];
 #pragma unroll

@@ -63,3 +63,13 @@ if "--herk-shapes" in sys.argv:
             ms = timeit(lambda: ctx.call("fisdf_zgemm", 0, 3, n, n, N, one, L.ptr(An), N, 0, L.ptr(An), N, 0,
                                          zero, L.ptr(Cn), n, 0, 1, ks))
             print(f"zgemm NC n={n} K={N} ks={ks}: {ms:.3f} ms  {8.0 * n * n * N / ms / 1e9:.1f} TF/s", flush=True)
+if "--fx" in sys.argv:
+    # the y build's fx GEMM: FX[k] (nip x gb) = X_k (nip x nao) f_k^H, 48 k of a 4x4x4 mesh
+    nip, nao, gb, nks = 600, 26, 2330, 48
+    Xk = rnd(nks, nip, nao)
+    fk = rnd(nks, gb, nao)
+    FX = torch.empty(nks, nip, gb, dtype=torch.complex128, device=dev)
+    ms = timeit(lambda: ctx.call("fisdf_zgemm", 0, 3, nip, gb, nao, one, L.ptr(Xk), nao, nip * nao,
+                                 L.ptr(fk), nao, gb * nao, zero, L.ptr(FX), gb, nip * gb, nks, 1))
+    print(f"fx gemm nip={nip} gb={gb} nao={nao} batch={nks}: {ms:.3f} ms  "
+          f"{FX.numel() * 16 / ms / 1e6:.0f} GB/s written", flush=True)
