@@ -670,6 +670,33 @@ int fisdf_unpack_slices(fisdf_ctx* c, const void* recv, int nrows, int nparts, c
   return 0;
 }
 
+// ---- input layer: Bloch AO values -------------------------------------
+int fisdf_eval_ao(fisdf_ctx* c, const void* d_coords, int ng, int natm, const double* h_atoms,
+                  int nsh, const int* h_sh_atom, const int* h_sh_l, const int* h_sh_nprim,
+                  const double* h_exps, const double* h_coefs, int nT, const int* h_tn,
+                  const int* kmesh, const double* a, double rcut, int nao, void* d_out) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(kmesh && kmesh[0] > 0 && kmesh[1] > 0 && kmesh[2] > 0, "eval_ao: bad k-mesh");
+  StageTimer tm(c, FISDF_ST_AO);
+  int nao_sh = 0;
+  for (int i = 0; i < nsh; ++i) nao_sh += 2 * h_sh_l[i] + 1;
+  FISDF_CHECK(nao_sh == nao, "eval_ao: nao does not match the shells");
+  const int nimg = kmesh[0] * kmesh[1] * kmesh[2];
+  Carver cv;
+  const size_t oF = cv.take(sizeof(double) * (size_t)nimg * ng * nao);
+  const size_t tables = 1 << 20;
+  const size_t oT = cv.take(tables + sizeof(double) * 3 * (size_t)std::max(nT, 1));
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  char* b = (char*)base;
+  int nao_out = 0;
+  FISDF_TRY(eval_ao(c->stream, (const double*)d_coords, ng, natm, h_atoms, nsh, h_sh_atom,
+                    h_sh_l, h_sh_nprim, h_exps, h_coefs, nT, h_tn, kmesh, a, rcut,
+                    (double*)(b + oF), b + oT, tables + sizeof(double) * 3 * (size_t)std::max(nT, 1),
+                    (cplx*)d_out, &nao_out));
+  return 0;
+}
+
 int fisdf_gather_points(fisdf_ctx* c, const void* x0, int nk, int ng0, int nao, const int* h_perm,
                         int nip, void* X) {
   FISDF_TRY(device_guard(c));

@@ -16,7 +16,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfisdf%s.so" % (
     "_" + os.environ["FISDF_LIB_VARIANT"] if os.environ.get("FISDF_LIB_VARIANT") else ""))
 
-STAGES = ["select", "x4", "y", "factor", "fft", "trsm", "herk", "small", "get_j", "get_k", "ws"]
+STAGES = ["select", "x4", "y", "factor", "fft", "trsm", "herk", "small", "get_j", "get_k", "ws",
+          "ao"]
 
 _lib = None
 
@@ -42,6 +43,8 @@ _SIGS = {
     "fisdf_max_imag": ([_vp, _dp], _i),
     "fisdf_select_points": ([_vp, _vp, _i, _i, _i, _i, _d, _ip, _ip, _ip], _i),
     "fisdf_gather_points": ([_vp, _vp, _i, _i, _i, _ip, _i, _vp], _i),
+    "fisdf_eval_ao": ([_vp, _vp, _i, _i, _dp, _i, _ip, _ip, _ip, _dp, _dp, _i, _ip, _ip, _dp, _d,
+                       _i, _vp], _i),
     "fisdf_select_gram": ([_vp, _vp, _i, _i, _i, _i, _i, _vp], _i),
     "fisdf_select_pivots": ([_vp, _vp, _i, _i, _i, _d, _ip, _ip, _ip], _i),
     "fisdf_unpack_slices": ([_vp, _vp, _i, _i, C.POINTER(_l), C.POINTER(_l), _l, _vp], _i),

@@ -218,6 +218,21 @@ def get_phase(cell, kmesh):
     return np.exp(1j * ts @ kpts.T) / np.sqrt(nk)
 
 
+def lattice_translations(cell, coords):
+    """Lattice translations n (T = n @ a) that can bring an atom within ``rcut`` of the grid
+    (the box of eval_ao_folded), cartesian order."""
+    coords = np.asarray(coords, float)
+    b = cell.reciprocal_vectors()
+    rc = cell.rcut()
+    frac = coords @ b.T / (2 * np.pi)   # grid extent in fractional coords (may be wrapped)
+    fmin, fmax = frac.min(axis=0), frac.max(axis=0)
+    reach = rc * np.linalg.norm(b, axis=1) / (2 * np.pi)
+    afrac = cell.atom_coords() @ b.T / (2 * np.pi)
+    lo = np.floor(fmin - afrac.max(axis=0) - reach).astype(int) - 1
+    hi = np.ceil(fmax - afrac.min(axis=0) + reach).astype(int) + 1
+    return cartesian_prod([np.arange(lo[i], hi[i] + 1) for i in range(3)])
+
+
 def eval_ao_folded(cell, coords, kmesh):
     """F_R(r) = sum_{T == T_R mod kmesh} phi(r - T), real, shape (nimg, ng, nao).
 
@@ -229,22 +244,14 @@ def eval_ao_folded(cell, coords, kmesh):
     nimg = int(np.prod(kmesh))
     nao = cell.nao_nr()
     a = cell.lattice_vectors()
-    b = cell.reciprocal_vectors()
     rc = cell.rcut()
-    # grid extent in fractional coords (coords may be wrapped)
-    frac = coords @ b.T / (2 * np.pi)
-    fmin, fmax = frac.min(axis=0), frac.max(axis=0)
-    reach = rc * np.linalg.norm(b, axis=1) / (2 * np.pi)
     out = np.zeros((nimg, ng, nao))
     atom_xyz = cell.atom_coords()
-    afrac = atom_xyz @ b.T / (2 * np.pi)
-    lo = np.floor(fmin - afrac.max(axis=0) - reach).astype(int) - 1
-    hi = np.ceil(fmax - afrac.min(axis=0) + reach).astype(int) + 1
     rc2 = rc * rc
     shells_by_atom = {}
     for sh in cell.shells:
         shells_by_atom.setdefault(sh[0], []).append(sh)
-    for n in cartesian_prod([np.arange(lo[i], hi[i] + 1) for i in range(3)]):
+    for n in lattice_translations(cell, coords):
         T = n @ a
         R = tuple(int(x) % int(k) for x, k in zip(n, kmesh))
         ridx = (R[0] * kmesh[1] + R[1]) * kmesh[2] + R[2]

@@ -106,6 +106,8 @@ class InterpolativeSeparableDensityFitting:
     # x4_q factorisation: None = library default (unpivoted blocked Cholesky when every x4_q
     # is numerically full rank, else the greedy pivoted one); True forces the pivoted path
     pivoted_fit = None
+    # Bloch AO inputs evaluated on the GPU (fisdf_eval_ao) instead of the host restatement
+    ao_on_gpu = True
 
     def __init__(self, cell, kpts, m0=None, c0=20.0, device=None, comm=None):
         self.cell = cell
@@ -135,16 +137,22 @@ class InterpolativeSeparableDensityFitting:
     def grids_coords(self):
         return self.cell.gen_uniform_grids(self.mesh)
 
-    def preload_ao(self):
-        """Evaluate and upload the AO inputs (PySCF's job in the reference) before build."""
+    def _eval_ao(self, coords):
+        """Bloch AOs at ``coords`` on the device: the GPU evaluator (ao_on_gpu, default) or
+        the host restatement uploaded (cells without ``shells``, e.g. a PySCF cell, use the
+        host path through ``eval_ao_kpts``)."""
         kmesh = self._kmesh()
-        d = self.device
+        if self.ao_on_gpu and hasattr(self.cell, "shells"):
+            from .ao import eval_ao_kpts_gpu
+            return eval_ao_kpts_gpu(self.device, self.cell, coords, kmesh)
+        return self.device.to_dev(eval_ao_kpts(self.cell, coords, kmesh))
+
+    def preload_ao(self):
+        """Evaluate the AO inputs (PySCF's job in the reference) on the device before build."""
         if self._ao_parent is None:
-            x0 = eval_ao_kpts(self.cell, self.cell.gen_uniform_grids(self.m0), kmesh)
-            self._ao_parent = d.to_dev(x0)
+            self._ao_parent = self._eval_ao(self.cell.gen_uniform_grids(self.m0))
         if self._ao_grid is None:
-            f = eval_ao_kpts(self.cell, self.grids_coords(), kmesh)
-            self._ao_grid = d.to_dev(f)
+            self._ao_grid = self._eval_ao(self.grids_coords())
         return self
 
     def _kmesh(self):
@@ -180,8 +188,7 @@ class InterpolativeSeparableDensityFitting:
         nk = int(np.prod(kmesh))
         nao = self.cell.nao_nr()
         if self._ao_parent is None:
-            x0 = eval_ao_kpts(self.cell, self.cell.gen_uniform_grids(self.m0), kmesh)
-            self._ao_parent = d.to_dev(x0)
+            self._ao_parent = self._eval_ao(self.cell.gen_uniform_grids(self.m0))
         x0 = self._ao_parent
         ng0 = x0.shape[1]
         nip_max = min(int(nao * self.c0), ng0)
@@ -219,8 +226,7 @@ class InterpolativeSeparableDensityFitting:
         nk = int(np.prod(kmesh))
         nao = self.cell.nao_nr()
         if self._ao_parent is None:
-            x0 = eval_ao_kpts(self.cell, self.cell.gen_uniform_grids(self.m0), kmesh)
-            self._ao_parent = d.to_dev(x0)
+            self._ao_parent = self._eval_ao(self.cell.gen_uniform_grids(self.m0))
         x0 = self._ao_parent
         self.perm = np.ascontiguousarray(perm, dtype=np.int32)
         nip = len(self.perm)
@@ -393,7 +399,7 @@ def build(df_obj):
     nq = len(my_qs)
     qs_c = my_qs.ctypes.data_as(_lib._ip)
     if df_obj._ao_grid is None:
-        df_obj._ao_grid = d.to_dev(eval_ao_kpts(cell, df_obj.grids_coords(), kmesh))
+        df_obj._ao_grid = df_obj._eval_ao(df_obj.grids_coords())
     f = df_obj._ao_grid
     # x4_q factorisation (replaces zgelsy's QRCP, :108) on the library's side stream,
     # overlapped with the y build enqueued next on the main stream

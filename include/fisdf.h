@@ -42,7 +42,8 @@ enum {
   FISDF_ST_J = 8,      /* get_j_kpts (fftisdf.py:133-171)                         */
   FISDF_ST_K = 9,      /* get_k_kpts (fftisdf.py:173-228)                         */
   FISDF_ST_WS = 10,    /* W_s = Re(Phi W) sqrt(nk) (fftisdf.py:204-207)           */
-  FISDF_NSTAGES = 11
+  FISDF_ST_AO = 11,    /* Bloch AO values (input layer, fftisdf.py:72,367-370)    */
+  FISDF_NSTAGES = 12
 };
 
 /* ---- context / memory ---------------------------------------------------- */
@@ -60,6 +61,20 @@ int fisdf_timings(fisdf_ctx* ctx, double* h_ms /* FISDF_NSTAGES */, int* h_calls
 /* reality invariants, max |Im| seen since the last call: [0] x2_s (fftisdf.py:43),
  * [1] fx_s (fftisdf.py:81), [2] rho_s (fftisdf.py:216).  synchronous; resets. */
 int fisdf_max_imag(fisdf_ctx* ctx, double* h_out /* 3 */);
+
+/* ---- input layer: Bloch AO values ------------------------
+ * Replaces PySCF pbc_eval_gto('GTOval', coords, kpts) / KNumInt.block_loop as called at
+ * fftisdf.py:72,327-355,367-370 (restated on the host by fisdf/cell.py eval_ao_kpts):
+ *   chi_k(r_g)[nu] = sum_{T = n.a} exp(i k.T) phi_nu(r_g - T)
+ * for contracted real-spherical Gaussian shells (l <= 3, cell.py's harmonics and order).
+ * d_coords (ng, 3) f64 device; h_atoms (natm, 3); shells: atom, l, nprim, then the nprim
+ * exponents / normalised coefficients of each shell in order; h_tn (nT, 3) the lattice
+ * translations n to sum (T = n @ a, image R = n mod kmesh); terms with |r - T - atom| >= rcut
+ * are dropped.  d_out (nk, ng, nao) c128, nk = prod(kmesh), kpts = make_kpts order. */
+int fisdf_eval_ao(fisdf_ctx* ctx, const void* d_coords, int ng, int natm, const double* h_atoms,
+                  int nsh, const int* h_sh_atom, const int* h_sh_l, const int* h_sh_nprim,
+                  const double* h_exps, const double* h_coefs, int nT, const int* h_tn,
+                  const int kmesh[3], const double a[9], double rcut, int nao, void* d_out);
 
 /* ---- A1: interpolation-point selection ------------------------------------
  * Replaces InterpolativeSeparableDensityFitting.select_interpolation_points
