@@ -258,6 +258,11 @@ def main():
             "ranks": [int(ranks.min()), int(ranks.max())],
         }
         print(json.dumps(out))
+    # release the library context (streams, arena, factors) while the HIP runtime and any
+    # attached profiler are still up, not from an interpreter-shutdown finaliser
+    torch.cuda.synchronize()
+    del df
+    d.ctx.close()
     if comm is not None:
         torch.distributed.destroy_process_group()
 
