@@ -311,6 +311,9 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx al
 // lane-linear per wave-instruction (dest = base + lane*16); the K-contiguous operands keep
 // their XOR swizzle by permuting the per-lane SOURCE address instead.  Out-of-range lanes
 // read a zero page; conjugation is folded into the MFMA operand signs.
+#ifndef FISDF_GEMM_3M
+#define FISDF_GEMM_3M 1  // 3 real MFMAs per complex block in FULL mode (0: the 4-product form)
+#endif
 #ifndef FISDF_NST
 #define FISDF_NST 3
 #endif
@@ -423,13 +426,18 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
     }
   };
 
-  f64x4 accR[2][2], accI[2][2];
+  // FULL mode, 3 real products per complex block (FISDF_GEMM_3M): accR = P1 = ar br,
+  // accI = P2 = ai' bi', acc3 = P3 = (ar + ai')(br + bi'); Re = P1 - P2, Im = P3 - P1 - P2
+  // after the K loop (tests/experiments/three_mult.py: J/K unchanged to the last digit shown)
+  constexpr bool M3 = FISDF_GEMM_3M && MODE == GEMM_FULL;
+  f64x4 accR[2][2], accI[2][2], acc3[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       accR[i][j] = f64x4{0, 0, 0, 0};
       accI[i][j] = f64x4{0, 0, 0, 0};
+      acc3[i][j] = f64x4{0, 0, 0, 0};
     }
 
   int mask = 0;
@@ -483,6 +491,33 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
           bi[u] = CB ? -b[u].y : b[u].y;
         }
         constexpr bool AREAL = (MODE & GEMM_A_REAL) != 0, REONLY = (MODE & GEMM_RE_ONLY) != 0;
+        if constexpr (M3) {
+          double as[2], bs[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            as[u] = ar[u] + ai[u];
+            bs[u] = br[u] + bi[u];
+          }
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+              if ((MASK >> (mi * 2 + ni)) & 1)
+                accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], accR[mi][ni], 0, 0, 0);
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+              if ((MASK >> (mi * 2 + ni)) & 1)
+                accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], bi[ni], accI[mi][ni], 0, 0, 0);
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+              if ((MASK >> (mi * 2 + ni)) & 1)
+                acc3[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(as[mi], bs[ni], acc3[mi][ni], 0, 0, 0);
+          continue;
+        }
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -526,6 +561,18 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
   }
   // drain the (zero-page / unused) loads still in flight before the workgroup exits
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (M3) {
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double p1 = accR[mi][ni][r], p2 = accI[mi][ni][r], p3 = acc3[mi][ni][r];
+          accR[mi][ni][r] = p1 - p2;
+          accI[mi][ni][r] = p3 - p1 - p2;
+        }
+  }
 
   zgemm_epilogue<HERK>(M, N, alpha, beta, C, ldc, sC, ksplit, split, bz, work, epi, mon, m0, n0, wm,
                        wn, lane, mask, accR, accI);
