@@ -321,7 +321,7 @@ constexpr int NST = FISDF_NST;  // LDS ring depth; loads run NST-1 K-steps ahead
 constexpr int LPW = TILE / (64 * 4);  // glds wave-instructions per operand per step per wave
 __device__ cplx g_zero_page[64];      // zero-initialised device global
 
-template <int OPA, int OPB, bool HERK, int MODE>
+template <int OPA, int OPB, bool HERK, int MODE, int NS>
 __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cplx alpha,
                                                          const cplx* __restrict__ A, long lda, long sA,
                                                          const cplx* __restrict__ B, long ldb, long sB,
@@ -334,7 +334,8 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
   constexpr bool CA = (OPA & 2) != 0, CB = (OPB & 2) != 0;
   typedef Stage<AK> SA;
   typedef Stage<BKc> SB;
-  __shared__ cplx sm[NST * 2 * TILE];  // [stage][A|B][TILE], one object (48 KB at BK = 8)
+  // [stage][A|B][TILE], one object (48 KB at BK = 8, NS = 3; NS = 2 for short K loops)
+  __shared__ cplx sm[NS * 2 * TILE];
 
   const int per = (int)(gridDim.x >> 3);
   const int order = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
@@ -412,8 +413,8 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
   };
-  auto issue = [&](int st) {  // K-step st -> ring slot st % NST
-    const int buf = st % NST;
+  auto issue = [&](int st) {  // K-step st -> ring slot st % NS
+    const int buf = st % NS;
     const int k0 = kbeg + st * BK;
     const unsigned la = lds0 + (unsigned)((buf * 2 + 0) * TILE) * 16u;
     const unsigned lb = lds0 + (unsigned)((buf * 2 + 1) * TILE) * 16u;
@@ -454,7 +455,7 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
   // (steps past the end load the zero page: the counted waits assume NST-1 steps in flight)
   if (nsteps > 0) {
 #pragma unroll
-    for (int st = 0; st < NST - 1; ++st) issue(st);
+    for (int st = 0; st < NS - 1; ++st) issue(st);
   }
   const int i16 = lane & 15, kq = lane >> 4;
   auto mainloop = [&](auto maskc) {
@@ -462,10 +463,10 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
     for (int s = 0; s < nsteps; ++s) {
       // own loads of step s retired (step s+1's 2*LPW stay in flight), then every wave's:
       // the barrier also retires all reads of the slot step s+2 is about to overwrite
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * LPW * (NST - 2)) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * LPW * (NS - 2)) : "memory");
       __builtin_amdgcn_sched_barrier(0);
-      issue(s + NST - 1);
-      const int cur = s % NST;
+      issue(s + NS - 1);
+      const int cur = s % NS;
       const cplx* as = sm + (long)(cur * 2 + 0) * TILE;
       const cplx* bs = sm + (long)(cur * 2 + 1) * TILE;
       const int kleft = kend - kbeg - s * BK;  // K-substeps past the end hold only zeros
@@ -612,8 +613,14 @@ void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cpl
   const int ntile = (int)(grid.x * (HERK ? 1 : grid.y));
   const long ntot = (long)ntile * grid.z;
   const long per = (ntot + 7) / 8;
-  if (gemm_variant() == 1 || MODE != GEMM_FULL)
-    hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE>), dim3((unsigned)(8 * per)), dim3(256), 0,
+  // short K loops (<= 4 steps per workgroup, e.g. the y build's K = nao): a 2-deep ring
+  // (32 KB of LDS) lets more workgroups share a CU, overlapping their load and store phases
+  if ((gemm_variant() == 1 || MODE != GEMM_FULL) && kchunk <= 4 * BK)
+    hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, 2>), dim3((unsigned)(8 * per)),
+                       dim3(256), 0, s, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
+                       ksplit, kchunk, work, epi, mon, nMt, ntile, (int)ntot);
+  else if (gemm_variant() == 1 || MODE != GEMM_FULL)
+    hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, NST>), dim3((unsigned)(8 * per)), dim3(256), 0,
                        s, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk,
                        work, epi, mon, nMt, ntile, (int)ntot);
   else
