@@ -753,12 +753,13 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
   const cplx* f = (const cplx*)fv;
   const cplx* X = (const cplx*)Xv;
   cplx* yT = (cplx*)yTv;
-  // grid sub-blocks of ~1 GB of FX temporary (swept on MI355X at C3: 1 GB 168.6 ms/step,
-  // 256 MB 170.7, 128 MB 172.2, 64 MB 176.8 — cache-sized blocks lose more to the smaller
-  // GEMM/DFT launches than they gain from Infinity-Cache residency)
+  // grid sub-blocks of ~2 GB of FX temporary (swept on MI355X at C3 after the half-k /
+  // short-K changes: y 28.1 / 22.7 / 20.9 / 18.4 / 16.7 ms for 128 MB / 256 MB / 512 MB /
+  // 1 GB / 2 GB — cache-sized blocks lose more to the smaller GEMM/DFT launches than they
+  // gain from Infinity-Cache residency; bigger blocks slow the side-stream factorisation)
   static const long yblk_bytes = [] {
     const char* e = getenv("FISDF_YBLK_MB");
-    return (e ? atol(e) : 1024L) << 20;
+    return (e ? atol(e) : 2048L) << 20;
   }();
   // time reversal (fisdf_set_time_reversal): fx_k only for the k-planes a <= n0/2, the
   // others are conj(fx_{-k}) inside kmesh_y — ~45% less FX traffic at 4x4x4
