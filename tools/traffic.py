@@ -10,8 +10,8 @@ import sys
 from collections import defaultdict
 
 KERNELS = {  # label: (name substring, grid-size filter on the largest launches)
-    "herk": "zgemm_glds_kernel<0, 3, true, 0>",
-    "trsm_gemm": "zgemm_glds_kernel<0, 0, false, 0>",
+    "herk": "zgemm_glds_kernel<0, 3, true, 0, 3>",
+    "trsm_gemm": "zgemm_glds_kernel<0, 0, false, 4, 3>",   # lower-triangular GEMM (GEMM_A_LOWER)
     "fft_plane": "fft_plane_reg<36>",
     "fft_axis0": "fft_axis0_reg<36>",
     "kmesh_y": "kmesh_y_reg_kernel<4, 4, 4>",
