@@ -1147,12 +1147,22 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     // zeros beyond each rank):  T = L^{-H} G ; S = L^{-H} T^H ; W_PP = S^H ; scatter by pivots
     const cplx* Lp0 = c->f_Lp + (long)s0 * nn;
     const cplx* Li0 = c->f_Linv + (long)s0 * sLi;
-    FISDF_TRY(trsm_blocked(c->stream, 0, Lp0, nip, nn, rmax, Li0, sLi, nb, G, rmax, rr,
-                           T, rmax, rr, rmax, nq));
-    FISDF_TRY(conj_transpose(c->stream, T, rmax, rr, G, nq));
-    FISDF_TRY(trsm_blocked(c->stream, 0, Lp0, nip, nn, rmax, Li0, sLi, nb, G, rmax, rr,
-                           S, rmax, rr, rmax, nq));
-    FISDF_TRY(conj_transpose(c->stream, S, rmax, rr, T, nq));
+    bool all_full = rmax == nip;
+    for (int lq = 0; lq < nq && all_full; ++lq) all_full = c->f_rank[s0 + lq] == nip;
+    if (all_full) {  // with L^{-1} at hand: T = G L^{-1}, W_PP = L^{-H} T (two batched GEMMs)
+      const cplx* Lf = c->f_Li + (long)s0 * nn;
+      FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nip, nip, nip, ONE, G, rmax, rr, Lf, nip, nn, ZERO,
+                      S, rmax, rr, nq, 1));
+      FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nip, nip, nip, ONE, Lf, nip, nn, S, rmax, rr, ZERO,
+                      T, rmax, rr, nq, 1));
+    } else {
+      FISDF_TRY(trsm_blocked(c->stream, 0, Lp0, nip, nn, rmax, Li0, sLi, nb, G, rmax, rr,
+                             T, rmax, rr, rmax, nq));
+      FISDF_TRY(conj_transpose(c->stream, T, rmax, rr, G, nq));
+      FISDF_TRY(trsm_blocked(c->stream, 0, Lp0, nip, nn, rmax, Li0, sLi, nb, G, rmax, rr,
+                             S, rmax, rr, rmax, nq));
+      FISDF_TRY(conj_transpose(c->stream, S, rmax, rr, T, nq));
+    }
     FISDF_TRY(scatter_w(c->stream, T, rmax, rr, rmax, c->f_piv + (long)s0 * nip,
                         c->f_rank_dev + s0, Wq, nip, nq));
   }

@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
   // FULL mode, 3 real products per complex block (FISDF_GEMM_3M): accR = P1 = ar br,
   // accI = P2 = ai' bi', acc3 = P3 = (ar + ai')(br + bi'); Re = P1 - P2, Im = P3 - P1 - P2
   // after the K loop (tests/experiments/three_mult.py: J/K unchanged to the last digit shown)
-  constexpr bool M3 = FISDF_GEMM_3M && MODE == GEMM_FULL;
+  constexpr bool M3 = FISDF_GEMM_3M && (MODE & (GEMM_A_REAL | GEMM_RE_ONLY)) == 0;
   f64x4 accR[2][2], accI[2][2], acc3[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
