@@ -60,7 +60,8 @@ struct fisdf_ctx {
   std::vector<int> f_rank;  // host copy
   // the factorisation runs on a side stream, overlapped with the y build on `stream`
   hipStream_t side = nullptr;
-  hipEvent_t ev_x4 = nullptr, ev_fac = nullptr;
+  hipEvent_t ev_x4 = nullptr, ev_fac = nullptr, ev_chol = nullptr;
+  bool f_fac_unjoined = false;  // ev_fac not yet waited on by the main stream (fit lanes do)
   bool f_pending = false;
   int* f_rank_pinned = nullptr;  // host (pinned) copy target, f_nk ints
   void* f_scratch = nullptr;     // device scratch of the factorisation
@@ -403,6 +404,7 @@ int fisdf_destroy(fisdf_ctx* c) {
     (void)hipStreamDestroy(c->side);
     (void)hipEventDestroy(c->ev_x4);
     (void)hipEventDestroy(c->ev_fac);
+    (void)hipEventDestroy(c->ev_chol);
   }
   if (c->ev_fork) {
     (void)hipEventDestroy(c->ev_fork);
@@ -813,6 +815,10 @@ int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src) {
   const long nn = (long)nip * nip;
   FISDF_HIP(hipMemcpyAsync(c->f_rank_pinned, rank_dev_src, sizeof(int) * nk, hipMemcpyDeviceToHost, s));
   FISDF_HIP(hipMemcpyAsync(c->f_rank_dev, rank_dev_src, sizeof(int) * nk, hipMemcpyDeviceToDevice, s));
+  // ranks and pivots are known here: fisdf_factor_x4_wait returns on this event, and the fit
+  // starts its FFTs while the operators below are still being built (it waits on ev_fac
+  // per lane before its first TRSM)
+  FISDF_HIP(hipEventRecord(c->ev_chol, s));
   FISDF_TRY(gather_lp(s, c->f_L, nip, nip, c->f_piv, c->f_rank_dev, nip, c->f_Lp, nk));
   FISDF_TRY(trinv_blocks(s, c->f_Lp, nip, nip, nn, nb, (long)nblk * nb * nb, c->f_Linv, nk));
   FISDF_TRY(build_trsm_q(s, c->f_Lp, nip, nn, c->f_Q, nk, GEMM_FULL));
@@ -856,9 +862,16 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   FISDF_TRY(check_qlist(h_qs, nq, 1 << 30, "factor_x4"));
   if (c->f_pending) FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
   if (!c->side) {
-    FISDF_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    // FISDF_SIDE_PRIO=1: the factorisation (a chain of small kernels beside the y build's
+    // large ones) on a high-priority stream
+    const char* pe = getenv("FISDF_SIDE_PRIO");
+    int lo = 0, hi = 0;
+    FISDF_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    FISDF_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking,
+                                          (pe && pe[0] == '1') ? hi : lo));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_x4, hipEventDisableTiming));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_fac, hipEventDisableTiming));
+    FISDF_HIP(hipEventCreateWithFlags(&c->ev_chol, hipEventDisableTiming));
   }
   const int nb = c->f_nb;
   const int nblk = (nip + nb - 1) / nb;
@@ -964,7 +977,10 @@ int fisdf_factor_info(fisdf_ctx* c, int* h_used_pivoted) {
 int fisdf_factor_x4_wait(fisdf_ctx* c, int* h_ranks) {
   FISDF_TRY(device_guard(c));
   if (c->f_pending) {
-    FISDF_HIP(hipEventSynchronize(c->ev_fac));
+    // ranks, pivots and the full-rank verdict are ready at ev_chol; the operators built
+    // after it (L^-1 etc.) are waited for on the device (ev_fac, by the fit)
+    FISDF_HIP(hipEventSynchronize(c->ev_chol));
+    bool redone = false;
     if (c->f_check_fail) {
       bool any = false;
       for (int q = 0; q < c->f_nk; ++q) any |= c->f_fail_pinned[q] != 0;
@@ -973,10 +989,12 @@ int fisdf_factor_x4_wait(fisdf_ctx* c, int* h_ranks) {
         FISDF_TRY(factor_pivoted(c, c->side));
         FISDF_HIP(hipEventRecord(c->ev_fac, c->side));
         FISDF_HIP(hipEventSynchronize(c->ev_fac));
+        redone = true;
       }
     }
     c->f_rank.assign(c->f_rank_pinned, c->f_rank_pinned + c->f_nk);
-    FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_fac, 0));  // factors before any later use
+    if (redone) FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_fac, 0));
+    c->f_fac_unjoined = !redone;
     c->f_pending = false;
   }
   if (h_ranks)
@@ -984,10 +1002,20 @@ int fisdf_factor_x4_wait(fisdf_ctx* c, int* h_ranks) {
   return 0;
 }
 
+// the main stream waits for every factor operator (the fit joins per lane instead)
+static int join_factors(fisdf_ctx* c) {
+  if (c->f_fac_unjoined) {
+    FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_fac, 0));
+    c->f_fac_unjoined = false;
+  }
+  return 0;
+}
+
 int fisdf_factor_x4_qs(fisdf_ctx* c, const void* x4all, const int* h_qs, int nq, int nip,
                        double tol_rel, const int* kmesh, int* h_ranks) {
   FISDF_TRY(fisdf_factor_x4_async(c, x4all, h_qs, nq, nip, tol_rel, kmesh));
-  return fisdf_factor_x4_wait(c, h_ranks);
+  FISDF_TRY(fisdf_factor_x4_wait(c, h_ranks));
+  return join_factors(c);
 }
 
 int fisdf_factor_x4(fisdf_ctx* c, const void* x4v, int q0, int q1, int nip, double tol_rel,
@@ -1053,6 +1081,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   cplx* T = (cplx*)(b + oT);
   cplx* S = (cplx*)(b + oS);
   if (rmax == 0) {
+    FISDF_TRY(join_factors(c));
     FISDF_HIP(hipMemsetAsync(Wq, 0, sizeof(cplx) * nq * nn, c->stream));
     return 0;
   }
@@ -1094,6 +1123,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
                       mesh[1], mesh[2], kd, wt, nullptr));
     }
     cplx* Uq = U;  // where L^{-1} Yh lands
+    if (c->f_fac_unjoined) FISDF_HIP(hipStreamWaitEvent(st, c->ev_fac, 0));  // L^-1, Q, ...
     {
       StageTimer tm(c, FISDF_ST_TRSM, st);
       // U = L^{-1} Yh   (fit, factored order; (x4_q)_PP = L L^H)
@@ -1141,6 +1171,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     FISDF_HIP(hipEventRecord(c->ev_join[l - 1], lane_st[l]));
     FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_join[l - 1], 0));
   }
+  FISDF_TRY(join_factors(c));
   {
     StageTimer tm(c, FISDF_ST_SMALL);
     // W_PP = L^{-H} G L^{-1} for all q of the shard at once (L padded with identity, G with
