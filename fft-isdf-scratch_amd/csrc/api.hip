@@ -55,6 +55,7 @@ struct fisdf_ctx {
   // extra streams of the fit lanes (fisdf_fit_coulomb_qs)
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev_ybuf[4] = {nullptr, nullptr, nullptr, nullptr};  // y pipeline: fx ready / free
   int* f_piv = nullptr;     // (nk, nip)
   int* f_rank_dev = nullptr;
   std::vector<int> f_rank;  // host copy
@@ -309,6 +310,7 @@ int ensure_aux(fisdf_ctx* c) {
     FISDF_HIP(hipStreamCreateWithFlags(&c->aux[l], hipStreamNonBlocking));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_join[l], hipEventDisableTiming));
   }
+  for (int l = 0; l < 4; ++l) FISDF_HIP(hipEventCreateWithFlags(&c->ev_ybuf[l], hipEventDisableTiming));
   return 0;
 }
 
@@ -413,6 +415,7 @@ int fisdf_destroy(fisdf_ctx* c) {
       (void)hipStreamDestroy(c->aux[l]);
       (void)hipEventDestroy(c->ev_join[l]);
     }
+    for (int l = 0; l < 4; ++l) (void)hipEventDestroy(c->ev_ybuf[l]);
   }
   if (c->arena) (void)hipFree(c->arena);
   if (c->ev_stage) (void)hipEventSynchronize(c->ev_stage), (void)hipEventDestroy(c->ev_stage);
@@ -772,27 +775,56 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
   const long per_g = (long)nks * nip * sizeof(cplx);
   int gb = (int)std::max(64L, std::min<long>(nblk, yblk_bytes / std::max(per_g, 1L)));
   gb = std::min(gb, std::max(nblk, 1));
+  // pipelined (FISDF_Y_PIPE, default on): the fx GEMM of block i+1 (main stream) runs beside
+  // the k-mesh DFT of block i (aux stream) on two fx buffers — the GEMM is write/compute
+  // bound, the DFT read/write bound, and neither alone saturates HBM
+  static const bool pipe_env = [] {
+    const char* e = getenv("FISDF_Y_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  const int nbuf = pipe_env && gb < nblk ? 2 : 1;
   Carver cv;
-  size_t o1 = cv.take((size_t)per_g * gb);
+  size_t o1[2];
+  for (int i = 0; i < nbuf; ++i) o1[i] = cv.take((size_t)per_g * gb);
   size_t oq = cv.take(sizeof(int) * (size_t)nq);
   void* base;
   FISDF_TRY(arena_get(c, cv.off, &base));
-  cplx* FX = (cplx*)((char*)base + o1);
   int* dq = (int*)((char*)base + oq);
   FISDF_TRY(upload_ints(c, h_qs, nq, dq));
-  for (int s0 = 0; s0 < nblk; s0 += gb) {
+  hipStream_t sk = c->stream;
+  if (nbuf == 2) {
+    FISDF_TRY(ensure_aux(c));
+    sk = c->aux[0];
+    FISDF_HIP(hipEventRecord(c->ev_fork, c->stream));
+    FISDF_HIP(hipStreamWaitEvent(sk, c->ev_fork, 0));
+  }
+  static const int fx_epi = getenv("FISDF_FX_NT") && getenv("FISDF_FX_NT")[0] == '0'
+                                ? EPI_NONE : EPI_STREAM;
+  int blk = 0;
+  for (int s0 = 0; s0 < nblk; s0 += gb, ++blk) {
     const int m = std::min(gb, nblk - s0);
     const long nm = (long)nip * m;
+    const int bi = blk % nbuf;
+    cplx* FX = (cplx*)((char*)base + o1[bi]);
+    // buffer bi is free once the DFT of block blk-2 has read it
+    if (nbuf == 2 && blk >= 2) FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_ybuf[2 + bi], 0));
     // fx_k^T = X_k f_k^H  -> FX[k][I][g]   (:76, transposed layout)
-    static const int fx_epi = getenv("FISDF_FX_NT") && getenv("FISDF_FX_NT")[0] == '0'
-                                  ? EPI_NONE : EPI_STREAM;
     FISDF_TRY(zgemm(c->stream, OP_N, OP_C, nip, m, nao, ONE, X, nao, (long)nip * nao,
                     f + (long)s0 * nao, nao, f_kstride, ZERO, FX, m, nm, nks, 1, nullptr,
                     fx_epi));
+    if (nbuf == 2) {
+      FISDF_HIP(hipEventRecord(c->ev_ybuf[bi], c->stream));
+      FISDF_HIP(hipStreamWaitEvent(sk, c->ev_ybuf[bi], 0));
+    }
     // fx_s = Phi fx_k (:79, real :81), y_s = fx_s^2 (:83), y_k = Phi^T y_s (:84) for the
     // listed q, written into yT[slot][I][g0+s0+g] (:85): separable k-mesh DFTs
-    FISDF_TRY(kmesh_y(c->stream, FX, nm, kmesh, h_qs, dq, nq, m, yT, (long)nip * ngrid, ngrid,
+    FISDF_TRY(kmesh_y(sk, FX, nm, kmesh, h_qs, dq, nq, m, yT, (long)nip * ngrid, ngrid,
                       (long)g0 + s0, half, c->maximag + 1));
+    if (nbuf == 2) FISDF_HIP(hipEventRecord(c->ev_ybuf[2 + bi], sk));
+  }
+  if (nbuf == 2) {  // later work on the main stream (the fit, the arena's next user) sees y
+    FISDF_HIP(hipEventRecord(c->ev_join[0], sk));
+    FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_join[0], 0));
   }
   return 0;
 }
