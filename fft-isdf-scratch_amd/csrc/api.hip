@@ -297,7 +297,7 @@ int get_asym(fisdf_ctx* c, hipStream_t st, const int mesh[3], const int kmesh[3]
 int env_fit_lanes() {
   static const int n = [] {
     const char* e = getenv("FISDF_FIT_LANES");
-    const int v = e ? atoi(e) : 3;
+    const int v = e ? atoi(e) : 2;
     return std::max(1, std::min(4, v));
   }();
   return n;

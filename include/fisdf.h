@@ -167,7 +167,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* ctx, const int* h_qs, int nq, const void* d_
                          const int mesh[3], const int kmesh[3], const double a[9], void* d_Wq);
 /* Fit lanes: the q of one fisdf_fit_coulomb_qs call are spread round-robin over `lanes`
  * streams with private workspaces (one q's memory-bound FFT/HERK overlaps another's
- * MFMA-bound TRSM); 0 (default): FISDF_FIT_LANES from the environment, else 3.  Results do
+ * MFMA-bound TRSM); 0 (default): FISDF_FIT_LANES from the environment, else 2.  Results do
  * not depend on it (same kernels, same per-q arithmetic). */
 int fisdf_set_fit_lanes(fisdf_ctx* ctx, int lanes);
 /* Time reversal of the inputs (real AOs, k-mesh closed under k -> -k): f_{-k} = conj(f_k)
