@@ -52,10 +52,9 @@ enum Op { OP_N = 0, OP_T = 1, OP_R = 2 /*conj only*/, OP_C = 3 /*conj-transpose*
 // ---- kernels (launchers return 0 or negative; all asynchronous on `stream`)
 // C[b] = alpha * op(A[b]) * op(B[b]) + beta * C[b]; lda/ldb/ldc in complex elements,
 // strides sA/sB/sC per batch in complex elements. ksplit>1 uses `work` (ksplit*M*N cplx).
-// epilogues: EPI_SQUARE_RE writes Re(alpha*acc)^2 + 0i and records max|Im| into *mon
-// EPI_STREAM: C = alpha acc (beta = 0) with non-temporal stores (a large output read back
-// only much later, e.g. the y build's fx blocks)
-enum Epi { EPI_NONE = 0, EPI_SQUARE_RE = 1, EPI_STREAM = 2 };
+// epilogues: EPI_STREAM: C = alpha acc (beta = 0) with non-temporal stores (a large output
+// read back only much later, e.g. the y build's fx blocks)
+enum Epi { EPI_NONE = 0, EPI_STREAM = 2 };
 // arithmetic modes (MFMA work skipped): GEMM_A_REAL: Im(op(A)) is taken as zero (2 of the 4
 // real MFMAs per complex block); GEMM_RE_ONLY: only Re(C) is formed (Im(C) written as 0).
 // Supported for (N,N), (C,N) and the HERK; other op pairs require mode 0.

@@ -116,28 +116,6 @@ __device__ __forceinline__ void zgemm_epilogue(int M, int N, cplx alpha, cplx be
         }
     return;
   }
-  if (epi == EPI_SQUARE_RE) {
-    // y_s = Re(alpha acc)^2 + 0i, fused (fftisdf.py:83); monitor max|Im| (fftisdf.py:81)
-    double mi_ = 0.0;
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
-          int col = n0 + wn + ni * 16 + (lane & 15);
-          if (((mask >> (mi * 2 + ni)) & 1) && row < M && col < N) {
-            cplx v = cmul(alpha, cmk(accR[mi][ni][r], accI[mi][ni][r]));
-            C[(long)row * ldc + col] = cmk(v.x * v.x, 0.0);
-            mi_ = fmax(mi_, fabs(v.y));
-          }
-        }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mi_ = fmax(mi_, __shfl_xor(mi_, o, 64));
-    if (lane == 0 && mon) atomicMax(mon, (unsigned long long)__double_as_longlong(mi_));
-    return;
-  }
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
