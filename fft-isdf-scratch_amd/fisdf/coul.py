@@ -1,0 +1,193 @@
+"""Script surface of the reference's ``get_coul`` drivers.
+
+The reference's k-point ISDF scripts expose one function, ``get_coul(df_obj, ...) ->
+(coul_q, x_k)``, and a check loop that compares ISDF ERIs against exact FFTDF ERIs:
+
+* ``get_coul``       — ``fftdf-with-k-lstsq.py:20-187`` (parent grid from a kinetic-energy
+  cutoff ``k0``, selection Gram ``x2_s[0]**2``, ``dpstrf`` run with ``tol=1e-32``,
+  ``nip = min(rank, 600)``, ``zgelsy`` fit);
+* ``get_coul_pinv``  — ``fftdf-with-k.py:20-160`` (parent grid ``m0``, ``nip = min(nip, rank)``,
+  ``pinv(x4_q)`` fit);
+* ``check_eri``      — the harness ``fftdf-with-k-lstsq.py:208-258`` (``q = kconserv_ria[k1,k2]``,
+  ``k4 = kconserv[k1,k2,k3]``, fail above 1e-4).
+
+Every variant runs the GPU ISDF (``fisdf.ISDF``): the selection Gram ``x2_s[0]**2`` of
+``fftdf-with-k-lstsq.py:58-67`` equals ``fftisdf.py:376-379``'s ``(sum_k Re x2_k)**2 / nk``
+(``x2_s[0] = sum_k x2_k / sqrt(nk)``, real), so one selection kernel serves both; the fit is the
+factored pseudo-solve of DESIGN.md §3.4 for both ``gelsy`` and ``pinv`` (they agree with it to the
+ISDF fit's rounding on full-rank ``x4_q``).  ``coul_q`` (nk, nip, nip) and ``x_k``
+(nk, nip, nao) are returned as host arrays like the reference's; the ISDF object that produced
+them stays on ``df_obj._isdf`` (W_q, X_k resident in HBM) for ``check_eri``.
+"""
+import logging
+
+import numpy as np
+
+from .isdf import ISDF
+
+log = logging.getLogger("fisdf")
+
+NIP_CAP_LSTSQ = 600          # fftdf-with-k-lstsq.py:71 (``min(rank, 600)``)
+SELECT_TOL_LSTSQ = 1e-32     # fftdf-with-k-lstsq.py:70 (``pivoted_cholesky(x4, tol=1e-32)``)
+
+
+class _Grids:
+    def __init__(self, cell, mesh):
+        self.mesh = tuple(int(m) for m in mesh)
+        self.coords = cell.gen_uniform_grids(self.mesh)
+
+
+class FFTDF:
+    """The part of PySCF's ``FFTDF(cell, kpts)`` the ``get_coul`` drivers read: ``cell``,
+    ``mesh`` (default ``cell.mesh``), ``grids.coords``, ``verbose``.  ``get_eri`` is the exact
+    FFT-grid ERI of PySCF, which this library does not provide: pass ``eri_ref=callable(kpts)``
+    (e.g. the test oracle's ``exact_eri``) to use the reference harness ``check_eri``."""
+
+    def __init__(self, cell, kpts=None, eri_ref=None):
+        self.cell = cell
+        self.kpts = np.zeros((1, 3)) if kpts is None else np.asarray(kpts, float).reshape(-1, 3)
+        self.mesh = tuple(int(m) for m in cell.mesh)
+        self.verbose = getattr(cell, "verbose", 0)
+        self._eri_ref = eri_ref
+        self._isdf = None
+
+    @property
+    def grids(self):
+        return _Grids(self.cell, self.mesh)
+
+    def get_eri(self, kpts=None, compact=False):
+        if self._eri_ref is None:
+            raise NotImplementedError("exact FFTDF ERIs are PySCF's; pass eri_ref= to FFTDF")
+        return self._eri_ref(np.asarray(kpts, float).reshape(-1, 3))
+
+
+def cutoff_to_mesh(a, ke_cutoff):
+    """``pbctools.cutoff_to_mesh`` [pyscf] (fftdf-with-k-lstsq.py:32): the smallest mesh whose
+    plane waves reach ``|G| = sqrt(2 ke_cutoff)`` along every reciprocal axis,
+    ``ceil(2 sqrt(2 ke) / |b_i|)``.  PySCF >= 2.1 also widens the cutoff for non-orthogonal
+    cells (``_cubic2nonorth_factor``); the PySCF version is unpinned, so pass
+    ``m0=`` to ``get_coul`` to pin the parent mesh explicitly."""
+    a = np.asarray(a, float)
+    b = 2 * np.pi * np.linalg.inv(a.T)
+    return np.ceil(np.sqrt(2 * ke_cutoff) / np.linalg.norm(b, axis=1) * 2).astype(int)
+
+
+def _kvec(cell, kpts, kmesh):
+    scaled = np.asarray(kpts, float) @ cell.lattice_vectors().T / (2 * np.pi)
+    v = np.rint(scaled * np.asarray(kmesh)).astype(int)
+    if abs(scaled * np.asarray(kmesh) - v).max() > 1e-6:
+        raise ValueError("k-points are not on the k-mesh")
+    return v % np.asarray(kmesh)
+
+
+def _kindex(v, kmesh):
+    v = np.mod(v, kmesh)
+    return (v[..., 0] * kmesh[1] + v[..., 1]) * kmesh[2] + v[..., 2]
+
+
+def get_kconserv(cell, kpts, kmesh=None):
+    """``kpts_helper.get_kconserv`` [pyscf]: ``k4 = kconserv[k1, k2, k3]`` with
+    ``k1 - k2 + k3 - k4`` a reciprocal-lattice vector (fftdf-with-k-lstsq.py:215,224)."""
+    from .isdf import kpts_to_kmesh
+    kmesh = np.asarray(kpts_to_kmesh(cell, kpts) if kmesh is None else kmesh)
+    v = _kvec(cell, kpts, kmesh)
+    s = v[:, None, None, :] - v[None, :, None, :] + v[None, None, :, :]
+    return _kindex(s, kmesh).astype(int)
+
+
+def get_kconserv_ria(cell, kpts, kmesh=None):
+    """``kpts_helper.get_kconserv_ria`` [pyscf] as the ISDF harness uses it: ``q = kconserv[k1, k2]``
+    with ``k_q = k2 - k1`` modulo the reciprocal lattice (fftdf-with-k-lstsq.py:216,221; the
+    direction verified against exact ERIs)."""
+    from .isdf import kpts_to_kmesh
+    kmesh = np.asarray(kpts_to_kmesh(cell, kpts) if kmesh is None else kmesh)
+    v = _kvec(cell, kpts, kmesh)
+    return _kindex(v[None, :, :] - v[:, None, :], kmesh).astype(int)
+
+
+def _device_guard(nbytes, what):
+    """fftdf-with-k-lstsq.py:38-44: RuntimeError when the parent-grid Gram does not fit."""
+    import torch
+    if torch.cuda.is_available():
+        free, _ = torch.cuda.mem_get_info()
+        if nbytes > free:
+            raise RuntimeError("Max memory = %d MB is not enough.\nRequired memory = %d MB (%s)."
+                               % (free // 10**6, nbytes // 10**6, what))
+
+
+def _run(df_obj, kmesh, m0, nip_cap, select_tol, device=None, comm=None):
+    cell = df_obj.cell
+    kmesh = [1, 1, 1] if kmesh is None else [int(k) for k in kmesh]
+    ng0 = int(np.prod(m0))
+    _device_guard(ng0 * ng0 * 8, "parent-grid selection Gram")
+    isdf = ISDF(cell, cell.get_kpts(kmesh), m0=[int(m) for m in m0], device=device, comm=comm)
+    isdf.mesh = tuple(int(m) for m in df_obj.mesh)                   # df_obj.grids / df_obj.mesh
+    isdf.nip_max = int(nip_cap)
+    isdf.select_tol = float(select_tol)
+    isdf.build()
+    log.info("get_coul: m0 = %s, ng0 = %d, nip = %d, ranks = %s", list(m0), ng0, isdf.nip,
+             None if isdf.ranks is None else np.asarray(isdf.ranks).tolist())
+    df_obj._isdf = isdf
+    return isdf._wq, isdf._x
+
+
+def get_coul(df_obj, k0=10.0, kmesh=None, cisdf=0.6, verbose=5, blksize=16000, m0=None,
+             device=None, comm=None):
+    """``get_coul`` of fftdf-with-k-lstsq.py:20-187 -> ``(coul_q, x_k)``.
+
+    Parent grid ``cutoff_to_mesh(a, k0)`` (:31-33, or ``m0``), pivoted Cholesky with
+    ``tol=1e-32`` (:69-70), ``nip = min(rank, 600)`` (:71; ``cisdf`` is unused there too),
+    ``x_k`` = Bloch AOs at the chosen points (:75-78), lstsq fit and Coulomb per q (:155-181).
+    ``blksize`` and ``verbose`` are accepted for signature parity (the y build streams fixed
+    2 GB device blocks; logging goes through the ``fisdf`` logger)."""
+    if m0 is None:
+        m0 = cutoff_to_mesh(df_obj.cell.lattice_vectors(), k0)
+    return _run(df_obj, kmesh, m0, NIP_CAP_LSTSQ, SELECT_TOL_LSTSQ, device, comm)
+
+
+def get_coul_pinv(df_obj, m0=None, nip=100, kmesh=None, verbose=5, blksize=16000,
+                  device=None, comm=None):
+    """``get_coul`` of fftdf-with-k.py:20-160 (the ``pinv`` fit) -> ``(coul_q, x_k)``.
+
+    Parent grid ``m0`` (default 15^3, :27-28), dpstrf default tolerance (:62),
+    ``nip = min(nip, rank)`` (:63), ``pinv(x4_q)`` fit (:91-99) — served by the same factored
+    pseudo-solve as the lstsq driver."""
+    m0 = [15, 15, 15] if m0 is None else m0
+    return _run(df_obj, kmesh, m0, nip, -1.0, device, comm)
+
+
+def check_eri(df_obj, kmesh, coul_q=None, x_k=None, tol=1e-4, triples=None):
+    """The ERI check loop of fftdf-with-k-lstsq.py:208-258: for every (k1, k2, k3) (or the given
+    ``triples``), ``q = kconserv_ria[k1, k2]``, ``k4 = kconserv[k1, k2, k3]``, the ISDF ERI
+    ``sum_IJ c[q]_IJ x1*_Im x2_In x3*_Jk x4_Jl`` against ``df_obj.get_eri`` (exact FFTDF).
+
+    The ISDF ERI is evaluated on the GPU from the resident W_q / X_k of the ISDF object that
+    ``get_coul`` left on ``df_obj._isdf`` (``fisdf_get_eri``); ``coul_q``/``x_k`` are accepted for
+    signature parity.  Raises ``AssertionError`` above ``tol`` (the reference's ``assert 1 == 2``
+    at :258).  Returns the largest error seen."""
+    isdf = df_obj._isdf
+    if isdf is None:
+        raise RuntimeError("call get_coul(df_obj, ...) first")
+    cell = df_obj.cell
+    vk = cell.get_kpts(kmesh)
+    nk = len(vk)
+    nao = cell.nao_nr()
+    kconserv3 = get_kconserv(cell, vk, kmesh)
+    kconserv2 = get_kconserv_ria(cell, vk, kmesh)
+    if triples is None:
+        triples = [(k1, k2, k3) for k1 in range(nk) for k2 in range(nk) for k3 in range(nk)]
+    worst = 0.0
+    for k1, k2, k3 in triples:
+        q = kconserv2[k1, k2]
+        k4 = kconserv3[k1, k2, k3]
+        kq = vk[[k1, k2, k3, k4]]
+        eri_ref = np.asarray(df_obj.get_eri(kpts=kq, compact=False)).reshape(nao * nao, nao * nao)
+        eri_sol = isdf.get_eri(kq).reshape(nao * nao, nao * nao)
+        err = abs(eri_sol - eri_ref).max()
+        log.info("k1 = %2d, k2 = %2d, k3 = %2d, k4 = %2d (q = %2d) eri = %6.2e", k1, k2, k3, k4,
+                 q, err)
+        worst = max(worst, err)
+        if err > tol:
+            raise AssertionError("ISDF ERI error %.2e > %.1e at k = (%d, %d, %d, %d), q = %d"
+                                 % (err, tol, k1, k2, k3, k4, q))
+    return worst

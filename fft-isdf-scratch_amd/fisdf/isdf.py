@@ -98,6 +98,9 @@ class InterpolativeSeparableDensityFitting:
     blksize = 8000          # fftisdf.py:300
     fit_tol = 1e-14         # relative pivot cut of the x4_q factorisation
     select_tol = -1.0       # dpstrf default tolerance (ng0*eps*max diag)
+    # cap on the number of interpolation points; None -> int(nao * c0) (fftisdf.py:383);
+    # the get_coul drivers set it directly (fftdf-with-k-lstsq.py:71, fftdf-with-k.py:64)
+    nip_max = None
     # fit one q of each (q, -q) pair and take W_{-q} = conj(W_q) (y_s, x4_s real: :43,:81)
     time_reversal = True
     # q with 2 k_q in the reciprocal lattice (Gamma, all q of a 2x2x2 mesh): real x4_q and
@@ -191,7 +194,8 @@ class InterpolativeSeparableDensityFitting:
             self._ao_parent = self._eval_ao(self.cell.gen_uniform_grids(self.m0))
         x0 = self._ao_parent
         ng0 = x0.shape[1]
-        nip_max = min(int(nao * self.c0), ng0)
+        cap = int(nao * self.c0) if self.nip_max is None else int(self.nip_max)
+        nip_max = min(cap, ng0)
         perm = np.zeros(nip_max, np.int32)
         npiv = C_int()
         full = C_int()
