@@ -359,3 +359,34 @@ def make_dm(nao, kmesh, cell, seed=1234, scale=0.1):
     dk = np.sqrt(nimg) * np.einsum("Rk,Rmn->kmn", phase, dT)
     dk = 0.5 * (dk + dk.conj().transpose(0, 2, 1)) + np.eye(nao)[None]
     return dk
+
+
+def madelung(cell, kmesh, precision=1e-16):
+    """[pyscf] ``tools.pbc.madelung(cell, kpts)``: minus twice the Ewald energy of one unit point
+    charge in the Born-von Karman supercell (lattice vectors ``a_i * kmesh_i``) with a
+    neutralising background — the G=0 exchange correction of ``exxdiv='ewald'``.
+
+    E = 1/2 sum_{L!=0} erfc(eta|L|)/|L| + (2 pi/V) sum_{G!=0} exp(-G^2/4 eta^2)/G^2
+        - eta/sqrt(pi) - pi/(2 eta^2 V),
+    both lattice sums taken to ``precision`` (the result does not depend on eta; PySCF cuts its
+    sums by ``cell.precision`` and the supercell mesh instead).  Simple cubic, side L:
+    2.8372974794806 / L."""
+    from scipy.special import erfc
+    A = cell.lattice_vectors() * np.asarray(kmesh, float)[:, None]
+    V = abs(np.linalg.det(A))
+    B = 2 * np.pi * np.linalg.inv(A).T
+    eta = math.sqrt(math.pi) / V ** (1.0 / 3)
+    s = math.sqrt(-math.log(precision))
+    rmax, gmax = (s + 1.0) / eta, 2 * eta * (s + 1.0)
+    n = np.ceil(rmax * np.linalg.norm(B, axis=1) / (2 * np.pi)).astype(int) + 1
+    L = cartesian_prod([np.arange(-m, m + 1) for m in n]) @ A
+    r = np.linalg.norm(L, axis=1)
+    r = r[(r > 0) & (r < rmax)]
+    e_real = 0.5 * np.sum(erfc(eta * r) / r)
+    m = np.ceil(gmax * np.linalg.norm(A, axis=1) / (2 * np.pi)).astype(int) + 1
+    G = cartesian_prod([np.arange(-k, k + 1) for k in m]) @ B
+    g2 = np.einsum("gi,gi->g", G, G)
+    g2 = g2[(g2 > 0) & (g2 < gmax * gmax)]
+    e_recip = 2 * np.pi / V * np.sum(np.exp(-g2 / (4 * eta * eta)) / g2)
+    e_self = -eta / math.sqrt(math.pi) - math.pi / (2 * eta * eta * V)
+    return -2.0 * (e_real + e_recip + e_self)

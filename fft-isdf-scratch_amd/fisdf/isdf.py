@@ -23,7 +23,7 @@ import time
 import numpy as np
 
 from . import _lib, kshard
-from .cell import eval_ao_kpts, make_kpts
+from .cell import eval_ao_kpts, madelung, make_kpts
 
 log = logging.getLogger("fisdf")
 
@@ -245,7 +245,9 @@ class InterpolativeSeparableDensityFitting:
         """fftisdf.py:390-408."""
         if omega is not None:
             raise NotImplementedError
-        if exxdiv is not None:
+        if exxdiv is not None and exxdiv != "ewald":
+            # the reference raises for every exxdiv (:395-396); 'ewald' is added here as
+            # PySCF's FFTDF does it (SURVEY.md §8f next-4): K + madelung * S_k D_k S_k
             raise NotImplementedError
         kpts = self.kpts if kpts is None else np.asarray(kpts)
         if kpts.ndim == 1:                                            # _check_kpts single kpt
@@ -256,6 +258,35 @@ class InterpolativeSeparableDensityFitting:
         if with_j:
             vj = get_j_kpts(self, dm, hermi, kpts, kpts_band)
         return vj, vk
+
+    def get_ovlp(self):
+        """AO overlap S_k = (vol/ngrid) chi_k^H chi_k (nk, nao, nao) by the FFT-grid quadrature
+        (the grid FFTDF's J/K use; PySCF's ``pbc_intor('int1e_ovlp')`` is analytic), one batched
+        split-K GEMM over the resident Bloch AOs; cached on the device."""
+        st = self._dev_state
+        if st is not None and "S" in st:
+            return st["S"]
+        d = self.device
+        if self._ao_grid is None:
+            self._ao_grid = self._eval_ao(self.grids_coords())
+        chi = self._ao_grid
+        nk, ngrid, nao = chi.shape
+        S = d.empty((nk, nao, nao))
+        alpha = np.array([self.cell.vol / ngrid, 0.0])
+        beta = np.zeros(2)
+        d.ctx.call("fisdf_zgemm", 3, 0, nao, nao, ngrid, alpha.ctypes.data_as(_lib._dp),
+                   _lib.ptr(chi), nao, ngrid * nao, _lib.ptr(chi), nao, ngrid * nao,
+                   beta.ctypes.data_as(_lib._dp), _lib.ptr(S), nao, nao * nao, nk,
+                   max(1, min(64, ngrid // 1024)))
+        if st is not None:
+            st["S"] = S
+        return S
+
+    def madelung(self):
+        """``tools.pbc.madelung(cell, kpts)`` [pyscf] for this k-mesh (host scalar, cached)."""
+        if getattr(self, "_madelung", None) is None:
+            self._madelung = madelung(self.cell, self._kmesh())
+        return self._madelung
 
     # ---- 4-index integrals (north-star get_eri / ao2mo surface; next-2 of SURVEY §8f) ----
     def _kidx(self, kpts):
@@ -516,8 +547,8 @@ def get_j_kpts(df_obj, dm_kpts, hermi=1, kpts=np.zeros((1, 3)), kpts_band=None, 
 
 
 def get_k_kpts(df_obj, dm_kpts, hermi=1, kpts=np.zeros((1, 3)), kpts_band=None, exxdiv=None):
-    """fftisdf.py:173-228."""
-    assert exxdiv is None
+    """fftisdf.py:173-228 (+ exxdiv='ewald', next-4)."""
+    assert exxdiv in (None, "ewald")
     st = df_obj._dev_state
     assert st is not None and "Ws" in st, "call build() first"
     d = df_obj.device
@@ -533,4 +564,27 @@ def get_k_kpts(df_obj, dm_kpts, hermi=1, kpts=np.zeros((1, 3)), kpts_band=None, 
                nip, nao, km_p, a_p, i0, i1, _lib.ptr(vk))
     if d.size > 1:
         kshard.allreduce_sum(vk, d.comm)
+    if exxdiv == "ewald":
+        _ewald_exxdiv_for_G0(df_obj, ddms, vk)
     return _format_jks(vk.cpu().numpy(), dm_kpts)
+
+
+def _ewald_exxdiv_for_G0(df_obj, ddms, vk):
+    """PySCF ``pbc.df.df_jk._ewald_exxdiv_for_G0`` (kpts_band = kpts): the G=0 exchange term left
+    out by coulG(G=0) = 0, vk[x, k] += madelung * S_k D[x, k] S_k — two batched GEMMs per dm set
+    on the device (T = D_k S_k, then vk += madelung * S_k T)."""
+    d = df_obj.device
+    S = df_obj.get_ovlp()
+    nset, nk, nao = ddms.shape[:3]
+    mad = df_obj.madelung()
+    T = d.empty((nk, nao, nao))
+    one, zero = np.array([1.0, 0.0]), np.zeros(2)
+    amad = np.array([mad, 0.0])
+    st = nao * nao
+    for x in range(nset):
+        d.ctx.call("fisdf_zgemm", 0, 0, nao, nao, nao, one.ctypes.data_as(_lib._dp),
+                   _lib.ptr(ddms[x]), nao, st, _lib.ptr(S), nao, st,
+                   zero.ctypes.data_as(_lib._dp), _lib.ptr(T), nao, st, nk, 1)
+        d.ctx.call("fisdf_zgemm", 0, 0, nao, nao, nao, amad.ctypes.data_as(_lib._dp),
+                   _lib.ptr(S), nao, st, _lib.ptr(T), nao, st, one.ctypes.data_as(_lib._dp),
+                   _lib.ptr(vk[x]), nao, st, nk, 1)

@@ -23,6 +23,23 @@ def test_cutoff_to_mesh_cubic():
     assert m1.shape == (3,) and (m2 >= m1).all() and (m1 == m1[0]).all()
 
 
+def test_madelung_kat():
+    """tools.pbc.madelung restated: simple-cubic Madelung constant 2.8372974794806 / L for the
+    Born-von Karman supercell, invariant under the Ewald splitting; scales as 1/N for an NxNxN
+    k-mesh of a cubic cell."""
+    from fisdf import toy_cell
+    from fisdf.cell import madelung
+    cell = toy_cell()
+    for L in (1.0, 4.5):
+        cell.a = np.eye(3) * L
+        assert abs(madelung(cell, (1, 1, 1)) * L - 2.8372974794806) < 1e-12
+        assert abs(madelung(cell, (3, 3, 3)) * 3 * L - 2.8372974794806) < 1e-12
+    # a non-cubic cell: precision change leaves it unchanged
+    cell = toy_cell()
+    m1, m2 = madelung(cell, (2, 2, 1), 1e-16), madelung(cell, (2, 2, 1), 1e-12)
+    assert abs(m1 - m2) < 1e-10 and m1 > 0
+
+
 @pytest.mark.parametrize("kmesh", [(2, 2, 2), (3, 3, 1), (1, 1, 1), (4, 2, 3)])
 def test_kconserv_tables(kmesh):
     """k1 - k2 + k3 - k4 in the reciprocal lattice; q = k2 - k1 (brute force on scaled k)."""

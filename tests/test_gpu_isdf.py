@@ -218,7 +218,7 @@ def test_not_implemented_paths():
     with pytest.raises(NotImplementedError):
         df.get_jk(dm, omega=0.3)
     with pytest.raises(NotImplementedError):
-        df.get_jk(dm, exxdiv="ewald")
+        df.get_jk(dm, exxdiv="vcut_sph")        # only 'ewald' is added (next-4)
     with pytest.raises(NotImplementedError):
         df.get_jk(dm[0, 0], kpts=np.zeros(3))
 
@@ -328,3 +328,28 @@ def test_jk_row_blocks_sum_to_full():
     assert abs(vj.real - vj_full).max() < 1e-12 * scale if np.isrealobj(vj_full) else \
         abs(vj - vj_full).max() < 1e-12 * scale
     assert abs(vk - vk_full).max() < 1e-12 * scale
+
+
+def test_exxdiv_ewald():
+    """next-4: exxdiv='ewald' = exxdiv=None K + madelung * S_k D_k S_k (PySCF
+    _ewald_exxdiv_for_G0), S_k the FFT-grid overlap; J unchanged.  Checked against the oracle K
+    plus the same correction formed on the host from the oracle's AO inputs."""
+    from fisdf.cell import madelung
+    df, o, dm = make_df("toy222")
+    df.build()
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs("toy222")
+    vj0, vk0 = df.get_jk(dm)
+    vj1, vk1 = df.get_jk(dm, exxdiv="ewald")
+    assert abs(vj1 - vj0).max() == 0.0
+    S = np.einsum("kgm,kgn->kmn", chi.conj(), chi) * (cell.vol / chi.shape[1])
+    assert abs(df.get_ovlp().cpu().numpy() - S).max() < 1e-12 * max(1.0, abs(S).max())
+    mad = madelung(cell, kmesh)
+    ref = o["vk"] + mad * np.einsum("kmp,xkpq,kqn->xkmn", S, dm, S)
+    err = abs(vk1 - ref).max()
+    print("ewald K vs oracle + correction", err, "madelung", mad)
+    assert err < JK_TOL
+    # the correction is Hermitian for a Hermitian dm, and repeated calls reuse the cached S
+    d = vk1 - vk0
+    assert abs(d - d.conj().swapaxes(-1, -2)).max() < 1e-12
+    _, vk2 = df.get_jk(dm, exxdiv="ewald")
+    assert abs(vk2 - vk1).max() == 0.0
