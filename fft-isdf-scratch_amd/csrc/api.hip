@@ -64,6 +64,7 @@ struct fisdf_ctx {
   hipEvent_t ev_x4 = nullptr, ev_fac = nullptr, ev_chol = nullptr;
   bool f_fac_unjoined = false;  // ev_fac not yet waited on by the main stream (fit lanes do)
   bool f_pending = false;
+  bool x4_marked = false;  // fisdf_factor_x4_mark recorded ev_x4 for the next factor_x4_async
   int* f_rank_pinned = nullptr;  // host (pinned) copy target, f_nk ints
   void* f_scratch = nullptr;     // device scratch of the factorisation
   size_t f_scratch_size = 0;
@@ -886,13 +887,7 @@ int factor_pivoted(fisdf_ctx* c, hipStream_t s) {
   return factor_finish(c, s, (const int*)(b + oR));
 }
 
-int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int nq, int nip,
-                          double tol_rel, const int* kmesh) {
-  FISDF_TRY(device_guard(c));
-  const int nk = nq;
-  FISDF_CHECK(nk > 0 && nip > 0, "factor_x4: bad sizes");
-  FISDF_TRY(check_qlist(h_qs, nq, 1 << 30, "factor_x4"));
-  if (c->f_pending) FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
+static int ensure_side(fisdf_ctx* c) {
   if (!c->side) {
     // FISDF_SIDE_PRIO=1: the factorisation (a chain of small kernels beside the y build's
     // large ones) on a high-priority stream
@@ -905,6 +900,26 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_fac, hipEventDisableTiming));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_chol, hipEventDisableTiming));
   }
+  return 0;
+}
+
+int fisdf_factor_x4_mark(fisdf_ctx* c) {
+  FISDF_TRY(device_guard(c));
+  if (c->f_pending) FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
+  FISDF_TRY(ensure_side(c));
+  FISDF_HIP(hipEventRecord(c->ev_x4, c->stream));
+  c->x4_marked = true;
+  return 0;
+}
+
+int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int nq, int nip,
+                          double tol_rel, const int* kmesh) {
+  FISDF_TRY(device_guard(c));
+  const int nk = nq;
+  FISDF_CHECK(nk > 0 && nip > 0, "factor_x4: bad sizes");
+  FISDF_TRY(check_qlist(h_qs, nq, 1 << 30, "factor_x4"));
+  if (c->f_pending) FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
+  FISDF_TRY(ensure_side(c));
   const int nb = c->f_nb;
   const int nblk = (nip + nb - 1) / nb;
   const long nn = (long)nip * nip;
@@ -953,7 +968,10 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   c->f_used_pivoted = false;
   // the side stream starts once everything enqueued on `stream` so far (x4) is done; work
   // enqueued on `stream` after this call (the y build) runs concurrently
-  FISDF_HIP(hipEventRecord(c->ev_x4, c->stream));
+  // (or at fisdf_factor_x4_mark, so that work enqueued between the two calls — the y build —
+  // is not waited for, and the factor's host-blocking rank read-back cannot delay its launch)
+  if (!c->x4_marked) FISDF_HIP(hipEventRecord(c->ev_x4, c->stream));
+  c->x4_marked = false;
   FISDF_HIP(hipStreamWaitEvent(c->side, c->ev_x4, 0));
   StageTimer tm(c, FISDF_ST_FACTOR, c->side);
   hipStream_t s = c->side;

@@ -18,6 +18,7 @@ Differences from the reference, all deliberate:
 from __future__ import annotations
 
 import logging
+import os
 import time
 
 import numpy as np
@@ -87,6 +88,13 @@ class _Device:
         t = self.torch
         a = np.ascontiguousarray(arr)
         return t.from_numpy(a).to(self.dev, non_blocking=False)
+
+    def to_dev_async(self, arr):
+        """Upload through pinned memory without a host wait on the stream (small per-call inputs
+        such as density matrices: the GPU keeps running the work already enqueued)."""
+        t = self.torch
+        h = t.from_numpy(np.ascontiguousarray(arr)).pin_memory()
+        return h.to(self.dev, non_blocking=True)
 
 
 class InterpolativeSeparableDensityFitting:
@@ -253,10 +261,17 @@ class InterpolativeSeparableDensityFitting:
         if kpts.ndim == 1:                                            # _check_kpts single kpt
             raise NotImplementedError
         vj = vk = None
+        # one upload of the density matrices, K then J enqueued back to back (:404-407), one
+        # read-back each at the end: no host round trip between the two
+        dms, ddms = _dms_to_dev(self, dm)
         if with_k:
-            vk = get_k_kpts(self, dm, hermi, kpts, kpts_band, exxdiv)
+            vk = _get_k_dev(self, ddms, exxdiv)
         if with_j:
-            vj = get_j_kpts(self, dm, hermi, kpts, kpts_band)
+            vj = _get_j_dev(self, ddms)
+        if vk is not None:
+            vk = _format_jks(vk.cpu().numpy(), dm)
+        if vj is not None:
+            vj = _finish_j(vj, dm, kpts, kpts_band)
         return vj, vk
 
     def get_ovlp(self):
@@ -440,15 +455,26 @@ def build(df_obj):
     # overlapped with the y build enqueued next on the main stream
     d.ctx.call("fisdf_set_pivoted_fit", -1 if df_obj.pivoted_fit is None
                else (1 if df_obj.pivoted_fit else 0))
+    # the side stream starts from here (x4 built); the factor chain itself is enqueued after
+    # the y build, since it reads ranks back to the host part-way (a blocking copy)
     if nq:
-        d.ctx.call("fisdf_factor_x4_async", _lib.ptr(x4), qs_c, nq, nip, float(df_obj.fit_tol),
-                   km_p if df_obj.real_self_conjugate else None)
+        d.ctx.call("fisdf_factor_x4_mark")
+
+    def factor_async():
+        if nq:
+            d.ctx.call("fisdf_factor_x4_async", _lib.ptr(x4), qs_c, nq, nip,
+                       float(df_obj.fit_tol), km_p if df_obj.real_self_conjugate else None)
+    after_y = os.environ.get("FISDF_FACTOR_AFTER_Y", "1") != "0"
+    if not after_y:
+        factor_async()
+        factor_async = lambda: None          # noqa: E731
     # fx_{-k} = conj(fx_k) for real AOs: fx_k computed for half the k-mesh (:76)
     d.ctx.call("fisdf_set_time_reversal", 1 if df_obj.time_reversal else 0)
     yT = d.empty((nq, nip, ngrid))
     if d.size == 1:
         d.ctx.call("fisdf_build_y_qs", _lib.ptr(f), ngrid * nao, 0, ngrid, ngrid, _lib.ptr(X),
                    nip, nao, km_p, a_p, qs_c, nq, _lib.ptr(yT))                 # :67-87
+        factor_async()
     else:
         # grid-sharded y (all fitted q on this rank's plane-aligned grid slice), then one
         # all-to-all hands every rank the y_q of its own q-chunk on the whole grid
@@ -460,6 +486,7 @@ def build(df_obj):
             fptr = _lib._vp(f.data_ptr() + g0 * nao * f.element_size())
             d.ctx.call("fisdf_build_y_qs", fptr, ngrid * nao, 0, ng, ng, _lib.ptr(X), nip, nao,
                        km_p, a_p, all_qs.ctypes.data_as(_lib._ip), len(all_qs), _lib.ptr(send))
+        factor_async()
         # the all-to-all, split per local q, runs on the collective stream while this rank
         # factorises its x4_q and fits its earlier q
         pieces = kshard.exchange_y_chunked(send, nip, slices, d.rank, d.size, d.comm,
@@ -520,25 +547,34 @@ def _fit_qset(df_obj, kmesh):
 def _dms_to_dev(df_obj, dm_kpts):
     nk = int(np.prod(df_obj.kmesh))
     dms = _format_dms(dm_kpts, nk).astype(np.complex128)
-    return dms, df_obj.device.to_dev(dms)
+    return dms, df_obj.device.to_dev_async(dms)
 
 
 def get_j_kpts(df_obj, dm_kpts, hermi=1, kpts=np.zeros((1, 3)), kpts_band=None, exxdiv=None):
     """fftisdf.py:133-171."""
     assert exxdiv is None
+    dms, ddms = _dms_to_dev(df_obj, dm_kpts)
+    return _finish_j(_get_j_dev(df_obj, ddms), dm_kpts, kpts, kpts_band)
+
+
+def _get_j_dev(df_obj, ddms):
+    """vj on the device (fftisdf.py:150-166) for device dms (nset, nk, nao, nao)."""
     st = df_obj._dev_state
     assert st is not None and "W0" in st, "call build() first"
     d = df_obj.device
-    dms, ddms = _dms_to_dev(df_obj, dm_kpts)
-    nset, nk, nao = dms.shape[:3]
+    nset, nk, nao = ddms.shape[:3]
     nip = st["X"].shape[1]
-    vj = d.empty(dms.shape)
+    vj = d.empty(ddms.shape)
     # sharded: each rank contracts its block of interpolation points, one all-reduce (:166)
     i0, i1 = d.shard(nip) if d.size > 1 else (0, nip)
     d.ctx.call("fisdf_get_j_rows", _lib.ptr(st["X"]), _lib.ptr(st["W0"]), _lib.ptr(ddms), nset,
                nk, nip, nao, i0, i1, _lib.ptr(vj))
     if d.size > 1:  # the library runs on torch's current stream: the all-reduce is ordered
         kshard.allreduce_sum(vj, d.comm)
+    return vj
+
+
+def _finish_j(vj, dm_kpts, kpts, kpts_band):
     out = vj.cpu().numpy()
     band = np.asarray(kpts if kpts_band is None else kpts_band)
     if abs(band).max() < 1e-9:                                           # :169-170
@@ -549,15 +585,20 @@ def get_j_kpts(df_obj, dm_kpts, hermi=1, kpts=np.zeros((1, 3)), kpts_band=None, 
 def get_k_kpts(df_obj, dm_kpts, hermi=1, kpts=np.zeros((1, 3)), kpts_band=None, exxdiv=None):
     """fftisdf.py:173-228 (+ exxdiv='ewald', next-4)."""
     assert exxdiv in (None, "ewald")
+    dms, ddms = _dms_to_dev(df_obj, dm_kpts)
+    return _format_jks(_get_k_dev(df_obj, ddms, exxdiv).cpu().numpy(), dm_kpts)
+
+
+def _get_k_dev(df_obj, ddms, exxdiv=None):
+    """vk on the device (fftisdf.py:204-225) for device dms (nset, nk, nao, nao)."""
     st = df_obj._dev_state
     assert st is not None and "Ws" in st, "call build() first"
     d = df_obj.device
-    dms, ddms = _dms_to_dev(df_obj, dm_kpts)
-    nset, nk, nao = dms.shape[:3]
+    nset, nk, nao = ddms.shape[:3]
     nip = st["X"].shape[1]
     km_c, km_p = _lib.iarr(df_obj.kmesh)
     a_c, a_p = _lib.darr(np.asarray(df_obj.cell.lattice_vectors(), float).ravel())
-    vk = d.empty(dms.shape)
+    vk = d.empty(ddms.shape)
     # sharded: each rank contracts its block of interpolation points, one all-reduce (:225)
     i0, i1 = d.shard(nip) if d.size > 1 else (0, nip)
     d.ctx.call("fisdf_get_k_rows", _lib.ptr(st["X"]), _lib.ptr(st["Ws"]), _lib.ptr(ddms), nset,
@@ -566,7 +607,7 @@ def get_k_kpts(df_obj, dm_kpts, hermi=1, kpts=np.zeros((1, 3)), kpts_band=None, 
         kshard.allreduce_sum(vk, d.comm)
     if exxdiv == "ewald":
         _ewald_exxdiv_for_G0(df_obj, ddms, vk)
-    return _format_jks(vk.cpu().numpy(), dm_kpts)
+    return vk
 
 
 def _ewald_exxdiv_for_G0(df_obj, ddms, vk):

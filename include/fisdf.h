@@ -145,6 +145,10 @@ int fisdf_factor_x4_qs(fisdf_ctx* ctx, const void* d_x4, const int* h_qs, int nq
 int fisdf_factor_x4_async(fisdf_ctx* ctx, const void* d_x4, const int* h_qs, int nq, int nip,
                           double tol_rel, const int* kmesh);
 int fisdf_factor_x4_wait(fisdf_ctx* ctx, int* h_ranks /* nq, may be NULL */);
+/* Record the point on the main stream (x4 built) the next fisdf_factor_x4_async starts from, so
+ * that the y build can be enqueued between the two calls: the factorisation reads its ranks back
+ * to the host mid-chain, which can block the enqueueing thread until the side stream gets there. */
+int fisdf_factor_x4_mark(fisdf_ctx* ctx);
 /* Factorisation path.  Default (mode -1: unless FISDF_PIVOTED_FIT=1 in the environment): an
  * unpivoted blocked Cholesky, kept when every pivot exceeds tol_rel * max(diag) (the full-rank
  * verdict of the rank-revealing factorisation) and otherwise redone — for the whole batch —

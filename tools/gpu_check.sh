@@ -17,6 +17,6 @@ cat $OUT/bench.json
 # the profiled process may crash in its exit handlers after rocprofv3 has written the
 # stats (seen on this image); judge the pass by its output file
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > $OUT/prof_bench.json 2> $OUT/prof.err
-ls $OUT/prof/*kernel_stats.csv $OUT/prof/*/*kernel_stats.csv > /dev/null 2>&1 || { echo PROF FAILED; tail -30 $OUT/prof.err; exit 1; }
+[ -n "$(find $OUT/prof -name '*kernel_stats.csv')" ] || { echo PROF FAILED; tail -30 $OUT/prof.err; exit 1; }
 find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \;
 head -25 $OUT/kernel_stats.csv | cut -c1-200
