@@ -52,6 +52,7 @@ struct fisdf_ctx {
   int force_pivoted = -1;  // fisdf_set_pivoted_fit; -1: environment FISDF_PIVOTED_FIT
   int lanes = 0;           // fisdf_set_fit_lanes; 0: environment FISDF_FIT_LANES / default
   bool time_reversal = false;  // fisdf_set_time_reversal: fx_{-k} = conj(fx_k) in build_y
+  double omega = 0.0;          // fisdf_set_omega: range-separated Coulomb kernel of the fit
   // extra streams of the fit lanes (fisdf_fit_coulomb_qs)
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
@@ -274,7 +275,7 @@ bool self_conjugate(const int kmesh[3], int q) {
 int get_asym(fisdf_ctx* c, hipStream_t st, const int mesh[3], const int kmesh[3],
              const double a[9], int q, const double* wt, const fisdf_ctx::Asym** out) {
   std::vector<double> key = {(double)mesh[0], (double)mesh[1], (double)mesh[2], (double)kmesh[0],
-                             (double)kmesh[1], (double)kmesh[2], (double)q};
+                             (double)kmesh[1], (double)kmesh[2], (double)q, c->omega};
   for (int i = 0; i < 9; ++i) key.push_back(a[i]);
   auto it = c->asym_cache.find(key);
   if (it == c->asym_cache.end()) {
@@ -539,7 +540,7 @@ int fisdf_coulg(fisdf_ctx* c, const int mesh[3], const double a[9], const double
   FISDF_TRY(device_guard(c));
   CellGeom g;
   lattice(a, g);
-  return coulg_weight(c->stream, mesh, g, k, scale, take_sqrt, w);
+  return coulg_weight(c->stream, mesh, g, k, scale, take_sqrt, w, c->omega);
 }
 
 int fisdf_pivoted_cholesky(fisdf_ctx* c, const void* A, int n, int batch, int rmax,
@@ -1006,6 +1007,12 @@ int fisdf_set_pivoted_fit(fisdf_ctx* c, int mode) {
   return 0;
 }
 
+int fisdf_set_omega(fisdf_ctx* c, double omega) {
+  FISDF_CHECK(c != nullptr && std::isfinite(omega), "set_omega: omega must be finite");
+  c->omega = omega;
+  return 0;
+}
+
 int fisdf_set_time_reversal(fisdf_ctx* c, int on) {
   FISDF_CHECK(c != nullptr && (on == 0 || on == 1), "set_time_reversal: on must be 0 or 1");
   c->time_reversal = on == 1;
@@ -1167,7 +1174,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     {
       StageTimer tm(c, FISDF_ST_FFT, st);
       // sqrt(coulG(k_q+G) vol/N^2)  (:114-115 and the Parseval 1/N of :118)
-      FISDF_TRY(coulg_weight(st, mesh, g, kq, vol / ((double)ngrid * ngrid), 1, wt));
+      FISDF_TRY(coulg_weight(st, mesh, g, kq, vol / ((double)ngrid * ngrid), 1, wt, c->omega));
       // Yh = FFT(y_q[:, piv] * f_q) * w   (:99, :113; rows in pivot order)
       FISDF_TRY(fft3d(st, yT + (long)lq * nip * ngrid, ngrid, piv, Yh, ngrid, r, mesh[0],
                       mesh[1], mesh[2], kd, wt, nullptr));

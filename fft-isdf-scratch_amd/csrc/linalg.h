@@ -31,7 +31,7 @@ int scatter_w(hipStream_t s, const cplx* Wpp, int ldw, long sW, int rmax, const 
               const int* rank, cplx* W, int nip, int batch);
 int conj_transpose(hipStream_t s, const cplx* A, int n, long sA, cplx* B, int batch);
 int coulg_weight(hipStream_t s, const int mesh[3], const CellGeom& g, const double k[3],
-                 double scale, int take_sqrt, double* w);
+                 double scale, int take_sqrt, double* w, double omega = 0.0);
 int square_real(hipStream_t s, const cplx* in, cplx* out, long n, unsigned long long* maximag);
 int real_part(hipStream_t s, const cplx* in, double scale, cplx* out, long n,
               unsigned long long* maximag);

@@ -117,8 +117,11 @@ __global__ void conj_transpose_kernel(const cplx* __restrict__ A, int n, long sA
 }
 
 // sqrt(coulG(k+G) * scale); PySCF get_coulG (exxdiv=None, wrap_around=True) restated
+// omega != 0: PySCF's range-separated kernels, omega > 0 the long-range erf(w r)/r
+// (x exp(-|k+G|^2 / 4w^2)), omega < 0 the short-range erfc(|w| r)/r (x (1 - exp(...)), and its
+// finite |k+G| = 0 limit pi / w^2)
 __global__ void coulg_weight_kernel(int n0, int n1, int n2, CellGeom g, double kx, double ky,
-                                    double kz, double scale, int take_sqrt,
+                                    double kz, double scale, int take_sqrt, double omega,
                                     double* __restrict__ w) {
   long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
   long ngrid = (long)n0 * n1 * n2;
@@ -158,6 +161,13 @@ __global__ void coulg_weight_kernel(int n0, int n1, int n2, CellGeom g, double k
   }
   double g2 = kG[0] * kG[0] + kG[1] * kG[1] + kG[2] * kG[2];
   double cg = (g2 == 0.0 || boundary) ? 0.0 : 4.0 * 3.141592653589793 / g2;
+  if (omega != 0.0 && !boundary) {
+    const double f = exp(-0.25 * g2 / (omega * omega));
+    if (omega > 0.0)
+      cg *= f;
+    else
+      cg = g2 == 0.0 ? 3.141592653589793 / (omega * omega) : cg * (1.0 - f);
+  }
   double v = cg * scale;
   w[e] = take_sqrt ? sqrt(v) : v;
 }
@@ -767,10 +777,10 @@ int conj_transpose(hipStream_t s, const cplx* A, int n, long sA, cplx* B, int ba
 }
 
 int coulg_weight(hipStream_t s, const int mesh[3], const CellGeom& g, const double k[3],
-                 double scale, int take_sqrt, double* w) {
+                 double scale, int take_sqrt, double* w, double omega) {
   long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
   hipLaunchKernelGGL(coulg_weight_kernel, dim3(nblocks(ngrid, 256, 1L << 30)), dim3(256), 0, s,
-                     mesh[0], mesh[1], mesh[2], g, k[0], k[1], k[2], scale, take_sqrt, w);
+                     mesh[0], mesh[1], mesh[2], g, k[0], k[1], k[2], scale, take_sqrt, omega, w);
   FISDF_HIP(hipGetLastError());
   return 0;
 }

@@ -58,6 +58,7 @@ _SIGS = {
     "fisdf_factor_x4_async": ([_vp, _vp, _ip, _i, _i, _d, _ip], _i),
     "fisdf_factor_x4_wait": ([_vp, _ip], _i),
     "fisdf_factor_x4_mark": ([_vp], _i),
+    "fisdf_set_omega": ([_vp, _d], _i),
     "fisdf_set_pivoted_fit": ([_vp, _i], _i),
     "fisdf_factor_info": ([_vp, _ip], _i),
     "fisdf_set_fit_lanes": ([_vp, _i], _i),

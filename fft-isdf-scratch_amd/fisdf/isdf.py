@@ -251,8 +251,13 @@ class InterpolativeSeparableDensityFitting:
     def get_jk(self, dm, hermi=1, kpts=None, kpts_band=None, with_j=True, with_k=True,
                omega=None, exxdiv=None):
         """fftisdf.py:390-408."""
-        if omega is not None:
-            raise NotImplementedError
+        if omega is not None and omega != 0:
+            # range-separated kernel (PySCF get_coulG omega; the reference raises, :392-393):
+            # W_q refitted once per omega with the attenuated weight, X and the AO inputs shared
+            if exxdiv is not None:
+                raise NotImplementedError("exxdiv with a range-separated kernel")
+            return self._omega_df(float(omega)).get_jk(dm, hermi, kpts, kpts_band, with_j,
+                                                       with_k, None, None)
         if exxdiv is not None and exxdiv != "ewald":
             # the reference raises for every exxdiv (:395-396); 'ewald' is added here as
             # PySCF's FFTDF does it (SURVEY.md §8f next-4): K + madelung * S_k D_k S_k
@@ -273,6 +278,23 @@ class InterpolativeSeparableDensityFitting:
         if vj is not None:
             vj = _finish_j(vj, dm, kpts, kpts_band)
         return vj, vk
+
+    def _omega_df(self, omega):
+        """The ISDF state for a range-separated kernel (built on first use, cached per omega):
+        same interpolation points, W_q / W_s fitted with coulG(omega)."""
+        st = self._dev_state
+        assert st is not None and "W0" in st, "call build() first"
+        cache = self.__dict__.setdefault("_omega_dfs", {})
+        if omega not in cache:
+            import copy
+            sub = copy.copy(self)
+            sub._fit_omega = omega
+            sub._dev_state = dict(X=st["X"])
+            sub._omega_dfs = {}
+            sub.timings = {}
+            build(sub)
+            cache[omega] = sub
+        return cache[omega]
 
     def get_ovlp(self):
         """AO overlap S_k = (vol/ngrid) chi_k^H chi_k (nk, nao, nao) by the FFT-grid quadrature
@@ -470,6 +492,8 @@ def build(df_obj):
         factor_async = lambda: None          # noqa: E731
     # fx_{-k} = conj(fx_k) for real AOs: fx_k computed for half the k-mesh (:76)
     d.ctx.call("fisdf_set_time_reversal", 1 if df_obj.time_reversal else 0)
+    d.ctx.call("fisdf_set_omega", float(getattr(df_obj, "_fit_omega", 0.0)))
+    df_obj._omega_dfs = {}                   # range-separated states of an earlier build
     yT = d.empty((nq, nip, ngrid))
     if d.size == 1:
         d.ctx.call("fisdf_build_y_qs", _lib.ptr(f), ngrid * nao, 0, ngrid, ngrid, _lib.ptr(X),

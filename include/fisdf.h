@@ -174,6 +174,10 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* ctx, const int* h_qs, int nq, const void* d_
  * MFMA-bound TRSM); 0 (default): FISDF_FIT_LANES from the environment, else 2.  Results do
  * not depend on it (same kernels, same per-q arithmetic). */
 int fisdf_set_fit_lanes(fisdf_ctx* ctx, int lanes);
+/* Coulomb kernel of the fit (and of fisdf_coulg): 0 = 1/r (default, fftisdf.py:114); omega > 0 the
+ * long-range erf(omega r)/r, omega < 0 the short-range erfc(|omega| r)/r (PySCF get_coulG's
+ * omega; the reference's get_jk raises for omega, fftisdf.py:392-393). */
+int fisdf_set_omega(fisdf_ctx* ctx, double omega);
 /* Time reversal of the inputs (real AOs, k-mesh closed under k -> -k): f_{-k} = conj(f_k)
  * and x_{-k} = conj(x_k), so fx_{-k} = conj(fx_k) (fftisdf.py:76) and fisdf_build_y(_qs)
  * computes fx_k only for the k-planes a <= kmesh[0]/2.  Default 0 (every k computed). */

@@ -48,11 +48,14 @@ def get_Gv(a, mesh):
     return _cartesian_prod([np.fft.fftfreq(n, 1.0 / n) for n in mesh]) @ b
 
 
-def get_coulG(a, k, mesh, Gv=None, wrap_around=True):
+def get_coulG(a, k, mesh, Gv=None, wrap_around=True, omega=None):
     """[pyscf] tools.get_coulG(cell, k, mesh, Gv), exxdiv=None (fftisdf.py:114).
 
     4*pi/|k+G|^2, |k+G|^2 == 0 -> 0; for k != 0 the k+G vectors are wrapped by the
     box edge (mesh//2 + 1/2)·b and entries exactly on the edge are zeroed.
+    omega (get_coulG's range separation; used by the next-4 omega path, which the reference's
+    get_jk rejects): > 0 long range x exp(-|k+G|^2/4w^2); < 0 short range x (1 - exp(...)) with
+    the |k+G| = 0 limit pi/w^2.
     """
     b = 2 * np.pi * np.linalg.inv(a).T
     if Gv is None:
@@ -73,6 +76,13 @@ def get_coulG(a, k, mesh, Gv=None, wrap_around=True):
     with np.errstate(divide="ignore"):
         coulG = 4 * np.pi / g2
     coulG[g2 == 0] = 0
+    if omega:
+        f = np.exp(-0.25 * g2 / omega**2)
+        if omega > 0:
+            coulG *= f
+        else:
+            coulG *= 1 - f
+            coulG[g2 == 0] = np.pi / omega**2
     coulG[on_boundary] = 0
     return coulG
 
@@ -148,21 +158,21 @@ def build_y(f_k, xip, phase):
     return y_k.reshape(nkpt, nblk, nip)
 
 
-def fit_and_coulomb(x4_q, y_q, vq, coord, a, mesh, vol, Gv=None):
+def fit_and_coulomb(x4_q, y_q, vq, coord, a, mesh, vol, Gv=None, omega=None):
     """fftisdf.py:97-121 for one q: gelsy fit then FFT Coulomb -> (W_q, rank)."""
     ngrid = coord.shape[0]
     fq = np.exp(-1j * coord @ vq)                                     # :99
     res = scipy.linalg.lstsq(x4_q, y_q.T, lapack_driver="gelsy")     # :108
     z_q, rank = res[0], res[2]
     zeta = fft(z_q * fq, mesh)                                        # :113
-    zeta *= get_coulG(a, vq, mesh, Gv=Gv)                             # :114
+    zeta *= get_coulG(a, vq, mesh, Gv=Gv, omega=omega)                # :114
     zeta *= vol / ngrid                                               # :115
     zeta = ifft(zeta, mesh)                                           # :118
     zeta *= fq.conj()                                                 # :119
     return zeta @ z_q.conj().T, rank                                  # :121
 
 
-def build(xip, f_k, coord, a, kmesh, mesh, blksize=8000, progress=False):
+def build(xip, f_k, coord, a, kmesh, mesh, blksize=8000, progress=False, omega=None):
     """fftisdf.py:22-128 given the interpolation-point AOs ``xip`` and the grid AOs ``f_k``.
 
     Returns dict(x=xip, w0=W_0, wq=W_q, ranks=[...], y=y, x4=x4_k).
@@ -180,7 +190,7 @@ def build(xip, f_k, coord, a, kmesh, mesh, blksize=8000, progress=False):
     Gv = get_Gv(a, mesh)
     wq, ranks = [], []
     for q, vq in enumerate(kpts):                                     # :97
-        w, r = fit_and_coulomb(x4_k[q], y[q], vq, coord, a, mesh, vol, Gv)
+        w, r = fit_and_coulomb(x4_k[q], y[q], vq, coord, a, mesh, vol, Gv, omega)
         wq.append(w)
         ranks.append(r)
         if progress:

@@ -216,7 +216,7 @@ def test_not_implemented_paths():
     df, o, dm = make_df("toy222")
     df.build()
     with pytest.raises(NotImplementedError):
-        df.get_jk(dm, omega=0.3)
+        df.get_jk(dm, omega=0.3, exxdiv="ewald")   # range separation is supported alone
     with pytest.raises(NotImplementedError):
         df.get_jk(dm, exxdiv="vcut_sph")        # only 'ewald' is added (next-4)
     with pytest.raises(NotImplementedError):
@@ -353,3 +353,29 @@ def test_exxdiv_ewald():
     assert abs(d - d.conj().swapaxes(-1, -2)).max() < 1e-12
     _, vk2 = df.get_jk(dm, exxdiv="ewald")
     assert abs(vk2 - vk1).max() == 0.0
+
+
+@pytest.mark.parametrize("omega", [0.4, -0.4])
+def test_range_separated_omega(omega):
+    """next-4: get_jk(omega=w) = the ISDF J/K with PySCF get_coulG's range-separated kernel
+    (w > 0 long range erf, w < 0 short range erfc) — the oracle rebuilt with coulG(omega) on the
+    same points; the plain-Coulomb state is untouched and the omega state is cached."""
+    from oracle import isdf_ref as R
+    name = "toy331_fr"
+    df, o, dm = make_df(name)
+    df.build()
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
+    vj0, vk0 = df.get_jk(dm)
+    vj, vk = df.get_jk(dm, omega=omega)
+    out = R.build(o["xip"], chi, coords, cell.a, kmesh, cell.mesh, omega=omega)
+    kpts = R.get_kpts(cell.a, kmesh)
+    phase = R.get_phase(cell.a, kpts, kmesh)
+    vj_ref = R.get_j_kpts(o["xip"], out["w0"], dm)
+    vk_ref = R.get_k_kpts(o["xip"], out["wq"], dm, phase)
+    ej, ek = abs(vj - vj_ref).max(), abs(vk - vk_ref).max()
+    print(f"omega {omega}: |dJ| {ej:.2e} |dK| {ek:.2e}  (|K| {abs(vk_ref).max():.2e})")
+    assert ej < JK_TOL and ek < JK_TOL
+    assert abs(vk - vk0).max() > 1e-3            # a different kernel
+    vj1, vk1 = df.get_jk(dm)
+    assert abs(vj1 - vj0).max() == 0.0 and abs(vk1 - vk0).max() == 0.0
+    assert len(df._omega_dfs) == 1

@@ -62,7 +62,11 @@ def test_reference_surface():
     assert blocks[0][1] == 0 and blocks[-1][2] == 512
     assert blocks[0][0][0].shape == (6, 200, cell.nao_nr())
     with pytest.raises(NotImplementedError):
-        df.get_jk(dm, omega=0.1)
+        df.get_jk(dm, omega=0.1, exxdiv="ewald")   # range separation + exxdiv not supported
+    with pytest.raises(NotImplementedError):
+        df.get_jk(dm, exxdiv="vcut_sph")           # only 'ewald' (next-4)
+    with pytest.raises(NotImplementedError):
+        df.get_jk(dm[0], kpts=np.zeros(3))         # single k-point (fftisdf.py:399-401)
 
 
 def test_time_reversal_reps():
