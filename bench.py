@@ -181,44 +181,62 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = nk / (dt / args.steps)
 
-    # roofline of the dominant kernel: the Coulomb HERK W_q = Zhat Zhat^H (one launch per fitted
-    # q; HIP events around each launch on the library's stream).  Algorithmic flop per launch:
-    # 4 r^2 N (complex HERK), 2 r^2 N for a self-conjugate q (real-part HERK).
+    # roofline of the dominant kernel.  The fit's two MFMA kernels per fitted q have the same
+    # algorithmic work, 4 r^2 N flop (2 r^2 N for a self-conjugate q, real arithmetic):
+    #   trsm: U = L^-1 Yhat, one lower-triangular GEMM (half of the 8 r^2 N of a full GEMM),
+    #   herk: G = U U^H (Coulomb-weighted, Hermitian: lower tiles only).
+    # HIP events around each launch on the library's stream; the one with more time is
+    # `roofline`, the other `roofline_secondary`.
     ngrid = int(np.prod(cell.mesh))
     ranks = np.asarray(df.ranks, dtype=np.float64)
     real = np.array([bool(df.real_self_conjugate and df.q_partner[q] == q) for q in df.my_qs])
     flop_step = float(np.sum(np.where(real, 2.0, 4.0) * ranks ** 2) * ngrid)
-    herk_ms, herk_calls = stages["herk"]
-    achieved = flop_step * args.steps / (herk_ms * 1e-3) / 1e12 if herk_ms > 0 else 0.0
-    roof = {"bound": "mfma", "kernel": "zgemm_glds_kernel<0,3,true,*,3> (HERK W_q, split-K) + reduce",
-            "flop_note": "algorithmic 4 r^2 N per complex HERK (2 r^2 N real-part); the kernel "
-                         "executes 3 real MFMAs per complex block, so achieved/peak can reach 4/3",
-            "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_FP64_TFLOPS, 4), "traffic": None,
-            "flop_per_launch": flop_step / max(len(ranks), 1),
-            "avg_launch_ms": herk_ms / max(herk_calls, 1), "launches": int(herk_calls)}
-    # in the timed region the fit lanes share the CUs, so the per-launch HERK durations above
-    # include contention with the other lanes' TRSM/FFT; one extra untimed step with a single
-    # lane gives the kernel's own rate
+    KERNELS = {
+        "trsm": ("zgemm_glds_kernel<0,0,false,4|5,3> (lower-triangular GEMM U = L^-1 Yhat)",
+                 "trsm_gemm"),
+        "herk": ("zgemm_glds_kernel<0,3,true,*,3> (HERK W_q, split-K) + reduce", "herk"),
+    }
+    roofs = {}
+    for name, (label, _) in KERNELS.items():
+        ms, calls = stages[name]
+        ach = flop_step * args.steps / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        roofs[name] = {"bound": "mfma", "kernel": label,
+                       "flop_note": "algorithmic 4 r^2 N per complex q (2 r^2 N real); the kernel "
+                                    "executes 3 real MFMAs per complex block, so achieved/peak "
+                                    "can reach 4/3",
+                       "achieved": round(ach, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                       "frac": round(ach / PEAK_FP64_TFLOPS, 4), "traffic": None,
+                       "flop_per_launch": flop_step / max(len(ranks), 1),
+                       "avg_launch_ms": ms / max(calls, 1), "launches": int(calls),
+                       "ms_per_step": round(ms / args.steps, 3)}
+    # in the timed region the fit lanes share the CUs, so the per-launch durations above
+    # include contention with the other lane's kernels; one extra untimed step with a single
+    # lane gives each kernel's own rate
     d.ctx.call("fisdf_set_fit_lanes", 1)
     d.ctx.call("fisdf_set_timing", 1)
     d.ctx.timings()
     step()
     torch.cuda.synchronize()
-    iso_ms, iso_calls = d.ctx.timings()["herk"]
+    iso_st = d.ctx.timings()
     d.ctx.call("fisdf_set_timing", 0)
     d.ctx.call("fisdf_set_fit_lanes", 0)
-    if iso_ms > 0:
-        iso = flop_step / (iso_ms * 1e-3) / 1e12
-        roof["isolated"] = {"achieved": round(iso, 3), "frac": round(iso / PEAK_FP64_TFLOPS, 4),
-                            "avg_launch_ms": iso_ms / max(iso_calls, 1),
-                            "note": "one untimed step after the timed region, 1 fit lane"}
     tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tfile):
-        t = json.load(open(tfile))
-        if "herk" in t:  # rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes, tools/prof_round.sh
-            roof["traffic"] = t["herk"]["hbm_bytes_per_launch"]
-            roof["traffic_unit"] = "bytes/launch (measured, " + t.get("source", "profiles") + ")"
+    traffic = json.load(open(tfile)) if os.path.exists(tfile) else {}
+    for name, (label, tkey) in KERNELS.items():
+        iso_ms, iso_calls = iso_st[name]
+        if iso_ms > 0:
+            iso = flop_step / (iso_ms * 1e-3) / 1e12
+            roofs[name]["isolated"] = {"achieved": round(iso, 3),
+                                       "frac": round(iso / PEAK_FP64_TFLOPS, 4),
+                                       "avg_launch_ms": iso_ms / max(iso_calls, 1),
+                                       "note": "one untimed step after the timed region, 1 fit lane"}
+        if tkey in traffic:  # rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes, tools/prof_round.sh
+            roofs[name]["traffic"] = traffic[tkey]["hbm_bytes_per_launch"]
+            roofs[name]["traffic_unit"] = ("bytes/launch (measured, "
+                                           + traffic.get("source", "profiles") + ")")
+    dom = max(roofs, key=lambda n: roofs[n]["ms_per_step"])
+    roof = roofs[dom]
+    roof2 = roofs["herk" if dom == "trsm" else "trsm"]
 
     # input layer: Bloch AO values on the FFT grid by the GPU evaluator,
     # checked against the host restatement the timed steps used; outside the timed region
@@ -254,6 +272,7 @@ def main():
                        "nip": int(df.nip), "ngrid": ngrid, "fit": "pivoted-Cholesky factored",
                        "parallelism": f"k-shard x{world}"},
             "roofline": roof,
+            "roofline_secondary": roof2,
             "cpu_baseline": cpu,
             "ao_eval": ao,
             "stages_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()},
