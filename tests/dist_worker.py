@@ -43,8 +43,24 @@ def main():
         phase = R.get_phase(cell.a, kpts, kmesh)
         vj0 = R.get_j_kpts(xip, ob["w0"], dm, kpts_band_is_zero=bool(abs(kpts).max() < 1e-9))
         vk0 = R.get_k_kpts(xip, ob["wq"], dm, phase)
+    extra = {}
+    if os.environ.get("FISDF_DIST_EXTRAS") == "1":
+        # next-4 in the sharded path: exxdiv='ewald' (the correction is added after the vk
+        # all-reduce) and a range-separated refit (a collective build on every rank)
+        from oracle import isdf_ref as R
+        from fisdf.cell import madelung
+        _, vk_e = df.get_jk(dm, exxdiv="ewald")
+        S = np.einsum("kgm,kgn->kmn", chi.conj(), chi) * (cell.vol / chi.shape[1])
+        vke0 = vk0 + madelung(cell, kmesh) * np.einsum("kmp,xkpq,kqn->xkmn", S, dm, S)
+        vj_w, vk_w = df.get_jk(dm, omega=0.4)
+        xip = x0[:, df.perm]
+        ob = R.build(xip, chi, coords, cell.a, kmesh, cell.mesh, omega=0.4)
+        kpts = R.get_kpts(cell.a, kmesh)
+        phase = R.get_phase(cell.a, kpts, kmesh)
+        extra = dict(vk_e=vk_e, vke0=vke0, vj_w=vj_w, vk_w=vk_w,
+                     vjw0=R.get_j_kpts(xip, ob["w0"], dm), vkw0=R.get_k_kpts(xip, ob["wq"], dm, phase))
     np.savez(out, vj=vj, vk=vk, perm=df.perm, ranks=df.ranks, vj0=vj0, vk0=vk0,
-             perm0=o["perm"])
+             perm0=o["perm"], **extra)
     torch.cuda.synchronize()
     dist.destroy_process_group()
 

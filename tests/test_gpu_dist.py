@@ -30,7 +30,8 @@ def test_sharded_build_matches_oracle(name, world):
         procs = []
         for r in range(world):
             env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
-                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                       FISDF_DIST_EXTRAS="1" if name == "toy333_fr" else "0")
             procs.append(subprocess.Popen(
                 [sys.executable, os.path.join(HERE, "dist_worker.py"), name, "gloo",
                  os.path.join(tmp, f"r{r}.npz")], env=env))
@@ -46,6 +47,12 @@ def test_sharded_build_matches_oracle(name, world):
         # time reversal (1.5e-8 bar, test_gpu_isdf.py)
         tol = 1.5e-8 if name == "toy331" else 1e-8
         assert ej < tol and ek < tol
+        if "vk_e" in o:   # exxdiv='ewald' and omega=0.4 through the sharded path (next-4)
+            ee = abs(o["vk_e"] - o["vke0"]).max()
+            ewj, ewk = abs(o["vj_w"] - o["vjw0"]).max(), abs(o["vk_w"] - o["vkw0"]).max()
+            print(f"  ewald |dK|={ee:.2e}  omega=0.4 |dJ|={ewj:.2e} |dK|={ewk:.2e}")
+            assert ee < tol and ewj < tol and ewk < tol
+            assert abs(o["vk_w"] - outs[0]["vk_w"]).max() == 0.0
         # every rank returns the same J/K and the same pivots
         assert abs(o["vj"] - outs[0]["vj"]).max() == 0.0
         assert np.array_equal(o["perm"], outs[0]["perm"])
