@@ -140,3 +140,20 @@ def test_get_coul_lstsq_and_eri_harness():
                     optimize=True)
     got = isdf.get_eri(cell.get_kpts(kmesh)[[k1_, k2_, k3_, k4_]])
     assert abs(got.reshape(ref.shape) - ref).max() < 1e-10 * max(1.0, abs(ref).max())
+
+
+@pytest.mark.gpu
+def test_get_coul_gamma_default_kmesh():
+    """kmesh=None is the reference's [1, 1, 1] (fftdf-with-k-lstsq.py:25-26): a Gamma-only
+    get_coul on the C1-shaped diamond gth-szv cell; coul_q (1, nip, nip) is real-symmetric up to
+    rounding and equals the oracle's W on the same points."""
+    from oracle import isdf_ref as R
+    cell, kmesh, m0, c0, x0, coords, chi, dm = _toy("diamond_szv_gamma")
+    df = coul.FFTDF(cell)
+    c, x = coul.get_coul_pinv(df, m0=list(m0), nip=int(cell.nao_nr() * c0))
+    assert c.shape[0] == 1 and x.shape[0] == 1
+    assert abs(c[0] - c[0].T.conj()).max() < 1e-10 * abs(c).max()
+    out = R.build(x0[:, df._isdf.perm], chi, coords, cell.a, (1, 1, 1), cell.mesh)
+    err = abs(c - out["wq"]).max()
+    print("Gamma coul_q vs oracle", err, "scale", abs(out["wq"]).max())
+    assert err < 1e-8 * max(1.0, abs(out["wq"]).max())
