@@ -57,6 +57,7 @@ struct fisdf_ctx {
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_ybuf[4] = {nullptr, nullptr, nullptr, nullptr};  // y pipeline: fx ready / free
+  std::vector<hipEvent_t> ev_q;  // FISDF_FIT_PIPE: Yhat of fitted q ready (FFT stream)
   int* f_piv = nullptr;     // (nk, nip)
   int* f_rank_dev = nullptr;
   std::vector<int> f_rank;  // host copy
@@ -419,6 +420,7 @@ int fisdf_destroy(fisdf_ctx* c) {
     }
     for (int l = 0; l < 4; ++l) (void)hipEventDestroy(c->ev_ybuf[l]);
   }
+  for (hipEvent_t e : c->ev_q) (void)hipEventDestroy(e);
   if (c->arena) (void)hipFree(c->arena);
   if (c->ev_stage) (void)hipEventSynchronize(c->ev_stage), (void)hipEventDestroy(c->ev_stage);
   if (c->stage_pinned) (void)hipHostFree(c->stage_pinned);
@@ -1118,15 +1120,37 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   // q are processed on NL "lanes" (the main stream and aux streams), each with its own
   // workspaces, so one q's HBM-bound FFT and memory-stalled HERK overlap another q's
   // MFMA-bound TRSM on the same CUs
-  const int NL = std::min(nq, c->lanes > 0 ? c->lanes : env_fit_lanes());
+  int NL = std::min(nq, c->lanes > 0 ? c->lanes : env_fit_lanes());
+  // Pipelined FFTs (default with >= 2 lanes; FISDF_FIT_PIPE=0 turns it off): every q's
+  // HBM-bound FFT runs on its own stream into a per-q Yhat buffer (nq x rmax x ngrid: 16 GB at
+  // C3), ahead of the MFMA lanes, which wait per q on its event — the FFTs then always overlap
+  // TRSM/HERK work instead of meeting another lane's FFT.  C3, interleaved A/B on two boxes:
+  // 100.44 vs 100.90 and 102.3 vs 103.5 ms/step (3 pairs each); with a single MFMA lane it
+  // is slower (107.8), so one lane keeps the FFT in-lane.
+  static const bool pipe_env = [] {
+    const char* e = getenv("FISDF_FIT_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  const bool pipe = pipe_env && nq > 1 && NL > 1;
+  if (pipe) NL = std::min(NL, 2);
   Carver cv;
   size_t oY[4], oU[4], oWt[4], oK[4], oTc[4];
+  size_t oYall = 0, oWall = 0;
   for (int l = 0; l < NL; ++l) {
-    oY[l] = cv.take(sizeof(cplx) * rmax * ngrid);
+    if (!pipe) oY[l] = cv.take(sizeof(cplx) * rmax * ngrid);
     oU[l] = cv.take(sizeof(cplx) * rmax * ngrid);
-    oWt[l] = cv.take(sizeof(double) * ngrid);
+    if (!pipe) oWt[l] = cv.take(sizeof(double) * ngrid);
     oK[l] = cv.take(sizeof(cplx) * (size_t)ks * rmax * rmax);
     oTc[l] = cv.take(sizeof(cplx) * rr);
+  }
+  if (pipe) {
+    oYall = cv.take(sizeof(cplx) * (size_t)nq * rmax * ngrid);
+    oWall = cv.take(sizeof(double) * (size_t)nq * ngrid);
+    while ((int)c->ev_q.size() < nq) {
+      hipEvent_t e;
+      FISDF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c->ev_q.push_back(e);
+    }
   }
   size_t oG = cv.take(sizeof(cplx) * nq * rr);
   size_t oT = cv.take(sizeof(cplx) * nq * rr);
@@ -1144,20 +1168,47 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   }
   FISDF_HIP(hipMemsetAsync(G, 0, sizeof(cplx) * nq * rr, c->stream));
   hipStream_t lane_st[4] = {c->stream, nullptr, nullptr, nullptr};
-  if (NL > 1) {
+  hipStream_t fst = nullptr;  // the FFT stream of the pipelined mode
+  if (NL > 1 || pipe) {
     FISDF_TRY(ensure_aux(c));
     FISDF_HIP(hipEventRecord(c->ev_fork, c->stream));
     for (int l = 1; l < NL; ++l) {
       lane_st[l] = c->aux[l - 1];
       FISDF_HIP(hipStreamWaitEvent(lane_st[l], c->ev_fork, 0));
     }
+    if (pipe) {
+      fst = c->aux[2];
+      FISDF_HIP(hipStreamWaitEvent(fst, c->ev_fork, 0));
+    }
+  }
+  // Yhat_q = FFT(y_q[:, piv] * f_q) * w_q   (:99, :113-115, :118; rows in pivot order)
+  auto fft_q = [&](hipStream_t st, int lq, cplx* Yh, double* wt) -> int {
+    const int sl = s0 + lq;
+    const int r = c->f_rank[sl];
+    double kq[3], kd[3];
+    kpoint(kmesh, g, h_qs[lq], kq);
+    for (int i = 0; i < 3; ++i) kd[i] = g.a[i][0] * kq[0] + g.a[i][1] * kq[1] + g.a[i][2] * kq[2];
+    StageTimer tm(c, FISDF_ST_FFT, st);
+    // sqrt(coulG(k_q+G) vol/N^2)  (:114-115 and the Parseval 1/N of :118)
+    FISDF_TRY(coulg_weight(st, mesh, g, kq, vol / ((double)ngrid * ngrid), 1, wt, c->omega));
+    FISDF_TRY(fft3d(st, yT + (long)lq * nip * ngrid, ngrid, c->f_piv + (long)sl * nip, Yh, ngrid,
+                    r, mesh[0], mesh[1], mesh[2], kd, wt, nullptr));
+    return 0;
+  };
+  if (pipe) {
+    for (int lq = 0; lq < nq; ++lq) {
+      if (c->f_rank[s0 + lq] == 0) continue;
+      FISDF_TRY(fft_q(fst, lq, (cplx*)(b + oYall) + (long)lq * rmax * ngrid,
+                      (double*)(b + oWall) + (long)lq * ngrid));
+      FISDF_HIP(hipEventRecord(c->ev_q[lq], fst));
+    }
   }
   for (int lq = 0; lq < nq; ++lq) {
     const int ln = lq % NL;
     hipStream_t st = lane_st[ln];
-    cplx* Yh = (cplx*)(b + oY[ln]);
+    cplx* Yh = pipe ? (cplx*)(b + oYall) + (long)lq * rmax * ngrid : (cplx*)(b + oY[ln]);
     cplx* U = (cplx*)(b + oU[ln]);
-    double* wt = (double*)(b + oWt[ln]);
+    double* wt = pipe ? (double*)(b + oWall) + (long)lq * ngrid : (double*)(b + oWt[ln]);
     cplx* kw = (cplx*)(b + oK[ln]);
     cplx* Tc = (cplx*)(b + oTc[ln]);
     const int q = h_qs[lq];
@@ -1168,17 +1219,11 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     const cplx* Lp = c->f_Lp + (long)sl * nn;
     const bool real_q = c->f_real[sl];
     const cplx* Linv = c->f_Linv + (long)sl * sLi;
-    double kq[3], kd[3];
-    kpoint(kmesh, g, q, kq);
-    for (int i = 0; i < 3; ++i) kd[i] = g.a[i][0] * kq[0] + g.a[i][1] * kq[1] + g.a[i][2] * kq[2];
-    {
-      StageTimer tm(c, FISDF_ST_FFT, st);
-      // sqrt(coulG(k_q+G) vol/N^2)  (:114-115 and the Parseval 1/N of :118)
-      FISDF_TRY(coulg_weight(st, mesh, g, kq, vol / ((double)ngrid * ngrid), 1, wt, c->omega));
-      // Yh = FFT(y_q[:, piv] * f_q) * w   (:99, :113; rows in pivot order)
-      FISDF_TRY(fft3d(st, yT + (long)lq * nip * ngrid, ngrid, piv, Yh, ngrid, r, mesh[0],
-                      mesh[1], mesh[2], kd, wt, nullptr));
-    }
+    (void)piv;
+    if (pipe)
+      FISDF_HIP(hipStreamWaitEvent(st, c->ev_q[lq], 0));
+    else
+      FISDF_TRY(fft_q(st, lq, Yh, wt));
     cplx* Uq = U;  // where L^{-1} Yh lands
     if (c->f_fac_unjoined) FISDF_HIP(hipStreamWaitEvent(st, c->ev_fac, 0));  // L^-1, Q, ...
     {
@@ -1227,6 +1272,10 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   for (int l = 1; l < NL; ++l) {  // join the lanes before the batched small stage
     FISDF_HIP(hipEventRecord(c->ev_join[l - 1], lane_st[l]));
     FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_join[l - 1], 0));
+  }
+  if (pipe) {  // (the lanes waited on every FFT already; this keeps the arena reuse ordered)
+    FISDF_HIP(hipEventRecord(c->ev_join[2], fst));
+    FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_join[2], 0));
   }
   FISDF_TRY(join_factors(c));
   {
