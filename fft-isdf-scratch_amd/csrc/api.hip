@@ -1132,7 +1132,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     return !(e && e[0] == '0');
   }();
   const bool pipe = pipe_env && nq > 1 && NL > 1;
-  if (pipe) NL = std::min(NL, 2);
+  if (pipe) NL = std::min(NL, 3);  // aux[0..1] + the main stream; aux[2] is the FFT stream
   Carver cv;
   size_t oY[4], oU[4], oWt[4], oK[4], oTc[4];
   size_t oYall = 0, oWall = 0;
