@@ -58,6 +58,12 @@ struct fisdf_ctx {
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_ybuf[4] = {nullptr, nullptr, nullptr, nullptr};  // y pipeline: fx ready / free
   std::vector<hipEvent_t> ev_q;  // FISDF_FIT_PIPE: Yhat of fitted q ready (FFT stream)
+  std::vector<hipEvent_t> ev_free;  // FISDF_FIT_PIPE: Yhat ring slot read by its lane
+  int pipe_mode = -1;   // fisdf_set_fit_pipe; -1: environment FISDF_FIT_PIPE (default on)
+  int pipe_depth = 0;   // ring slots; 0: FISDF_PIPE_DEPTH or lanes + 2
+  int last_fit_lanes = 0, last_fit_pipe = 0;  // what the last fisdf_fit_coulomb_qs ran with
+  std::vector<hipEvent_t> ev_ready;  // fisdf_mark_y_ready: y of local q j landed (sharded fit)
+  std::vector<char> ready_marked;
   int* f_piv = nullptr;     // (nk, nip)
   int* f_rank_dev = nullptr;
   std::vector<int> f_rank;  // host copy
@@ -90,8 +96,14 @@ int arena_get(fisdf_ctx* c, size_t bytes, void** out) {
     FISDF_HIP(hipStreamSynchronize(c->stream));
     if (c->arena) FISDF_HIP(hipFree(c->arena));
     c->arena = nullptr;
+    c->arena_size = 0;  // a failed growth below must not leave a stale size behind a null base
     size_t sz = bytes + bytes / 8;
-    FISDF_HIP(hipMalloc(&c->arena, sz));
+    if (hipMalloc(&c->arena, sz) != hipSuccess) {
+      (void)hipGetLastError();
+      c->arena = nullptr;
+      FISDF_HIP(hipMalloc(&c->arena, bytes));  // without the growth slack, then give up
+      sz = bytes;
+    }
     c->arena_size = sz;
   }
   *out = c->arena;
@@ -306,6 +318,22 @@ int env_fit_lanes() {
   return n;
 }
 
+int env_fit_pipe() {
+  static const int v = [] {
+    const char* e = getenv("FISDF_FIT_PIPE");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
+int env_pipe_depth(int lanes) {
+  static const int v = [] {
+    const char* e = getenv("FISDF_PIPE_DEPTH");
+    return e ? atoi(e) : 0;
+  }();
+  return v > 0 ? v : lanes + 2;
+}
+
 int ensure_aux(fisdf_ctx* c) {
   if (c->ev_fork) return 0;
   FISDF_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
@@ -421,6 +449,8 @@ int fisdf_destroy(fisdf_ctx* c) {
     for (int l = 0; l < 4; ++l) (void)hipEventDestroy(c->ev_ybuf[l]);
   }
   for (hipEvent_t e : c->ev_q) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->ev_free) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->ev_ready) (void)hipEventDestroy(e);
   if (c->arena) (void)hipFree(c->arena);
   if (c->ev_stage) (void)hipEventSynchronize(c->ev_stage), (void)hipEventDestroy(c->ev_stage);
   if (c->stage_pinned) (void)hipHostFree(c->stage_pinned);
@@ -890,6 +920,44 @@ int factor_pivoted(fisdf_ctx* c, hipStream_t s) {
   return factor_finish(c, s, (const int*)(b + oR));
 }
 
+// the greedy pivoted factorisation of only the listed slots (those whose unpivoted Cholesky
+// failed the full-rank test): gathered into a contiguous batch, factored, scattered back, so a
+// q's factor does not depend on which other q share the batch (1-GPU and sharded builds agree)
+int factor_pivoted_slots(fisdf_ctx* c, hipStream_t s, const std::vector<int>& slots) {
+  const int nk = c->f_nk, nip = c->f_nip, nf = (int)slots.size();
+  const long nn = (long)nip * nip;
+  char* b = (char*)c->f_scratch;
+  Carver cv;
+  size_t oR = cv.take(sizeof(int) * nk);
+  size_t oD = cv.take(sizeof(double) * (size_t)nk * nip);
+  size_t oF = cv.take(sizeof(int) * nk);
+  size_t oW = cv.take(sizeof(double) * (size_t)nk * (1 + nip));
+  size_t oU = cv.take(sizeof(int) * nk);  // the unpivoted path's per-slot ranks
+  cplx *A = nullptr, *L = nullptr;
+  int* P = nullptr;
+  FISDF_HIP(hipMallocAsync((void**)&A, sizeof(cplx) * nf * nn, s));
+  FISDF_HIP(hipMallocAsync((void**)&L, sizeof(cplx) * nf * nn, s));
+  FISDF_HIP(hipMallocAsync((void**)&P, sizeof(int) * (size_t)nf * nip, s));
+  for (int j = 0; j < nf; ++j)
+    FISDF_HIP(hipMemcpyAsync(A + j * nn, c->f_x4s + slots[j] * nn, sizeof(cplx) * nn,
+                             hipMemcpyDeviceToDevice, s));
+  FISDF_TRY(pchol(s, A, nip, nn, nip, nf, nip, c->f_tol, 0.0, L, P, (int*)(b + oR),
+                  (double*)(b + oD), (int*)(b + oF), (double*)(b + oW)));
+  for (int j = 0; j < nf; ++j) {
+    const int i = slots[j];
+    FISDF_HIP(hipMemcpyAsync(c->f_L + i * nn, L + j * nn, sizeof(cplx) * nn, hipMemcpyDeviceToDevice, s));
+    FISDF_HIP(hipMemcpyAsync(c->f_piv + (long)i * nip, P + (long)j * nip, sizeof(int) * nip,
+                             hipMemcpyDeviceToDevice, s));
+    FISDF_HIP(hipMemcpyAsync((int*)(b + oU) + i, (int*)(b + oR) + j, sizeof(int),
+                             hipMemcpyDeviceToDevice, s));
+  }
+  FISDF_HIP(hipFreeAsync(A, s));
+  FISDF_HIP(hipFreeAsync(L, s));
+  FISDF_HIP(hipFreeAsync(P, s));
+  c->f_used_pivoted = true;
+  return factor_finish(c, s, (const int*)(b + oU));
+}
+
 static int ensure_side(fisdf_ctx* c) {
   if (!c->side) {
     // FISDF_SIDE_PRIO=1: the factorisation (a chain of small kernels beside the y build's
@@ -1027,6 +1095,41 @@ int fisdf_set_fit_lanes(fisdf_ctx* c, int lanes) {
   return 0;
 }
 
+int fisdf_set_fit_pipe(fisdf_ctx* c, int mode, int depth) {
+  FISDF_CHECK(c != nullptr && mode >= -1 && mode <= 1 && depth >= 0 && depth <= 64,
+              "set_fit_pipe: mode must be -1..1, depth 0..64");
+  c->pipe_mode = mode;
+  c->pipe_depth = depth;
+  return 0;
+}
+
+int fisdf_mark_y_ready(fisdf_ctx* c, int j) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(j >= 0 && j < 4096, "mark_y_ready: bad index");
+  while ((int)c->ev_ready.size() <= j) {
+    hipEvent_t e;
+    FISDF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->ev_ready.push_back(e);
+  }
+  if ((int)c->ready_marked.size() <= j) c->ready_marked.resize(j + 1, 0);
+  FISDF_HIP(hipEventRecord(c->ev_ready[j], c->stream));
+  c->ready_marked[j] = 1;
+  return 0;
+}
+
+int fisdf_fit_info(fisdf_ctx* c, int* h_lanes, int* h_pipe_depth) {
+  FISDF_CHECK(c != nullptr, "null context");
+  if (h_lanes) *h_lanes = c->last_fit_lanes;
+  if (h_pipe_depth) *h_pipe_depth = c->last_fit_pipe;
+  return 0;
+}
+
+int fisdf_reserve_workspace(fisdf_ctx* c, size_t bytes) {
+  FISDF_TRY(device_guard(c));
+  void* base;
+  return arena_get(c, bytes, &base);
+}
+
 int fisdf_factor_info(fisdf_ctx* c, int* h_used_pivoted) {
   FISDF_CHECK(c != nullptr, "null context");
   if (h_used_pivoted) *h_used_pivoted = c->f_used_pivoted ? 1 : 0;
@@ -1041,11 +1144,12 @@ int fisdf_factor_x4_wait(fisdf_ctx* c, int* h_ranks) {
     FISDF_HIP(hipEventSynchronize(c->ev_chol));
     bool redone = false;
     if (c->f_check_fail) {
-      bool any = false;
-      for (int q = 0; q < c->f_nk; ++q) any |= c->f_fail_pinned[q] != 0;
+      std::vector<int> failed;
+      for (int q = 0; q < c->f_nk; ++q)
+        if (c->f_fail_pinned[q] != 0) failed.push_back(q);
       c->f_check_fail = false;
-      if (any) {  // not numerically full rank at tol: rank-revealing pivoted factorisation
-        FISDF_TRY(factor_pivoted(c, c->side));
+      if (!failed.empty()) {  // not numerically full rank at tol: rank-revealing factorisation
+        FISDF_TRY(factor_pivoted_slots(c, c->side, failed));
         FISDF_HIP(hipEventRecord(c->ev_fac, c->side));
         FISDF_HIP(hipEventSynchronize(c->ev_fac));
         redone = true;
@@ -1114,44 +1218,81 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     const char* e = getenv("FISDF_HERK_KS");
     return e ? atoi(e) : 0;
   }();
-  const int ks = ks_env > 0 ? ks_env : pick_ksplit_herk(rmax, (int)ngrid, num_cus(c->device));
+  // split-K of each q's HERK from its own rank (not the call's largest), so a q's arithmetic
+  // does not depend on which other q share the call (1-GPU vs sharded builds agree bitwise)
+  const int ncu = num_cus(c->device);
+  auto ks_of = [&](int r) { return ks_env > 0 ? ks_env : pick_ksplit_herk(r, (int)ngrid, ncu); };
+  int ks = 1;
+  for (int lq = 0; lq < nq; ++lq) ks = std::max(ks, ks_of(c->f_rank[s0 + lq]));
   const long rr = (long)rmax * rmax;
   const long sLi = (long)nblk * nb * nb;
   // q are processed on NL "lanes" (the main stream and aux streams), each with its own
   // workspaces, so one q's HBM-bound FFT and memory-stalled HERK overlap another q's
   // MFMA-bound TRSM on the same CUs
   int NL = std::min(nq, c->lanes > 0 ? c->lanes : env_fit_lanes());
-  // Pipelined FFTs (default with >= 2 lanes; FISDF_FIT_PIPE=0 turns it off): every q's
-  // HBM-bound FFT runs on its own stream into a per-q Yhat buffer (nq x rmax x ngrid: 16 GB at
-  // C3), ahead of the MFMA lanes, which wait per q on its event — the FFTs then always overlap
-  // TRSM/HERK work instead of meeting another lane's FFT.  C3, interleaved A/B on two boxes:
-  // 100.44 vs 100.90 and 102.3 vs 103.5 ms/step (3 pairs each); with a single MFMA lane it
-  // is slower (107.8), so one lane keeps the FFT in-lane.
-  static const bool pipe_env = [] {
-    const char* e = getenv("FISDF_FIT_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  const bool pipe = pipe_env && nq > 1 && NL > 1;
-  if (pipe) NL = std::min(NL, 3);  // aux[0..1] + the main stream; aux[2] is the FFT stream
+  // Pipelined FFTs (default with >= 2 lanes; fisdf_set_fit_pipe / FISDF_FIT_PIPE=0 turn it
+  // off): the HBM-bound FFTs run on their own stream into a ring of D Yhat slots, ahead of the
+  // MFMA lanes, which wait per q on its event — the FFTs then overlap TRSM/HERK work instead of
+  // meeting another lane's FFT.  A slot is reused once the lane that read it records its
+  // `free` event, so the working set is D x rmax x ngrid (D = lanes + 2 by default) whatever
+  // nq is.  With a single MFMA lane it is slower (C3 107.8 vs 100.9 ms/step), so one lane
+  // keeps the FFT in-lane.
+  const int pipe_mode = c->pipe_mode >= 0 ? c->pipe_mode : env_fit_pipe();
+  bool pipe = pipe_mode != 0 && nq > 1 && NL > 1;
+  // sharded build (fisdf_mark_y_ready): y of the call's j-th q lands at ev_ready[j] on the main
+  // stream (all-to-all piece + unpack); the lanes then run on the aux streams only and each q
+  // starts as soon as its own piece is there, one call for the whole shard
+  int nready = 0;
+  for (int lq = 0; lq < nq; ++lq)
+    nready += (lq < (int)c->ready_marked.size() && c->ready_marked[lq]) ? 1 : 0;
+  FISDF_CHECK(nready == 0 || nready == nq, "fit_coulomb: mark every q of the call ready, or none");
+  const bool ready = nready > 0;
+  if (pipe) NL = std::min(NL, ready ? 2 : 3);  // aux[2] is the FFT stream
+  if (ready) NL = std::min(NL, 3);
+  int D = pipe ? std::min(nq, c->pipe_depth > 0 ? c->pipe_depth : env_pipe_depth(NL)) : 0;
   Carver cv;
   size_t oY[4], oU[4], oWt[4], oK[4], oTc[4];
   size_t oYall = 0, oWall = 0;
-  for (int l = 0; l < NL; ++l) {
-    if (!pipe) oY[l] = cv.take(sizeof(cplx) * rmax * ngrid);
-    oU[l] = cv.take(sizeof(cplx) * rmax * ngrid);
-    if (!pipe) oWt[l] = cv.take(sizeof(double) * ngrid);
-    oK[l] = cv.take(sizeof(cplx) * (size_t)ks * rmax * rmax);
-    oTc[l] = cv.take(sizeof(cplx) * rr);
+  auto carve = [&]() {
+    cv = Carver();
+    for (int l = 0; l < NL; ++l) {
+      if (!pipe) oY[l] = cv.take(sizeof(cplx) * rmax * ngrid);
+      oU[l] = cv.take(sizeof(cplx) * rmax * ngrid);
+      if (!pipe) oWt[l] = cv.take(sizeof(double) * ngrid);
+      oK[l] = cv.take(sizeof(cplx) * (size_t)ks * rmax * rmax);
+      oTc[l] = cv.take(sizeof(cplx) * rr);
+    }
+    if (pipe) {
+      oYall = cv.take(sizeof(cplx) * (size_t)D * rmax * ngrid);
+      oWall = cv.take(sizeof(double) * (size_t)D * ngrid);
+    }
+  };
+  carve();
+  if (pipe && cv.off > c->arena_size) {
+    // the ring's extra slots only if the device has room for them; else the in-lane FFT
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+    const size_t extra = (size_t)D * rmax * ngrid * sizeof(cplx);
+    if (free_b + c->arena_size < cv.off + extra / 8) {
+      pipe = false;
+      D = 0;
+      carve();
+    }
   }
   if (pipe) {
-    oYall = cv.take(sizeof(cplx) * (size_t)nq * rmax * ngrid);
-    oWall = cv.take(sizeof(double) * (size_t)nq * ngrid);
     while ((int)c->ev_q.size() < nq) {
       hipEvent_t e;
       FISDF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       c->ev_q.push_back(e);
     }
+    while ((int)c->ev_free.size() < D) {
+      hipEvent_t e;
+      FISDF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c->ev_free.push_back(e);
+    }
   }
+  c->last_fit_lanes = NL;
+  c->last_fit_pipe = pipe ? D : 0;
   size_t oG = cv.take(sizeof(cplx) * nq * rr);
   size_t oT = cv.take(sizeof(cplx) * nq * rr);
   size_t oS = cv.take(sizeof(cplx) * nq * rr);
@@ -1163,23 +1304,46 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   cplx* S = (cplx*)(b + oS);
   if (rmax == 0) {
     FISDF_TRY(join_factors(c));
+    c->ready_marked.assign(c->ready_marked.size(), 0);
     FISDF_HIP(hipMemsetAsync(Wq, 0, sizeof(cplx) * nq * nn, c->stream));
     return 0;
   }
-  FISDF_HIP(hipMemsetAsync(G, 0, sizeof(cplx) * nq * rr, c->stream));
   hipStream_t lane_st[4] = {c->stream, nullptr, nullptr, nullptr};
   hipStream_t fst = nullptr;  // the FFT stream of the pipelined mode
-  if (NL > 1 || pipe) {
+  bool aux_used[3] = {false, false, false};
+  if (ready) {
+    // everything enqueued before the first piece landed (the y build, the arena's previous
+    // users) is complete at ev_ready[0]
+    FISDF_TRY(ensure_aux(c));
+    for (int l = 0; l < NL; ++l) {
+      lane_st[l] = c->aux[l];
+      aux_used[l] = true;
+      FISDF_HIP(hipStreamWaitEvent(lane_st[l], c->ev_ready[0], 0));
+    }
+    FISDF_HIP(hipMemsetAsync(G, 0, sizeof(cplx) * nq * rr, lane_st[0]));
+    FISDF_HIP(hipEventRecord(c->ev_fork, lane_st[0]));
+    for (int l = 1; l < NL; ++l) FISDF_HIP(hipStreamWaitEvent(lane_st[l], c->ev_fork, 0));
+    if (pipe) {
+      fst = c->aux[2];
+      aux_used[2] = true;
+      FISDF_HIP(hipStreamWaitEvent(fst, c->ev_fork, 0));
+    }
+  } else if (NL > 1 || pipe) {
+    FISDF_HIP(hipMemsetAsync(G, 0, sizeof(cplx) * nq * rr, c->stream));
     FISDF_TRY(ensure_aux(c));
     FISDF_HIP(hipEventRecord(c->ev_fork, c->stream));
     for (int l = 1; l < NL; ++l) {
       lane_st[l] = c->aux[l - 1];
+      aux_used[l - 1] = true;
       FISDF_HIP(hipStreamWaitEvent(lane_st[l], c->ev_fork, 0));
     }
     if (pipe) {
       fst = c->aux[2];
+      aux_used[2] = true;
       FISDF_HIP(hipStreamWaitEvent(fst, c->ev_fork, 0));
     }
+  } else {
+    FISDF_HIP(hipMemsetAsync(G, 0, sizeof(cplx) * nq * rr, c->stream));
   }
   // Yhat_q = FFT(y_q[:, piv] * f_q) * w_q   (:99, :113-115, :118; rows in pivot order)
   auto fft_q = [&](hipStream_t st, int lq, cplx* Yh, double* wt) -> int {
@@ -1195,35 +1359,46 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
                     r, mesh[0], mesh[1], mesh[2], kd, wt, nullptr));
     return 0;
   };
-  if (pipe) {
-    for (int lq = 0; lq < nq; ++lq) {
-      if (c->f_rank[s0 + lq] == 0) continue;
-      FISDF_TRY(fft_q(fst, lq, (cplx*)(b + oYall) + (long)lq * rmax * ngrid,
-                      (double*)(b + oWall) + (long)lq * ngrid));
-      FISDF_HIP(hipEventRecord(c->ev_q[lq], fst));
-    }
-  }
+  // ring slot of q lq (pipelined mode)
+  auto slot_y = [&](int lq) { return (cplx*)(b + oYall) + (long)(lq % D) * rmax * ngrid; };
+  auto slot_w = [&](int lq) { return (double*)(b + oWall) + (long)(lq % D) * ngrid; };
+  // FFT of q lq into its ring slot, after the lane that read the slot's previous q is done
+  auto enqueue_fft = [&](int lq) -> int {
+    if (lq >= nq || c->f_rank[s0 + lq] == 0) return 0;
+    if (lq >= D) FISDF_HIP(hipStreamWaitEvent(fst, c->ev_free[lq % D], 0));
+    if (ready) FISDF_HIP(hipStreamWaitEvent(fst, c->ev_ready[lq], 0));
+    FISDF_TRY(fft_q(fst, lq, slot_y(lq), slot_w(lq)));
+    FISDF_HIP(hipEventRecord(c->ev_q[lq], fst));
+    return 0;
+  };
+  if (pipe)
+    for (int lq = 0; lq < D; ++lq) FISDF_TRY(enqueue_fft(lq));
   for (int lq = 0; lq < nq; ++lq) {
     const int ln = lq % NL;
     hipStream_t st = lane_st[ln];
-    cplx* Yh = pipe ? (cplx*)(b + oYall) + (long)lq * rmax * ngrid : (cplx*)(b + oY[ln]);
+    cplx* Yh = pipe ? slot_y(lq) : (cplx*)(b + oY[ln]);
     cplx* U = (cplx*)(b + oU[ln]);
-    double* wt = pipe ? (double*)(b + oWall) + (long)lq * ngrid : (double*)(b + oWt[ln]);
+    double* wt = pipe ? slot_w(lq) : (double*)(b + oWt[ln]);
     cplx* kw = (cplx*)(b + oK[ln]);
     cplx* Tc = (cplx*)(b + oTc[ln]);
     const int q = h_qs[lq];
     const int sl = s0 + lq;  // factor slot
     const int r = c->f_rank[sl];
-    if (r == 0) continue;
+    if (r == 0) {
+      if (pipe) FISDF_TRY(enqueue_fft(lq + D));
+      continue;
+    }
     const int* piv = c->f_piv + (long)sl * nip;
     const cplx* Lp = c->f_Lp + (long)sl * nn;
     const bool real_q = c->f_real[sl];
     const cplx* Linv = c->f_Linv + (long)sl * sLi;
     (void)piv;
-    if (pipe)
+    if (pipe) {
       FISDF_HIP(hipStreamWaitEvent(st, c->ev_q[lq], 0));
-    else
+    } else {
+      if (ready) FISDF_HIP(hipStreamWaitEvent(st, c->ev_ready[lq], 0));
       FISDF_TRY(fft_q(st, lq, Yh, wt));
+    }
     cplx* Uq = U;  // where L^{-1} Yh lands
     if (c->f_fac_unjoined) FISDF_HIP(hipStreamWaitEvent(st, c->ev_fac, 0));  // L^-1, Q, ...
     {
@@ -1251,7 +1426,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     {
       StageTimer tm(c, FISDF_ST_HERK, st);
       // G = U U^H  (:121 by Parseval)
-      FISDF_TRY(herk(st, r, (int)ngrid, 1.0, Uq, ngrid, G + lq * rr, rmax, ks, kw,
+      FISDF_TRY(herk(st, r, (int)ngrid, 1.0, Uq, ngrid, G + lq * rr, rmax, ks_of(r), kw,
                      real_q ? GEMM_RE_ONLY : GEMM_FULL));
     }
     if (real_q) {
@@ -1263,20 +1438,24 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
         if (as->n > 0) {
           FISDF_TRY(gather_cols(st, Uq, ngrid, r, as->idx, as->n, scratch));
           FISDF_TRY(herk(st, r, as->n, 1.0, scratch, as->n, Tc, rmax,
-                         std::min(ks, std::max(1, as->n / 256)), kw));
+                         std::min(ks_of(r), std::max(1, as->n / 256)), kw));
           FISDF_TRY(add_imag(st, G + lq * rr, rmax, Tc, rmax, r));
         }
       }
     }
+    if (pipe) {  // this lane is done with the ring slot: the FFT D q ahead may overwrite it
+      FISDF_HIP(hipEventRecord(c->ev_free[lq % D], st));
+      FISDF_TRY(enqueue_fft(lq + D));
+    }
   }
-  for (int l = 1; l < NL; ++l) {  // join the lanes before the batched small stage
-    FISDF_HIP(hipEventRecord(c->ev_join[l - 1], lane_st[l]));
-    FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_join[l - 1], 0));
+  // join the lanes (and the FFT stream: that keeps the arena reuse ordered) before the batched
+  // small stage on the main stream
+  for (int i = 0; i < 3; ++i) {
+    if (!aux_used[i]) continue;
+    FISDF_HIP(hipEventRecord(c->ev_join[i], c->aux[i]));
+    FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_join[i], 0));
   }
-  if (pipe) {  // (the lanes waited on every FFT already; this keeps the arena reuse ordered)
-    FISDF_HIP(hipEventRecord(c->ev_join[2], fst));
-    FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_join[2], 0));
-  }
+  c->ready_marked.assign(c->ready_marked.size(), 0);
   FISDF_TRY(join_factors(c));
   {
     StageTimer tm(c, FISDF_ST_SMALL);

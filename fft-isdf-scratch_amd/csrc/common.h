@@ -17,6 +17,7 @@ void set_error(const std::string& msg);
   do {                                                                               \
     hipError_t _e = (call);                                                          \
     if (_e != hipSuccess) {                                                          \
+      (void)hipGetLastError(); /* reported here: do not leave it for the next caller */ \
       ::fisdf::set_error(std::string("HIP error '") + hipGetErrorString(_e) +        \
                          "' at " __FILE__ ":" + std::to_string(__LINE__) + " in " #call); \
       return -2;                                                                     \

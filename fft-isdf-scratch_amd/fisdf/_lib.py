@@ -63,6 +63,10 @@ _SIGS = {
     "fisdf_factor_info": ([_vp, _ip], _i),
     "fisdf_set_fit_lanes": ([_vp, _i], _i),
     "fisdf_set_time_reversal": ([_vp, _i], _i),
+    "fisdf_set_fit_pipe": ([_vp, _i, _i], _i),
+    "fisdf_fit_info": ([_vp, _ip, _ip], _i),
+    "fisdf_mark_y_ready": ([_vp, _i], _i),
+    "fisdf_reserve_workspace": ([_vp, C.c_size_t], _i),
     "fisdf_fit_coulomb_qs": ([_vp, _ip, _i, _vp, _i, _ip, _ip, _dp, _vp], _i),
     "fisdf_build_ws_qs": ([_vp, _vp, _ip, _dp, _i, _i, _ip, _dp, _vp], _i),
     "fisdf_get_j": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp], _i),

@@ -119,6 +119,9 @@ class InterpolativeSeparableDensityFitting:
     pivoted_fit = None
     # Bloch AO inputs evaluated on the GPU (fisdf_eval_ao) instead of the host restatement
     ao_on_gpu = True
+    # multi-rank selection: False (default) replicates the 1-GPU Gram + pivots on every rank
+    # (rank-count-invariant pivots); True k-shards the Gram and all-reduces it
+    sharded_gram = False
 
     def __init__(self, cell, kpts, m0=None, c0=20.0, device=None, comm=None):
         self.cell = cell
@@ -211,8 +214,9 @@ class InterpolativeSeparableDensityFitting:
             d.ctx.call("fisdf_select_points", _lib.ptr(x0), nk, ng0, nao, nip_max,
                        float(self.select_tol), perm.ctypes.data_as(_lib._ip), byref(npiv),
                        byref(full))
-        else:
-            # k-sharded Gram (fftisdf.py:376-378) + all-reduce, then identical pivots everywhere
+        elif self.sharded_gram:
+            # k-sharded Gram (fftisdf.py:376-378) + all-reduce: the sum runs in another order
+            # than the 1-GPU Gram, so near-tied pivots may differ from the 1-GPU selection
             q0, q1 = d.shard(nk)
             x2 = d.empty((ng0, ng0))
             d.ctx.call("fisdf_select_gram", _lib.ptr(x0), nk, q0, q1, ng0, nao, _lib.ptr(x2))
@@ -221,6 +225,13 @@ class InterpolativeSeparableDensityFitting:
                        float(self.select_tol), perm.ctypes.data_as(_lib._ip), byref(npiv),
                        byref(full))
             del x2
+        else:
+            # replicated selection (default): every rank forms the whole Gram in the 1-GPU
+            # order (0.75 ms at C3) — the pivots are those of the 1-GPU build on every rank,
+            # with no collective
+            d.ctx.call("fisdf_select_points", _lib.ptr(x0), nk, ng0, nao, nip_max,
+                       float(self.select_tol), perm.ctypes.data_as(_lib._ip), byref(npiv),
+                       byref(full))
         nip = min(nip_max, npiv.value)                                  # fftisdf.py:383
         self.perm = perm[:nip].copy()
         X = d.empty((nk, nip, nao))
@@ -292,7 +303,12 @@ class InterpolativeSeparableDensityFitting:
             sub._dev_state = dict(X=st["X"])
             sub._omega_dfs = {}
             sub.timings = {}
-            build(sub)
+            try:
+                build(sub)
+            finally:
+                # the sub-object shares the device context: put its Coulomb kernel back to the
+                # parent's, so later direct fisdf_coulg / fit calls do not see erf(w) weights
+                self.device.ctx.call("fisdf_set_omega", float(getattr(self, "_fit_omega", 0.0)))
             cache[omega] = sub
         return cache[omega]
 
@@ -535,9 +551,12 @@ def build(df_obj):
                 work.wait()               # stream-ordered: no host block with RCCL
             d.ctx.call("fisdf_unpack_slices", _lib.ptr(recv), nip, d.size, g0s, ngs, ngrid,
                        _lib.ptr(yT[j]))
-            qj = my_qs[j:j + 1]
-            d.ctx.call("fisdf_fit_coulomb_qs", qj.ctypes.data_as(_lib._ip), 1, _lib.ptr(yT[j]),
-                       nip, mesh_p, km_p, a_p, _lib.ptr(Wq[j]))
+            d.ctx.call("fisdf_mark_y_ready", j)   # the fit of q j waits for this point only
+        # one call over the whole shard: its lanes and pipelined FFT stream start each q as
+        # soon as that q's piece has landed
+        if nq:
+            d.ctx.call("fisdf_fit_coulomb_qs", qs_c, nq, _lib.ptr(yT), nip, mesh_p, km_p, a_p,
+                       _lib.ptr(Wq))
         del send, pieces
     del yT
 

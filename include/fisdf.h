@@ -174,6 +174,23 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* ctx, const int* h_qs, int nq, const void* d_
  * MFMA-bound TRSM); 0 (default): FISDF_FIT_LANES from the environment, else 2.  Results do
  * not depend on it (same kernels, same per-q arithmetic). */
 int fisdf_set_fit_lanes(fisdf_ctx* ctx, int lanes);
+/* Pipelined FFT stream of the fit (with >= 2 lanes): mode -1 = FISDF_FIT_PIPE from the
+ * environment (default on), 0 off (the FFT runs in its lane), 1 on; the FFTs run ahead of the
+ * lanes into a ring of `depth` Yhat slots (0: FISDF_PIPE_DEPTH or lanes + 2), i.e.
+ * depth x rank x ngrid complex of workspace (C3: 448 MB per slot), whatever the number of q.
+ * Falls back to the in-lane FFT when the device lacks the memory.  Results do not depend on it. */
+int fisdf_set_fit_pipe(fisdf_ctx* ctx, int mode, int depth);
+/* What the last fisdf_fit_coulomb_qs ran with: MFMA lanes and ring depth (0 = not pipelined). */
+int fisdf_fit_info(fisdf_ctx* ctx, int* h_lanes, int* h_pipe_depth);
+/* Sharded build: record, on the context's stream, that y of the j-th q of the NEXT
+ * fisdf_fit_coulomb_qs call has landed in d_yT (after its all-to-all piece is unpacked).  When
+ * every q of that call is marked, the call runs its lanes on side streams and starts each q's
+ * FFT as soon as its own piece is there (one call for the whole shard keeps the lanes and the
+ * pipelined FFT stream; replaces one call per q).  Marks are consumed by the call. */
+int fisdf_mark_y_ready(fisdf_ctx* ctx, int j);
+/* Grow the context's scratch arena to at least `bytes` now (pre-allocation; a failed growth
+ * leaves an empty arena, never a stale one). */
+int fisdf_reserve_workspace(fisdf_ctx* ctx, size_t bytes);
 /* Coulomb kernel of the fit (and of fisdf_coulg): 0 = 1/r (default, fftisdf.py:114); omega > 0 the
  * long-range erf(omega r)/r, omega < 0 the short-range erfc(|omega| r)/r (PySCF get_coulG's
  * omega; the reference's get_jk raises for omega, fftisdf.py:392-393). */

@@ -11,6 +11,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path[:0] = [ROOT, os.path.join(ROOT, "fft-isdf-scratch_amd"), HERE]
 
+import ctypes as C  # noqa: E402
+
 import numpy as np  # noqa: E402
 
 
@@ -29,20 +31,13 @@ def main():
     df._kmesh()
     df._ao_parent = d.to_dev(x0)
     df._ao_grid = d.to_dev(chi)
+    if os.environ.get("FISDF_DIST_INJECT") == "1":
+        df.set_interpolation_points(o["perm"])   # the oracle's (dpstrf) pivots
     df.build()
     vj, vk = df.get_jk(dm)
     vj0, vk0 = o["vj"], o["vk"]
-    if not np.array_equal(df.perm, o["perm"]):
-        # the sharded Gram sums in another order than dpstrf's input: a near-tie may pick an
-        # equally valid different point set; the reference value is then the oracle's build
-        # on THAT point set (the selection itself is checked against dpstrf elsewhere)
-        from oracle import isdf_ref as R
-        xip = x0[:, df.perm]
-        ob = R.build(xip, chi, coords, cell.a, kmesh, cell.mesh)
-        kpts = R.get_kpts(cell.a, kmesh)
-        phase = R.get_phase(cell.a, kpts, kmesh)
-        vj0 = R.get_j_kpts(xip, ob["w0"], dm, kpts_band_is_zero=bool(abs(kpts).max() < 1e-9))
-        vk0 = R.get_k_kpts(xip, ob["wq"], dm, phase)
+    lanes, depth = C.c_int(), C.c_int()
+    d.ctx.call("fisdf_fit_info", C.byref(lanes), C.byref(depth))
     extra = {}
     if os.environ.get("FISDF_DIST_EXTRAS") == "1":
         # next-4 in the sharded path: exxdiv='ewald' (the correction is added after the vk
@@ -60,7 +55,8 @@ def main():
         extra = dict(vk_e=vk_e, vke0=vke0, vj_w=vj_w, vk_w=vk_w,
                      vjw0=R.get_j_kpts(xip, ob["w0"], dm), vkw0=R.get_k_kpts(xip, ob["wq"], dm, phase))
     np.savez(out, vj=vj, vk=vk, perm=df.perm, ranks=df.ranks, vj0=vj0, vk0=vk0,
-             perm0=o["perm"], **extra)
+             perm0=o["perm"], wq=df._wq, my_qs=df.my_qs, fit_lanes=lanes.value,
+             fit_pipe=depth.value, **extra)
     torch.cuda.synchronize()
     dist.destroy_process_group()
 

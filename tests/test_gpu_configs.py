@@ -70,8 +70,9 @@ def test_config_parity_full_size(cfg):
     # W_q of Gamma, one self-conjugate q (2 k_q in the reciprocal lattice) and two complex q.
     # W_q itself is as ill-conditioned as x4_q (measured rel |dW| 2.6e-3 at C5, 2.7e-6 at C3
     # between the two solvers) — the well-conditioned quantity J/K and the ERIs see is its
-    # AO-pair projection M_q = B^H W_q B, B[I, mn] = conj(X_0[I, m]) X_q[I, n]
-    # (the (m 0, n q | ...) ERI block of fftdf-with-k-lstsq.py:221-232)
+    # AO-pair projection M_q = B^T W_q conj(B), B[I, mn] = conj(X_0[I, m]) X_q[I, n]: the
+    # (m 0, n q | l q, k 0) ERI block of fftdf-with-k-lstsq.py:221-232 (pair momentum q on
+    # both sides, the only combination W_q is fitted for)
     wq = df._wq
     ks = np.stack(np.unravel_index(np.arange(nk), tuple(kmesh)), 1)
     selfc = [q for q in range(1, nk) if not ((2 * ks[q]) % kmesh).any()]
@@ -79,8 +80,8 @@ def test_config_parity_full_size(cfg):
     check = [0] + selfc[:1] + cplxq[:1] + cplxq[len(cplxq) // 2:len(cplxq) // 2 + 1]
     for q in check:
         B = (xip[0].conj()[:, :, None] * xip[q][:, None, :]).reshape(df.nip, -1)
-        m_gpu = B.conj().T @ (wq[q] @ B)
-        m_ref = B.conj().T @ (out["wq"][q] @ B)
+        m_gpu = B.T @ (wq[q] @ B.conj())
+        m_ref = B.T @ (out["wq"][q] @ B.conj())
         rel = abs(m_gpu - m_ref).max() / abs(m_ref).max()
         relw = abs(wq[q] - out["wq"][q]).max() / abs(out["wq"][q]).max()
         print(f"{cfg}: q {q} rel |dM_q| {rel:.2e} (raw rel |dW_q| {relw:.2e})", flush=True)

@@ -206,10 +206,12 @@ def test_gpu_selection(name):
     overlap = len(set(perm_gpu.tolist()) & set(o["perm"].tolist())) / o["nip"]
     first = int(np.argmax(perm_gpu != o["perm"])) if (perm_gpu != o["perm"]).any() else len(perm_gpu)
     print(f"{name}: pivot-set overlap with dpstrf {overlap:.3f}, identical prefix {first}/{o['nip']}")
-    # greedy order is tie-sensitive on a symmetric crystal: compare the resulting J/K
+    # the GPU picks dpstrf's pivots here (test_gpu_selection.py certifies the general case),
+    # so the J/K of the GPU-selected build meet the north_star bar against the oracle
+    assert np.array_equal(perm_gpu, o["perm"])
     vj, vk = df.get_jk(dm)
-    assert abs(vj - o["vj"]).max() < 1e-7
-    assert abs(vk - o["vk"]).max() < 1e-7
+    assert abs(vj - o["vj"]).max() < JK_TOL
+    assert abs(vk - o["vk"]).max() < JK_TOL
 
 
 def test_not_implemented_paths():
@@ -379,3 +381,54 @@ def test_range_separated_omega(omega):
     vj1, vk1 = df.get_jk(dm)
     assert abs(vj1 - vj0).max() == 0.0 and abs(vk1 - vk0).max() == 0.0
     assert len(df._omega_dfs) == 1
+
+
+@pytest.mark.parametrize("name,piv", [("toy333_fr", None), ("toy222", None), ("toy331", True)])
+def test_fit_schedule_invariance(name, piv):
+    """W_q does not depend on the fit schedule: 1/2/3 MFMA lanes, the FFT in-lane or
+    on the pipelined stream with ring depths 2..lanes+2 — same kernels, same per-q arithmetic,
+    bitwise equal W_q.  Covers self-conjugate q (toy222: all q), complex q (toy333_fr) and the
+    forced pivoted, rank-deficient factorisation (toy331)."""
+    import ctypes as C
+    base = None
+    for lanes, mode, depth in [(1, 0, 0), (2, 0, 0), (3, 0, 0), (2, 1, 0), (3, 1, 0), (2, 1, 2),
+                               (3, 1, 3)]:
+        df, o, dm = make_df(name, pivoted=piv)
+        d = df.device
+        d.ctx.call("fisdf_set_fit_lanes", lanes)
+        d.ctx.call("fisdf_set_fit_pipe", mode, depth)
+        df.build()
+        nl, nd = C.c_int(), C.c_int()
+        d.ctx.call("fisdf_fit_info", C.byref(nl), C.byref(nd))
+        nq = len(df.my_qs)
+        assert nl.value == min(lanes, nq)
+        assert nd.value == (0 if mode == 0 or nq < 2 or lanes < 2 else
+                            min(nq, depth if depth else min(lanes, nq, 3) + 2))
+        wq = df._wq
+        if base is None:
+            base = wq
+        print(f"{name} lanes {lanes} pipe {mode} ring {nd.value}: max|W - W(1 lane)| "
+              f"{abs(wq - base).max():.1e}")
+        assert abs(wq - base).max() == 0.0
+
+
+def test_arena_failed_growth_is_recoverable():
+    """a failed arena growth leaves an empty arena (not a stale size over a null
+    base); the next small request allocates a real buffer and the kernels using it are right."""
+    import torch
+    from fisdf._lib import FisdfError
+    df, o, dm = make_df("toy222")
+    d = df.device
+    with pytest.raises(FisdfError):
+        d.ctx.call("fisdf_reserve_workspace", 1 << 52)      # 4 PB
+    from fisdf import _lib as L
+    g = torch.Generator().manual_seed(5)
+    A = torch.randn(96, 700, dtype=torch.complex128, generator=g)
+    B = torch.randn(700, 80, dtype=torch.complex128, generator=g)
+    dA, dB = A.to(d.dev), B.to(d.dev)
+    dC = torch.zeros(96, 80, dtype=torch.complex128, device=d.dev)
+    one, zero = np.array([1.0, 0.0]), np.zeros(2)
+    d.ctx.call("fisdf_zgemm", 0, 0, 96, 80, 700, one.ctypes.data_as(L._dp), L.ptr(dA), 700, 0,
+               L.ptr(dB), 80, 0, zero.ctypes.data_as(L._dp), L.ptr(dC), 80, 0, 1, 4)  # split-K: arena
+    ref = A @ B
+    assert (dC.cpu() - ref).abs().max() < 1e-12 * ref.abs().max()
