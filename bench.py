@@ -269,7 +269,7 @@ def main():
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "f64 (complex128)", "data": "synthetic (gth-dzvp-shaped contracted Gaussians)",
             "config": {"workload": DESC[args.config], "nk": nk, "nao": cell.nao_nr(),
-                       "nip": int(df.nip), "ngrid": ngrid, "fit": "pivoted-Cholesky factored",
+                       "nip": int(df.nip), "ngrid": ngrid, "fit": "lstsq (Cholesky, factored order; min-norm on rank-deficient q)",
                        "parallelism": f"k-shard x{world}"},
             "roofline": roof,
             "roofline_secondary": roof2,

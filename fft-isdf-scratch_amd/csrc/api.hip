@@ -50,6 +50,13 @@ struct fisdf_ctx {
   bool f_check_fail = false, f_used_pivoted = false;
   int f_cap_nk = 0, f_cap_nip = 0;  // shape the factor buffers were allocated for
   int force_pivoted = -1;  // fisdf_set_pivoted_fit; -1: environment FISDF_PIVOTED_FIT
+  // fisdf_set_fit_mode: FISDF_FIT_LSTSQ (gelsy semantics: the unique solution of a full-rank
+  // x4_q, the minimum-norm one of a rank-deficient x4_q), FISDF_FIT_SVD (rank-revealing factor
+  // and the minimum-norm operator on every q), FISDF_FIT_BASIC (basic solution, round-1 path)
+  int fit_mode = 0;
+  cplx* f_M = nullptr;          // (nk, nip, nip) minimum-norm operators A^+ (rows < rank)
+  std::vector<char> f_cod;      // slot fitted through its minimum-norm operator
+  int* f_nip_dev = nullptr;     // device copy of nip (scatter of a full W_PP)
   int lanes = 0;           // fisdf_set_fit_lanes; 0: environment FISDF_FIT_LANES / default
   bool time_reversal = false;  // fisdf_set_time_reversal: fx_{-k} = conj(fx_k) in build_y
   double omega = 0.0;          // fisdf_set_omega: range-separated Coulomb kernel of the fit
@@ -240,6 +247,11 @@ int free_factors(fisdf_ctx* c) {
   c->f_Li = nullptr;
   if (c->f_x4s) FISDF_HIP(hipFree(c->f_x4s));
   c->f_x4s = nullptr;
+  if (c->f_M) FISDF_HIP(hipFree(c->f_M));
+  c->f_M = nullptr;
+  if (c->f_nip_dev) FISDF_HIP(hipFree(c->f_nip_dev));
+  c->f_nip_dev = nullptr;
+  c->f_cod.clear();
   if (c->f_fail_pinned) FISDF_HIP(hipHostFree(c->f_fail_pinned));
   c->f_fail_pinned = nullptr;
   if (c->f_piv) FISDF_HIP(hipFree(c->f_piv));
@@ -573,6 +585,40 @@ int fisdf_coulg(fisdf_ctx* c, const int mesh[3], const double a[9], const double
   CellGeom g;
   lattice(a, g);
   return coulg_weight(c->stream, mesh, g, k, scale, take_sqrt, w, c->omega);
+}
+
+int fisdf_min_norm_operator(fisdf_ctx* c, const void* A, int n, double tol_rel, void* M,
+                            void* Qo, void* Rio, int* h_piv, int* h_rank) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(n >= 1, "min_norm_operator: bad size");
+  Carver cv;
+  size_t oL = cv.take(sizeof(cplx) * (size_t)n * n);
+  size_t oP = cv.take(sizeof(int) * (size_t)n);
+  size_t oR = cv.take(sizeof(int));
+  size_t oD = cv.take(sizeof(double) * (size_t)n);
+  size_t oF = cv.take(sizeof(int) * 4);
+  size_t oW = cv.take(sizeof(double) * (size_t)(1 + n));
+  size_t oM = cv.take(min_norm_work_bytes(n, n));
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  char* b = (char*)base;
+  FISDF_TRY(pchol(c->stream, (const cplx*)A, n, (long)n * n, n, 1, n, tol_rel, 0.0, (cplx*)(b + oL),
+                  (int*)(b + oP), (int*)(b + oR), (double*)(b + oD), (int*)(b + oF),
+                  (double*)(b + oW)));
+  int r = 0;
+  FISDF_HIP(hipMemcpyAsync(&r, b + oR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  FISDF_CHECK(r >= 1, "min_norm_operator: zero matrix");
+  FISDF_HIP(hipMemsetAsync(M, 0, sizeof(cplx) * (size_t)n * n, c->stream));
+  FISDF_TRY(min_norm_operator(c->stream, (const cplx*)(b + oL), n, n, (int*)(b + oP), r, (cplx*)M, n,
+                              b + oM, (int*)(b + oF), (cplx*)Qo, (cplx*)Rio));
+  int fl[3] = {0, 0, 0};
+  FISDF_HIP(hipMemcpyAsync(fl, b + oF, sizeof(fl), hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipMemcpyAsync(h_piv, b + oP, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  FISDF_CHECK(fl[0] == 0 && fl[1] == 0 && fl[2] == 0, "min_norm_operator: CholeskyQR breakdown");
+  *h_rank = r;
+  return 0;
 }
 
 int fisdf_pivoted_cholesky(fisdf_ctx* c, const void* A, int n, int batch, int rmax,
@@ -1052,7 +1098,8 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
                              sizeof(cplx) * nn, hipMemcpyDeviceToDevice, s));
     if (c->f_real[i]) FISDF_TRY(zero_imag(s, c->f_x4s + i * nn, nn));
   }
-  if (c->force_pivoted == 1 || (c->force_pivoted < 0 && pivoted_fit_forced())) {
+  if (c->force_pivoted == 1 || (c->force_pivoted < 0 && pivoted_fit_forced()) ||
+      c->fit_mode == FISDF_FIT_SVD) {
     FISDF_TRY(factor_pivoted(c, s));
     c->f_check_fail = false;
   } else {
@@ -1074,6 +1121,21 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
 int fisdf_set_pivoted_fit(fisdf_ctx* c, int mode) {
   FISDF_CHECK(c != nullptr && mode >= -1 && mode <= 1, "set_pivoted_fit: bad mode");
   c->force_pivoted = mode;
+  return 0;
+}
+
+int fisdf_set_fit_mode(fisdf_ctx* c, int mode) {
+  FISDF_CHECK(c != nullptr && mode >= FISDF_FIT_LSTSQ && mode <= FISDF_FIT_BASIC,
+              "set_fit_mode: mode must be FISDF_FIT_LSTSQ, FISDF_FIT_SVD or FISDF_FIT_BASIC");
+  c->fit_mode = mode;
+  return 0;
+}
+
+int fisdf_min_norm_info(fisdf_ctx* c, int* h_nslots) {
+  FISDF_CHECK(c != nullptr, "null context");
+  int n = 0;
+  for (char v : c->f_cod) n += v ? 1 : 0;
+  if (h_nslots) *h_nslots = n;
   return 0;
 }
 
@@ -1136,6 +1198,48 @@ int fisdf_factor_info(fisdf_ctx* c, int* h_used_pivoted) {
   return 0;
 }
 
+// Minimum-norm operators (fisdf_set_fit_mode) of the slots that need one, on the side stream
+// once the ranks are known: a rank-deficient x4_q (FISDF_FIT_LSTSQ) or every q (FISDF_FIT_SVD).
+// gelsy (fftisdf.py:108) returns the minimum-norm least-squares solution; the basic solution
+// of the rank-revealing factor differs from it in the null space (tests/experiments/
+// min_norm_fit.py).  Synchronous: the Cholesky breakdown flags of each CholeskyQR pass are read.
+static int build_min_norm(fisdf_ctx* c, bool* built) {
+  *built = false;
+  const int nk = c->f_nk, nip = c->f_nip;
+  const long nn = (long)nip * nip;
+  c->f_cod.assign(nk, 0);
+  int ncod = 0;
+  for (int q = 0; q < nk; ++q) {
+    const int r = c->f_rank[q];
+    const bool cod = r > 0 && (c->fit_mode == FISDF_FIT_SVD || (c->fit_mode == FISDF_FIT_LSTSQ && r < nip));
+    c->f_cod[q] = cod ? 1 : 0;
+    ncod += cod ? 1 : 0;
+  }
+  if (ncod == 0) return 0;
+  if (!c->f_M) FISDF_HIP(hipMalloc(&c->f_M, sizeof(cplx) * (size_t)c->f_cap_nk * nn));
+  if (!c->f_nip_dev) FISDF_HIP(hipMalloc(&c->f_nip_dev, sizeof(int)));
+  FISDF_HIP(hipMemcpy(c->f_nip_dev, &nip, sizeof(int), hipMemcpyHostToDevice));
+  hipStream_t s = c->side;
+  const size_t wb = (min_norm_work_bytes(nip, nip) + 255) / 256 * 256;
+  char* work = nullptr;
+  FISDF_HIP(hipMallocAsync((void**)&work, wb + sizeof(int) * 3 * (size_t)nk, s));
+  int* fail = (int*)(work + wb);
+  for (int q = 0; q < nk; ++q)
+    if (c->f_cod[q])
+      FISDF_TRY(min_norm_operator(s, c->f_L + q * nn, nip, nip, c->f_piv + (long)q * nip,
+                                  c->f_rank[q], c->f_M + q * nn, nip, work, fail + 3 * q));
+  std::vector<int> hf(3 * (size_t)nk, 0);
+  FISDF_HIP(hipMemcpyAsync(hf.data(), fail, sizeof(int) * 3 * nk, hipMemcpyDeviceToHost, s));
+  FISDF_HIP(hipFreeAsync(work, s));
+  FISDF_HIP(hipEventRecord(c->ev_fac, s));
+  FISDF_HIP(hipEventSynchronize(c->ev_fac));
+  for (int q = 0; q < nk; ++q)
+    FISDF_CHECK(!c->f_cod[q] || (hf[3 * q] == 0 && hf[3 * q + 1] == 0 && hf[3 * q + 2] == 0),
+                "min-norm fit: CholeskyQR breakdown of the rank-revealing factor");
+  *built = true;
+  return 0;
+}
+
 int fisdf_factor_x4_wait(fisdf_ctx* c, int* h_ranks) {
   FISDF_TRY(device_guard(c));
   if (c->f_pending) {
@@ -1159,6 +1263,9 @@ int fisdf_factor_x4_wait(fisdf_ctx* c, int* h_ranks) {
     if (redone) FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_fac, 0));
     c->f_fac_unjoined = !redone;
     c->f_pending = false;
+    bool built = false;
+    FISDF_TRY(build_min_norm(c, &built));
+    if (built) c->f_fac_unjoined = true;  // ev_fac re-recorded after the operators
   }
   if (h_ranks)
     for (int q = 0; q < c->f_nk; ++q) h_ranks[q] = c->f_rank[q];
@@ -1214,6 +1321,14 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   cplx* Wq = (cplx*)Wqv;
   int rmax = 0;
   for (int lq = 0; lq < nq; ++lq) rmax = std::max(rmax, c->f_rank[s0 + lq]);
+  // minimum-norm slots transform all nip rows of y (the operator A^+ mixes every row)
+  auto cod_of = [&](int sl) { return sl < (int)c->f_cod.size() && c->f_cod[sl] != 0; };
+  int rfmax = rmax, ncod = 0;
+  for (int lq = 0; lq < nq; ++lq)
+    if (cod_of(s0 + lq)) {
+      rfmax = nip;
+      ++ncod;
+    }
   static const int ks_env = [] {
     const char* e = getenv("FISDF_HERK_KS");
     return e ? atoi(e) : 0;
@@ -1256,14 +1371,14 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   auto carve = [&]() {
     cv = Carver();
     for (int l = 0; l < NL; ++l) {
-      if (!pipe) oY[l] = cv.take(sizeof(cplx) * rmax * ngrid);
+      if (!pipe) oY[l] = cv.take(sizeof(cplx) * rfmax * ngrid);
       oU[l] = cv.take(sizeof(cplx) * rmax * ngrid);
       if (!pipe) oWt[l] = cv.take(sizeof(double) * ngrid);
       oK[l] = cv.take(sizeof(cplx) * (size_t)ks * rmax * rmax);
       oTc[l] = cv.take(sizeof(cplx) * rr);
     }
     if (pipe) {
-      oYall = cv.take(sizeof(cplx) * (size_t)D * rmax * ngrid);
+      oYall = cv.take(sizeof(cplx) * (size_t)D * rfmax * ngrid);
       oWall = cv.take(sizeof(double) * (size_t)D * ngrid);
     }
   };
@@ -1272,7 +1387,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     // the ring's extra slots only if the device has room for them; else the in-lane FFT
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
-    const size_t extra = (size_t)D * rmax * ngrid * sizeof(cplx);
+    const size_t extra = (size_t)D * rfmax * ngrid * sizeof(cplx);
     if (free_b + c->arena_size < cv.off + extra / 8) {
       pipe = false;
       D = 0;
@@ -1296,6 +1411,8 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   size_t oG = cv.take(sizeof(cplx) * nq * rr);
   size_t oT = cv.take(sizeof(cplx) * nq * rr);
   size_t oS = cv.take(sizeof(cplx) * nq * rr);
+  size_t oMS = ncod ? cv.take(sizeof(cplx) * (size_t)ncod * rmax * nip) : 0;  // G M per min-norm slot
+  size_t oMT = ncod ? cv.take(sizeof(cplx) * nn) : 0;                  // M^H G M
   void* base;
   FISDF_TRY(arena_get(c, cv.off, &base));
   char* b = (char*)base;
@@ -1348,7 +1465,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   // Yhat_q = FFT(y_q[:, piv] * f_q) * w_q   (:99, :113-115, :118; rows in pivot order)
   auto fft_q = [&](hipStream_t st, int lq, cplx* Yh, double* wt) -> int {
     const int sl = s0 + lq;
-    const int r = c->f_rank[sl];
+    const int r = cod_of(sl) ? nip : c->f_rank[sl];
     double kq[3], kd[3];
     kpoint(kmesh, g, h_qs[lq], kq);
     for (int i = 0; i < 3; ++i) kd[i] = g.a[i][0] * kq[0] + g.a[i][1] * kq[1] + g.a[i][2] * kq[2];
@@ -1360,7 +1477,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     return 0;
   };
   // ring slot of q lq (pipelined mode)
-  auto slot_y = [&](int lq) { return (cplx*)(b + oYall) + (long)(lq % D) * rmax * ngrid; };
+  auto slot_y = [&](int lq) { return (cplx*)(b + oYall) + (long)(lq % D) * rfmax * ngrid; };
   auto slot_w = [&](int lq) { return (double*)(b + oWall) + (long)(lq % D) * ngrid; };
   // FFT of q lq into its ring slot, after the lane that read the slot's previous q is done
   auto enqueue_fft = [&](int lq) -> int {
@@ -1408,7 +1525,12 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
         const char* e = getenv("FISDF_TRSM");
         return !(e && std::string(e) == "merged");
       }();
-      if (r == nip && tri_gemm) {  // one lower-triangular GEMM with L^{-1}
+      if (cod_of(sl)) {  // U = A^+ Yh[P]: the minimum-norm operator over all nip rows
+        FISDF_TRY(zgemm(st, OP_N, OP_N, r, (int)ngrid, nip, ONE, c->f_M + (long)sl * nn, nip, 0, Yh,
+                        ngrid, 0, ZERO, U, ngrid, 0, 1, 1, nullptr, EPI_NONE, nullptr,
+                        real_q ? GEMM_A_REAL : GEMM_FULL));
+        Uq = U;
+      } else if (r == nip && tri_gemm) {  // one lower-triangular GEMM with L^{-1}
         FISDF_TRY(zgemm(st, OP_N, OP_N, nip, (int)ngrid, nip, ONE, c->f_Li + (long)sl * nn, nip, 0,
                         Yh, ngrid, 0, ZERO, U, ngrid, 0, 1, 1, nullptr, EPI_NONE, nullptr,
                         GEMM_A_LOWER | (real_q ? GEMM_A_REAL : GEMM_FULL)));
@@ -1463,6 +1585,14 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     // zeros beyond each rank):  T = L^{-H} G ; S = L^{-H} T^H ; W_PP = S^H ; scatter by pivots
     const cplx* Lp0 = c->f_Lp + (long)s0 * nn;
     const cplx* Li0 = c->f_Linv + (long)s0 * sLi;
+    // minimum-norm slots: G M first (the batched back-substitutions below overwrite G)
+    for (int lq = 0, j = 0; lq < nq && ncod; ++lq) {
+      const int sl = s0 + lq, r = c->f_rank[sl];
+      if (!cod_of(sl)) continue;
+      FISDF_TRY(zgemm(c->stream, OP_N, OP_N, r, nip, r, ONE, G + lq * rr, rmax, 0,
+                      c->f_M + (long)sl * nn, nip, 0, ZERO, (cplx*)(b + oMS) + (long)j++ * rmax * nip,
+                      nip, 0, 1));
+    }
     bool all_full = rmax == nip;
     for (int lq = 0; lq < nq && all_full; ++lq) all_full = c->f_rank[s0 + lq] == nip;
     if (all_full) {  // with L^{-1} at hand: T = G L^{-1}, W_PP = L^{-H} T (two batched GEMMs)
@@ -1481,6 +1611,18 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     }
     FISDF_TRY(scatter_w(c->stream, T, rmax, rr, rmax, c->f_piv + (long)s0 * nip,
                         c->f_rank_dev + s0, Wq, nip, nq));
+    // minimum-norm slots: W_PP = M^H (G M) (nip x nip: z[P] = M^H U) replaces the above
+    for (int lq = 0, j = 0; lq < nq && ncod; ++lq) {
+      const int sl = s0 + lq, r = c->f_rank[sl];
+      if (!cod_of(sl)) continue;
+      const cplx* MS = (cplx*)(b + oMS) + (long)j++ * rmax * nip;
+      cplx* MT = (cplx*)(b + oMT);
+      const cplx* Mq = c->f_M + (long)sl * nn;
+      FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nip, nip, r, ONE, Mq, nip, 0, MS, nip, 0, ZERO, MT,
+                      nip, 0, 1));
+      FISDF_TRY(scatter_w(c->stream, MT, nip, 0, nip, c->f_piv + (long)sl * nip, c->f_nip_dev,
+                          Wq + lq * nn, nip, 1));
+    }
   }
   return 0;
 }

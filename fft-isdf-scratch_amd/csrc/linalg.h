@@ -27,6 +27,16 @@ int gather_cols(hipStream_t s, const cplx* A, long ld, int r, const int* idx, in
 int add_imag(hipStream_t s, cplx* G, int ldg, const cplx* H, int ldh, int n);
 // zero the imaginary parts of n complex elements
 int zero_imag(hipStream_t s, cplx* a, long n);
+// Minimum-norm operator of a rank-deficient x4_q from its rank-revealing pivoted Cholesky
+// x4[P,P] ~ L L^H (L: rows of f_L, row order; piv: the pivot order; r = rank): A = P L (n x r),
+// thin QR A = Q R by shifted CholeskyQR3, M = A^+ = R^{-1} Q^H (r x n, ld ldm; columns in pivot
+// order) so that z[P] = M^H M y[P] is the minimum-norm solution (gelsy's complete orthogonal
+// step).  Completes piv[r..n) with the rows outside the first r pivots (ascending).
+// q_out (n x r) / rinv_out (r x r), if given, receive Q and R^{-1}.  work: min_norm_work_bytes(n, r); fail: 3 device ints (Cholesky breakdown per pass).
+int min_norm_operator(hipStream_t s, const cplx* L, int n, int rmax, int* piv, int r,
+                      cplx* M, long ldm, void* work, int* fail, cplx* q_out = nullptr,
+                      cplx* rinv_out = nullptr);
+size_t min_norm_work_bytes(int n, int r);
 int scatter_w(hipStream_t s, const cplx* Wpp, int ldw, long sW, int rmax, const int* piv,
               const int* rank, cplx* W, int nip, int batch);
 int conj_transpose(hipStream_t s, const cplx* A, int n, long sA, cplx* B, int batch);

@@ -756,6 +756,114 @@ int zero_imag(hipStream_t s, cplx* a, long n) {
   return 0;
 }
 
+// ---- minimum-norm (complete orthogonal) operator of a rank-deficient x4_q ----------------
+namespace {
+
+// A[s][t] = L[piv[s]][t] for every row s < n (the rejected pivots' rows included), t < r
+__global__ void gather_trapezoid_kernel(const cplx* __restrict__ L, int n, int rmax,
+                                        const int* __restrict__ piv, int r, cplx* __restrict__ A) {
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= (long)n * r) return;
+  const int s = (int)(e / r), t = (int)(e % r);
+  A[e] = (t <= s) ? L[(long)piv[s] * rmax + t] : cmk(0, 0);
+}
+
+// S += shift I with shift = 11 (n r + r (r + 1)) eps tr(S): the first pass of shifted
+// CholeskyQR3 (tr(A^H A) = |A|_F^2 >= |A|_2^2), so the Cholesky of a Gram with cond ~ 1/eps
+// cannot break down; the two unshifted passes after it restore orthogonality
+__global__ __launch_bounds__(256) void shift_gram_kernel(cplx* __restrict__ S, int r, int n) {
+  __shared__ double part[256];
+  double t = 0.0;
+  for (int i = threadIdx.x; i < r; i += 256) t += S[(long)i * r + i].x;
+  part[threadIdx.x] = t;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  const double shift = 11.0 * ((double)n * r + (double)r * (r + 1)) * 2.220446049250313e-16 * part[0];
+  for (int i = threadIdx.x; i < r; i += 256) S[(long)i * r + i].x += shift;
+}
+
+// piv[r..n) = the rows not among the first r pivots, ascending (the pivoted Cholesky stops at
+// its rank and leaves them unset): the minimum-norm operator uses every row of x4_q
+__global__ __launch_bounds__(1024) void complete_perm_kernel(int* __restrict__ piv, int n, int r) {
+  extern __shared__ int used[];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) used[i] = 0;
+  __syncthreads();
+  for (int s = threadIdx.x; s < r; s += blockDim.x) used[piv[s]] = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int k = r;
+    for (int i = 0; i < n; ++i)
+      if (!used[i]) piv[k++] = i;
+  }
+}
+
+// H = X^H (r x r, ld r)
+__global__ void adjoint_kernel(const cplx* __restrict__ X, int r, cplx* __restrict__ H) {
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= (long)r * r) return;
+  const int i = (int)(e / r), j = (int)(e % r);
+  H[(long)j * r + i] = cconj(X[e]);
+}
+
+}  // namespace
+
+int min_norm_operator(hipStream_t s, const cplx* L, int n, int rmax, int* piv, int r,
+                      cplx* M, long ldm, void* work, int* fail, cplx* q_out, cplx* rinv_out) {
+  FISDF_CHECK(r >= 1 && r <= n && n <= rmax, "min_norm_operator: bad sizes");
+  const long rr = (long)r * r, nr = (long)n * r;
+  cplx* A = (cplx*)work;            // n x r: A = P L, then Q
+  cplx* A2 = A + nr;                // n x r
+  cplx* S = A2 + nr;                // r x r Gram / its Cholesky factor
+  cplx* Qop = S + rr;               // r x r block-row operator of the triangular inverse
+  cplx* Li = Qop + rr;              // r x r inverse of the pass's factor
+  cplx* Ri = Li + rr;               // r x r accumulated R^{-1}
+  cplx* Rt = Ri + rr;               // r x r
+  cplx* cw = Rt + rr;               // chol_unpivoted work: 4096 cplx + 1 double
+  int* iw = (int*)(cw + 4096 + 1);  // piv (r), rank
+  const cplx one = cmk(1, 0), zero = cmk(0, 0);
+  if (r < n) {
+    hipLaunchKernelGGL(complete_perm_kernel, dim3(1), dim3(1024), sizeof(int) * n, s,
+                       piv, n, r);
+    FISDF_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(gather_trapezoid_kernel, dim3(nblocks(nr, 256, 1L << 30)), dim3(256), 0, s, L,
+                     n, rmax, piv, r, A);
+  FISDF_HIP(hipGetLastError());
+  for (int pass = 0; pass < 3; ++pass) {
+    // S = A^H A = Lc Lc^H;  A <- A Lc^{-H};  R^{-1} <- R^{-1} Lc^{-H}
+    FISDF_TRY(zgemm(s, OP_C, OP_N, r, r, n, one, A, r, 0, A, r, 0, zero, S, r, 0, 1));
+    if (pass == 0) {
+      hipLaunchKernelGGL(shift_gram_kernel, dim3(1), dim3(256), 0, s, S, r, n);
+      FISDF_HIP(hipGetLastError());
+    }
+    FISDF_TRY(chol_unpivoted(s, S, r, 1, 0.0, iw, iw + r, fail + pass, cw));
+    FISDF_TRY(build_trsm_q(s, S, r, rr, Qop, 1, GEMM_FULL));
+    FISDF_TRY(set_identity(s, Li, r, 1));
+    FISDF_TRY(trsm_merged_batched(s, Qop, rr, r, Li, r, rr, r, 1));
+    FISDF_TRY(zgemm(s, OP_N, OP_C, n, r, r, one, A, r, 0, Li, r, 0, zero, A2, r, 0, 1));
+    std::swap(A, A2);
+    if (pass == 0) {
+      hipLaunchKernelGGL(adjoint_kernel, dim3(nblocks(rr, 256, 1L << 30)), dim3(256), 0, s, Li, r, Ri);
+      FISDF_HIP(hipGetLastError());
+    } else {
+      FISDF_TRY(zgemm(s, OP_N, OP_C, r, r, r, one, Ri, r, 0, Li, r, 0, zero, Rt, r, 0, 1));
+      std::swap(Ri, Rt);
+    }
+  }
+  // A^+ = R^{-1} Q^H  (r x n)
+  FISDF_TRY(zgemm(s, OP_N, OP_C, r, n, r, one, Ri, r, 0, A, r, 0, zero, M, ldm, 0, 1));
+  if (q_out) FISDF_HIP(hipMemcpyAsync(q_out, A, sizeof(cplx) * nr, hipMemcpyDeviceToDevice, s));
+  if (rinv_out) FISDF_HIP(hipMemcpyAsync(rinv_out, Ri, sizeof(cplx) * rr, hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+size_t min_norm_work_bytes(int n, int r) {
+  return sizeof(cplx) * (2 * (size_t)n * r + 5 * (size_t)r * r + 4097) + sizeof(int) * ((size_t)r + 1);
+}
+
 int scatter_w(hipStream_t s, const cplx* Wpp, int ldw, long sW, int rmax, const int* piv,
               const int* rank, cplx* W, int nip, int batch) {
   FISDF_HIP(hipMemsetAsync(W, 0, sizeof(cplx) * (size_t)nip * nip * batch, s));

@@ -295,6 +295,9 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx al
 #ifndef FISDF_NST
 #define FISDF_NST 3
 #endif
+#ifndef FISDF_PREREAD
+#define FISDF_PREREAD 0
+#endif
 constexpr int NST = FISDF_NST;  // LDS ring depth; loads run NST-1 K-steps ahead
 constexpr int LPW = TILE / (64 * 4);  // glds wave-instructions per operand per step per wave
 __device__ cplx g_zero_page[64];      // zero-initialised device global
@@ -443,21 +446,41 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
       // the barrier also retires all reads of the slot step s+2 is about to overwrite
       asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * LPW * (NS - 2)) : "memory");
       __builtin_amdgcn_sched_barrier(0);
-      issue(s + NS - 1);
       const int cur = s % NS;
       const cplx* as = sm + (long)(cur * 2 + 0) * TILE;
       const cplx* bs = sm + (long)(cur * 2 + 1) * TILE;
       const int kleft = kend - kbeg - s * BK;  // K-substeps past the end hold only zeros
+#if FISDF_PREREAD
+      // every K-substep's fragments are read from the ring slot before the next step's loads
+      // are issued, so their LDS latency overlaps the glds issue and the first MFMAs
+      cplx fa[BK / 4][2], fb[BK / 4][2];
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 4)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          fa[kk / 4][u] = as[SA::slot((wm + u * 16 + i16) & 63, kk + kq)];
+          fb[kk / 4][u] = bs[SB::slot((wn + u * 16 + i16) & 63, kk + kq)];
+        }
+#endif
+      issue(s + NS - 1);
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 4) {
         if (kk > 0 && kk >= kleft) break;
-        const int k = kk + kq;
         cplx a[2], b[2];
+#if FISDF_PREREAD
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          a[u] = fa[kk / 4][u];
+          b[u] = fb[kk / 4][u];
+        }
+#else
+        const int k = kk + kq;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {  // & 63: a masked block past the tile reads in-tile rows
           a[u] = as[SA::slot((wm + u * 16 + i16) & 63, k)];
           b[u] = bs[SB::slot((wn + u * 16 + i16) & 63, k)];
         }
+#endif
         // op(A) = a (or conj a), op(B) = b (or conj b):
         //   Re += ar br - ai' bi' ;  Im += ar bi' + ai' br   (ai' = +-ai, bi' = +-bi)
         double ar[2], ai[2], nai[2], br[2], bi[2];

@@ -117,6 +117,11 @@ class InterpolativeSeparableDensityFitting:
     # x4_q factorisation: None = library default (unpivoted blocked Cholesky when every x4_q
     # is numerically full rank, else the greedy pivoted one); True forces the pivoted path
     pivoted_fit = None
+    # the solution the fit applies (fisdf_set_fit_mode): "lstsq" = scipy lstsq/gelsy semantics
+    # (fftisdf.py:108; unique solution of a full-rank x4_q, minimum-norm one of a rank-deficient
+    # x4_q), "svd" = the truncated pseudo-solve on every q (fftdf-with-k-svd.py:158-164 intent),
+    # "basic" = the rank-revealing factor's basic solution (round-1 path)
+    fit = "lstsq"
     # Bloch AO inputs evaluated on the GPU (fisdf_eval_ao) instead of the host restatement
     ao_on_gpu = True
     # multi-rank selection: False (default) replicates the 1-GPU Gram + pivots on every rank
@@ -493,6 +498,10 @@ def build(df_obj):
     # overlapped with the y build enqueued next on the main stream
     d.ctx.call("fisdf_set_pivoted_fit", -1 if df_obj.pivoted_fit is None
                else (1 if df_obj.pivoted_fit else 0))
+    modes = {"lstsq": 0, "svd": 1, "basic": 2}
+    if df_obj.fit not in modes:
+        raise ValueError(f"ISDF.fit must be one of {sorted(modes)}, not {df_obj.fit!r}")
+    d.ctx.call("fisdf_set_fit_mode", modes[df_obj.fit])
     # the side stream starts from here (x4 built); the factor chain itself is enqueued after
     # the y build, since it reads ranks back to the host part-way (a blocking copy)
     if nq:
@@ -538,6 +547,8 @@ def build(df_obj):
         used = C_int()
         d.ctx.call("fisdf_factor_info", byref(used))
         df_obj.used_pivoted_fit = bool(used.value)
+        d.ctx.call("fisdf_min_norm_info", byref(used))
+        df_obj.min_norm_slots = int(used.value)
     Wq = d.empty((nq, nip, nip))
     if d.size == 1:
         if nq:

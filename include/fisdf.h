@@ -156,6 +156,22 @@ int fisdf_factor_x4_mark(fisdf_ctx* ctx);
  * fisdf_factor_info: 1 if the last factorisation used the pivoted path. */
 int fisdf_set_pivoted_fit(fisdf_ctx* ctx, int mode);
 int fisdf_factor_info(fisdf_ctx* ctx, int* h_used_pivoted);
+/* Solution the fit applies (replaces scipy lstsq/gelsy, fftisdf.py:108, and the SVD
+ * pseudo-solve of fftdf-with-k-svd.py:158-164):
+ *  FISDF_FIT_LSTSQ (default): gelsy's semantics — the unique solution of a full-rank x4_q
+ *    (blocked Cholesky, TRSM-first factored order) and, when the rank-revealing factor finds
+ *    rank r < nip, the MINIMUM-NORM solution z = x4_r^+ y: A = P L (nip x r), thin QR A = Q R
+ *    (shifted CholeskyQR3 on the device), z[P] = M^H M y[P] with M = A^+ = R^{-1} Q^H — the
+ *    complete orthogonal step gelsy takes after its QRCP;
+ *  FISDF_FIT_SVD: the truncated pseudo-solve on every q (rank-revealing factor with the
+ *    relative cut tol_rel, then the same minimum-norm operator), the "SVD fit" configuration;
+ *  FISDF_FIT_BASIC: the basic solution z[P1] = L11^-H L11^-1 y[P1] (round-1 behaviour).
+ * fisdf_min_norm_info: number of q of the last factorisation fitted through M. */
+#define FISDF_FIT_LSTSQ 0
+#define FISDF_FIT_SVD 1
+#define FISDF_FIT_BASIC 2
+int fisdf_set_fit_mode(fisdf_ctx* ctx, int mode);
+int fisdf_min_norm_info(fisdf_ctx* ctx, int* h_nslots);
 
 /* ---- A4+A5: fit + FFT Coulomb for the factored shard q in [q0, q1) (fftisdf.py:97-121)
  * Needs fisdf_factor_x4 on the same range.  W_q = zeta_q z_q^H computed as
@@ -250,6 +266,12 @@ int fisdf_fft3d(fisdf_ctx* ctx, const void* d_in, void* d_out, int rows, const i
 /* sqrt(coulG(k+G) * scale) (or without sqrt), PySCF get_coulG(exxdiv=None) restated */
 int fisdf_coulg(fisdf_ctx* ctx, const int mesh[3], const double a[9], const double k[3],
                 double scale, int take_sqrt, double* d_w);
+/* minimum-norm operator of one Hermitian PSD n x n matrix (the fit's FISDF_FIT_LSTSQ/SVD path):
+ * rank-revealing pivoted Cholesky (cut tol_rel * max diag) then M = (P L)^+ (n x n, rows < rank
+ * valid, columns in pivot order h_piv), so x4^+ ~ P M^H M P^T; d_Q (n x rank) and d_Rinv
+ * (rank x rank), if not NULL, receive the thin QR factors P L = Q R; synchronous */
+int fisdf_min_norm_operator(fisdf_ctx* ctx, const void* d_A, int n, double tol_rel, void* d_M,
+                            void* d_Q, void* d_Rinv, int* h_piv /* n */, int* h_rank);
 /* batched pivoted Cholesky (pivots + ranks to host; synchronous) */
 int fisdf_pivoted_cholesky(fisdf_ctx* ctx, const void* d_A, int n, int batch, int rmax,
                            double tol_rel, int* h_piv /* batch*rmax */, int* h_rank /* batch */);

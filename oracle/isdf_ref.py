@@ -158,12 +158,26 @@ def build_y(f_k, xip, phase):
     return y_k.reshape(nkpt, nblk, nip)
 
 
-def fit_and_coulomb(x4_q, y_q, vq, coord, a, mesh, vol, Gv=None, omega=None):
-    """fftisdf.py:97-121 for one q: gelsy fit then FFT Coulomb -> (W_q, rank)."""
+def svd_solve(x4_q, rhs, cut=np.finfo(float).eps):
+    """Truncated SVD pseudo-solve z = V_r S_r^-1 U_r^H rhs, s_i > cut * s_0 (cut = machine eps,
+    scipy lstsq's default rcond): what the SVD fit of fftdf-with-k-svd.py:158-164
+    intends (that code keeps a fixed rank 300 and leaves z in the rotated basis, SURVEY
+    Appendix B; restated here without those defects)."""
+    u, sv, vh = scipy.linalg.svd(x4_q, full_matrices=False)
+    r = int((sv > cut * sv[0]).sum())
+    return vh[:r].conj().T @ ((u[:, :r].conj().T @ rhs) / sv[:r, None]), r
+
+
+def fit_and_coulomb(x4_q, y_q, vq, coord, a, mesh, vol, Gv=None, omega=None, solver="gelsy"):
+    """fftisdf.py:97-121 for one q: gelsy fit (or the SVD pseudo-solve) then FFT Coulomb ->
+    (W_q, rank)."""
     ngrid = coord.shape[0]
     fq = np.exp(-1j * coord @ vq)                                     # :99
-    res = scipy.linalg.lstsq(x4_q, y_q.T, lapack_driver="gelsy")     # :108
-    z_q, rank = res[0], res[2]
+    if solver == "svd":
+        z_q, rank = svd_solve(x4_q, y_q.T)                            # fftdf-with-k-svd.py:158
+    else:
+        res = scipy.linalg.lstsq(x4_q, y_q.T, lapack_driver="gelsy")  # :108
+        z_q, rank = res[0], res[2]
     zeta = fft(z_q * fq, mesh)                                        # :113
     zeta *= get_coulG(a, vq, mesh, Gv=Gv, omega=omega)                # :114
     zeta *= vol / ngrid                                               # :115
@@ -172,7 +186,8 @@ def fit_and_coulomb(x4_q, y_q, vq, coord, a, mesh, vol, Gv=None, omega=None):
     return zeta @ z_q.conj().T, rank                                  # :121
 
 
-def build(xip, f_k, coord, a, kmesh, mesh, blksize=8000, progress=False, omega=None):
+def build(xip, f_k, coord, a, kmesh, mesh, blksize=8000, progress=False, omega=None,
+          solver="gelsy"):
     """fftisdf.py:22-128 given the interpolation-point AOs ``xip`` and the grid AOs ``f_k``.
 
     Returns dict(x=xip, w0=W_0, wq=W_q, ranks=[...], y=y, x4=x4_k).
@@ -190,7 +205,7 @@ def build(xip, f_k, coord, a, kmesh, mesh, blksize=8000, progress=False, omega=N
     Gv = get_Gv(a, mesh)
     wq, ranks = [], []
     for q, vq in enumerate(kpts):                                     # :97
-        w, r = fit_and_coulomb(x4_k[q], y[q], vq, coord, a, mesh, vol, Gv, omega)
+        w, r = fit_and_coulomb(x4_k[q], y[q], vq, coord, a, mesh, vol, Gv, omega, solver)
         wq.append(w)
         ranks.append(r)
         if progress:

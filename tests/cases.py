@@ -22,6 +22,10 @@ CASES = {
     "nio_small": (lambda: C.nio_cell(mesh=(16, 16, 16)), (1, 1, 2), (9, 9, 9), 5.0),
     # C5-shaped: Si 2x2x2 diamond supercell, 16 atoms, szv-shaped (nao 64), Gamma only
     "si_small": (lambda: C.si_supercell(mesh=(12, 12, 12)), (1, 1, 1), (9, 9, 9), 8.0),
+    # the reference demo's regime (fftisdf.py:455-461, c0 = 40 with m0 = 15^3): nao * c0
+    # exceeds the parent-Gram rank, so nip = rank (fftisdf.py:383) and every x4_q is
+    # rank-deficient
+    "toy222_rank": (lambda: C.toy_cell(mesh=(12, 12, 12)), (2, 2, 2), (9, 9, 9), 100.0),
 }
 
 
@@ -58,3 +62,17 @@ def oracle(name):
     vj = R.get_j_kpts(xip, out["w0"], dm, kpts_band_is_zero=bool(abs(kpts).max() < 1e-9))
     vk = R.get_k_kpts(xip, out["wq"], dm, phase)
     return dict(perm=perm, rank=rank, nip=nip, x4sel=x4sel, xip=xip, vj=vj, vk=vk, **out)
+
+
+@functools.lru_cache(maxsize=None)
+def oracle_svd(name):
+    """The oracle with the SVD pseudo-solve (fftdf-with-k-svd.py:158-164 intent) on the gelsy
+    oracle's interpolation points."""
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
+    o = oracle(name)
+    out = R.build(o["xip"], chi, coords, cell.a, kmesh, cell.mesh, solver="svd")
+    kpts = R.get_kpts(cell.a, kmesh)
+    phase = R.get_phase(cell.a, kpts, kmesh)
+    vj = R.get_j_kpts(o["xip"], out["w0"], dm, kpts_band_is_zero=bool(abs(kpts).max() < 1e-9))
+    vk = R.get_k_kpts(o["xip"], out["wq"], dm, phase)
+    return dict(vj=vj, vk=vk, ranks=out["ranks"], wq=out["wq"])

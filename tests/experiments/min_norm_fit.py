@@ -109,3 +109,20 @@ def run(name):
 if __name__ == "__main__":
     for n in sys.argv[1:] or ["toy331", "toy222"]:
         run(n)
+
+
+def w_cod(x4, yh, tol):
+    """minimum-norm solution from the pivoted Cholesky via a thin QR of A = P L (nip x r):
+    x4 ~ A A^H, z = A^{+H} A^+ y, A^+ = R_A^{-1} Q_A^H (no normal equations)."""
+    L, P, r = pchol(x4, tol)
+    A = np.zeros((len(x4), r), complex)
+    A[P] = L
+    Qa, Ra = np.linalg.qr(A)
+    M = sl.solve_triangular(Ra, Qa.conj().T)          # r x nip  = A^+
+    U = M @ yh
+    G = U @ U.conj().T
+    return M.conj().T @ G @ M, r
+
+
+if __name__ == "__main__" and os.environ.get("COD"):
+    pass

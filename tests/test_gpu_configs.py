@@ -31,6 +31,8 @@ def _gpu_build(cfg):
     from fisdf import ISDF
     cell, kmesh, m0, c0, x0, chi, dm = bench.setup(cfg)
     df = ISDF(cell, cell.get_kpts(kmesh), m0=list(m0), c0=c0)
+    if cfg == "c4":          # C4 is the "SVD fit" configuration (BASELINE.json configs[3])
+        df.fit = "svd"
     d = df.device
     df._kmesh()
     df._ao_parent = d.to_dev(x0)
@@ -49,7 +51,10 @@ def test_config_parity_full_size(cfg):
     df, cell, kmesh, x0, chi, dm, vj, vk, mi = _gpu_build(cfg)
     nk = int(np.prod(kmesh))
     print(f"\n{cfg}: nk {nk} nao {cell.nao_nr()} nip {df.nip} mesh {tuple(cell.mesh)} "
-          f"ranks {df.ranks.min()}-{df.ranks.max()} max_imag {mi}", flush=True)
+          f"ranks {df.ranks.min()}-{df.ranks.max()} fit {df.fit} (min-norm q {df.min_norm_slots}) "
+          f"max_imag {mi}", flush=True)
+    if cfg == "c4":
+        assert df.min_norm_slots == len(df.fit_qs)
     # reality monitors of fftisdf.py:43 (x2_s), :81 (fx_s), :216 (rho_s), relative to O(1) data
     assert max(mi) < 1e-10, mi
     xip = x0[:, df.perm]

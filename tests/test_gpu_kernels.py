@@ -162,3 +162,48 @@ def test_pivoted_cholesky_batched_hermitian(env):
         Ap = A[b][:, p]
         resid = A[b] - Ap @ np.linalg.solve(App, Ap.conj().T)
         assert abs(resid).max() < 1e-8 * abs(A[b]).max()
+
+
+@pytest.mark.parametrize("real", [False, True])
+def test_min_norm_operator(env, real):
+    """fisdf_min_norm_operator (the fit's minimum-norm path) on a rank-deficient Hermitian PSD
+    matrix with a decaying spectrum: P L = Q R with Q orthonormal and Q R equal to the host's
+    truncated factor of the same pivots to its conditioning, M = R^{-1} Q^H, and the solve
+    z = P M^H M P^T b of a right-hand side b = x4 v in the range reproduces b (residual) with
+    |z| <= |v| (minimum norm)."""
+    torch, L, ctx = env
+    rng = np.random.default_rng(11)
+    n, rk = 150, 90
+    B = rnd(rng, n, rk) if not real else rng.standard_normal((n, rk)).astype(np.complex128)
+    B = B * np.exp(-0.25 * np.arange(rk))
+    A = B @ B.conj().T
+    dA = dev(torch, A)
+    dM, dQ, dR = (torch.zeros(n, n, dtype=torch.complex128, device=dA.device) for _ in range(3))
+    piv = np.zeros(n, np.int32)
+    rnk = np.zeros(1, np.int32)
+    ctx.call("fisdf_min_norm_operator", L.ptr(dA), n, 1e-14, L.ptr(dM), L.ptr(dQ), L.ptr(dR),
+             piv.ctypes.data_as(L._ip), rnk.ctypes.data_as(L._ip))
+    r = int(rnk[0])
+    assert 0 < r < n and sorted(piv) == list(range(n))
+    M = dM.cpu().numpy()[:r]
+    Q = dQ.cpu().numpy().reshape(-1)[:n * r].reshape(n, r)
+    Ri = dR.cpu().numpy().reshape(-1)[:r * r].reshape(r, r)
+    Ap = A[np.ix_(piv, piv)]
+    L11 = np.linalg.cholesky(Ap[:r, :r])
+    Af = np.concatenate([L11, np.linalg.solve(L11, Ap[:r, r:]).conj().T])
+    X = Q @ np.linalg.inv(Ri)                          # the device's P L
+    qerr = abs(Q.conj().T @ Q - np.eye(r)).max()
+    aerr = abs(X - Af).max() / abs(Af).max()
+    merr = abs(M - Ri @ Q.conj().T).max() / abs(M).max()
+    v = rng.standard_normal(n) + (0 if real else 1j * rng.standard_normal(n))
+    b = A @ v
+    z = np.zeros(n, complex)
+    z[piv] = M.conj().T @ (M @ b[piv])
+    res = np.linalg.norm(A @ z - b) / np.linalg.norm(b)
+    print(f"min-norm operator n={n} rank {r} real={real}: |Q^H Q - I| {qerr:.1e}, rel |QR - PL| "
+          f"{aerr:.1e}, |M - R^-1 Q^H| {merr:.1e}, residual {res:.1e}, |z|/|v| "
+          f"{np.linalg.norm(z) / np.linalg.norm(v):.3f}")
+    assert qerr < 1e-12 and aerr < 1e-6 and merr < 1e-12
+    assert res < 1e-6 and np.linalg.norm(z) <= np.linalg.norm(v)
+    if real:
+        assert abs(M.imag).max() == 0.0

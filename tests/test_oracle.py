@@ -194,3 +194,22 @@ def _blocked_trsm(L, B, nb):
         Linv = scipy.linalg.solve_triangular(L[b0:b1, b0:b1], np.eye(b1 - b0), lower=True)
         X[b0:b1] = Linv @ B[b0:b1]
     return X
+
+
+def test_svd_solver_is_the_unique_solution_when_full_rank():
+    """oracle svd_solve (the SVD fit of fftdf-with-k-svd.py:158-164, restated) equals gelsy on a
+    full-rank Hermitian system, and gives the minimum-norm solution on a rank-deficient one."""
+    import scipy.linalg
+    rng = np.random.default_rng(3)
+    B = rng.standard_normal((60, 60)) + 1j * rng.standard_normal((60, 60))
+    A = B @ B.conj().T + 60 * np.eye(60)
+    y = rng.standard_normal((60, 5)) + 1j * rng.standard_normal((60, 5))
+    z, r = R.svd_solve(A, y)
+    zg = scipy.linalg.lstsq(A, y, lapack_driver="gelsy")[0]
+    assert r == 60 and abs(z - zg).max() < 1e-12 * abs(zg).max()
+    Bd = B[:, :40]
+    Ad = Bd @ Bd.conj().T                       # rank 40
+    yd = Ad @ (rng.standard_normal((60, 3)) + 0j)
+    zd, rd = R.svd_solve(Ad, yd)
+    zp = np.linalg.pinv(Ad, rcond=1e-12) @ yd
+    assert rd == 40 and abs(zd - zp).max() < 1e-9 * abs(zp).max()

@@ -36,7 +36,7 @@ QUICK = "--quick" in sys.argv
 r, N = 600, 46656
 A = rnd(r, N)
 Cm = rnd(r, r)
-for ks in ((13,) if QUICK else (8, 13, 16, 32)):
+for ks in ((13, 41) if QUICK else (8, 13, 16, 32, 41)):
     ms = timeit(lambda: ctx.call("fisdf_herk", r, N, 1.0, L.ptr(A), N, L.ptr(Cm), r, ks))
     print(f"herk n={r} K={N} ksplit={ks}: {ms:.3f} ms  {4.0 * r * r * N / ms / 1e9:.1f} TF/s", flush=True)
 # TRSM-like block GEMMs: C(64 x N) -= L(64 x K) X(K x N)
