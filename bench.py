@@ -49,7 +49,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-q", type=int, default=1, help="q-points timed in the CPU sample")
+    p.add_argument("--cpu-q", type=int, default=4, help="q-points fitted in the CPU sample")
     return p.parse_args()
 
 
@@ -69,11 +69,11 @@ def setup(cfg):
 
 
 def cpu_baseline(cell, kmesh, m0, c0, x0, chi, dm, nq):
-    """Oracle (NumPy/SciPy restatement of fftisdf.py) on a bounded sample of the same job,
-    extrapolated to the whole job: selection + x4 + y for a grid slice + fit/FFT/W for nq
-    q-points + get_jk, scaled by ngrid/slice and nk/nq."""
+    """Oracle (NumPy/SciPy restatement of fftisdf.py, the reference CPU path) on a bounded
+    sample of the same job: selection, x4 and the y build over the WHOLE grid (y kept only for
+    the sampled q), the gelsy fit + FFT Coulomb for nq q-points (Gamma and complex q, like the
+    reference which fits every q), get_jk; the fit time is scaled by nk/nq."""
     from oracle import isdf_ref as R
-    import scipy
     nk = chi.shape[0]
     ngrid = chi.shape[1]
     t = {}
@@ -86,27 +86,27 @@ def cpu_baseline(cell, kmesh, m0, c0, x0, chi, dm, nq):
     t0 = time.perf_counter()
     x4 = R.build_x4(xip, phase)
     t["x4"] = time.perf_counter() - t0
-    blk = min(ngrid, 4000)
+    # sampled q: Gamma plus complex q (2 k_q not a reciprocal vector) spread over the mesh
+    ks = np.stack(np.unravel_index(np.arange(nk), tuple(kmesh)), 1)
+    cplx = [q for q in range(nk) if ((2 * ks[q]) % np.asarray(kmesh)).any()] or list(range(1, nk))
+    qs = [0] + [cplx[i] for i in np.linspace(0, len(cplx) - 1, max(nq - 1, 0)).astype(int)
+                if cplx][:max(nq - 1, 0)]
+    qs = sorted(set(qs))[:nk]
+    # the y build of fftisdf.py:67-87 over the whole grid in its 8000-point blocks; the
+    # 28.7 GB y (C3) is not kept, only the sampled q columns
+    yq = np.empty((len(qs), ngrid, nip), complex)
     t0 = time.perf_counter()
-    yb = R.build_y(chi[:, :blk], xip, phase)
-    t["y"] = (time.perf_counter() - t0) * ngrid / blk
-    del yb
-    # fit + Coulomb for nq q-points on the full grid (needs y_q for all g: build per q)
+    for g0 in range(0, ngrid, 8000):
+        g1 = min(g0 + 8000, ngrid)
+        yq[:, g0:g1] = R.build_y(chi[:, g0:g1], xip, phase)[qs]
+    t["y"] = time.perf_counter() - t0
     coords = cell.gen_uniform_grids(cell.mesh)
     Gv = R.get_Gv(cell.a, cell.mesh)
-    tq = 0.0
-    for q in range(nq):
-        # y_q over the whole grid (excluded from the fit timing: counted in t["y"])
-        yq = np.empty((ngrid, nip), complex)
-        for g0 in range(0, ngrid, 8000):
-            g1 = min(g0 + 8000, ngrid)
-            fx = np.asarray([f.conj() @ x.T for f, x in zip(chi[:, g0:g1], xip)])
-            fs = (phase @ fx.reshape(nk, -1)).real ** 2
-            yq[g0:g1] = (phase[:, q] @ fs.reshape(nk, -1)).reshape(g1 - g0, nip)
-        t0 = time.perf_counter()
-        R.fit_and_coulomb(x4[q], yq, kpts[q], coords, cell.a, cell.mesh, cell.vol, Gv)
-        tq += time.perf_counter() - t0
-    t["fit"] = tq * nk / nq
+    t0 = time.perf_counter()
+    for i, q in enumerate(qs):
+        R.fit_and_coulomb(x4[q], yq[i], kpts[q], coords, cell.a, cell.mesh, cell.vol, Gv)
+    t["fit"] = (time.perf_counter() - t0) * nk / len(qs)
+    del yq
     dms = dm[None]
     t0 = time.perf_counter()
     wq = np.zeros((nk, nip, nip), complex)  # timing only: get_jk cost is independent of values
@@ -120,11 +120,16 @@ def cpu_baseline(cell, kmesh, m0, c0, x0, chi, dm, nq):
         cores = max(i.get("num_threads", 1) for i in threadpool_info()) or cores
     except Exception:
         pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except Exception:
+        affinity = None
     return dict(value=nk / total, unit="k-points/s", cores=int(cores), kind="port",
                 sample=(f"oracle (NumPy/SciPy gelsy restatement of fftisdf.py) timed on "
-                        f"selection + x4 + y on {blk}/{ngrid} grid points + fit/FFT/W for "
-                        f"{nq}/{nk} q + get_jk, extrapolated to the full job "
+                        f"selection + x4 + the full-grid y build ({ngrid} points) + gelsy fit/"
+                        f"FFT/W for q {qs} of {nk} (x{nk / len(qs):.0f}) + get_jk "
                         f"(est. {total:.1f} s/job)"),
+                affinity_cpus=affinity, host_cpus=os.cpu_count(),
                 stages_s={k: round(v, 3) for k, v in t.items()})
 
 

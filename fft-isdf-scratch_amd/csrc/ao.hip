@@ -145,14 +145,34 @@ __global__ void bloch_dft_kernel(const double* __restrict__ F, long ncol, int n0
   chi[(long)k * ncol + col] = acc;
 }
 
+// band k-points (any k, kpts_band of get_jk): chi[k][col] = sum_t exp(i k . T_t) F[t][col], one
+// thread per (k, column), F holding one image per lattice translation
+__global__ void bloch_band_kernel(const double* __restrict__ F, long ncol, int nT,
+                                  const cplx* __restrict__ ph, int nkb, cplx* __restrict__ chi) {
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= ncol * nkb) return;
+  const int k = (int)(e / ncol);
+  const long col = e % ncol;
+  cplx acc = cmk(0, 0);
+  for (int t = 0; t < nT; ++t) {
+    const double x = F[(long)t * ncol + col];
+    const cplx p = ph[(long)t * nkb + k];
+    acc = cadd(acc, cmk(p.x * x, p.y * x));
+  }
+  chi[(long)k * ncol + col] = acc;
+}
+
 }  // namespace
 
 int eval_ao(hipStream_t s, const double* d_coords, int ng, int natm, const double* h_atoms, int nsh,
             const int* h_sh_atom, const int* h_sh_l, const int* h_sh_nprim, const double* h_exps,
             const double* h_coefs, int nT, const int* h_tn, const int kmesh[3], const double a[9],
-            double rcut, double* F, void* scratch, size_t scratch_size, cplx* chi, int* h_nao) {
+            double rcut, double* F, void* scratch, size_t scratch_size, cplx* chi, int* h_nao,
+            int nkb, const double* h_kband) {
   FISDF_CHECK(ng >= 0 && natm > 0 && nsh > 0 && nT >= 0, "eval_ao: bad sizes");
-  const int nimg = kmesh[0] * kmesh[1] * kmesh[2];
+  // band mode (nkb > 0): every translation is its own image, phases exp(i k.T) per band k
+  const bool band = nkb > 0;
+  const int nimg = band ? std::max(nT, 1) : kmesh[0] * kmesh[1] * kmesh[2];
   // shells, AO -> (shell, m) maps
   std::vector<AoShell> sh(nsh);
   std::vector<int> ao_shell, ao_m;
@@ -174,8 +194,8 @@ int eval_ao(hipStream_t s, const double* d_coords, int ng, int natm, const doubl
   for (int t = 0; t < nT; ++t) {
     const int* n = h_tn + 3 * t;
     int r[3];
-    for (int d = 0; d < 3; ++d) r[d] = ((n[d] % kmesh[d]) + kmesh[d]) % kmesh[d];
-    const int R = (r[0] * kmesh[1] + r[1]) * kmesh[2] + r[2];
+    for (int d = 0; d < 3 && !band; ++d) r[d] = ((n[d] % kmesh[d]) + kmesh[d]) % kmesh[d];
+    const int R = band ? t : (r[0] * kmesh[1] + r[1]) * kmesh[2] + r[2];
     for (int d = 0; d < 3; ++d)
       byR[R].push_back(n[0] * a[0 * 3 + d] + n[1] * a[1 * 3 + d] + n[2] * a[2 * 3 + d]);
   }
@@ -196,8 +216,19 @@ int eval_ao(hipStream_t s, const double* d_coords, int ng, int natm, const doubl
                oAM = take(sizeof(int) * nao), oE = take(sizeof(double) * p0),
                oC = take(sizeof(double) * p0), oA = take(sizeof(double) * 3 * natm),
                oT = take(sizeof(double) * std::max<size_t>(Tvec.size(), 1)),
-               oO = take(sizeof(int) * (nimg + 1));
+               oO = take(sizeof(int) * (nimg + 1)),
+               oP = take(sizeof(cplx) * (band ? (size_t)nimg * nkb : 1));
   FISDF_CHECK(off <= scratch_size, "eval_ao: scratch too small");
+  std::vector<cplx> ph;
+  if (band) {  // exp(i k . T_t), T_t = n_t . a in the translation order (one image each)
+    ph.resize((size_t)nimg * nkb, cmk(0, 0));
+    for (int t = 0; t < nT; ++t)
+      for (int k = 0; k < nkb; ++k) {
+        double th = 0;
+        for (int d = 0; d < 3; ++d) th += Tvec[3 * t + d] * h_kband[3 * k + d];
+        ph[(size_t)t * nkb + k] = cmk(std::cos(th), std::sin(th));
+      }
+  }
   char* b = (char*)scratch;
   FISDF_HIP(hipMemcpyAsync(b + oS, sh.data(), sizeof(AoShell) * nsh, hipMemcpyHostToDevice, s));
   FISDF_HIP(hipMemcpyAsync(b + oAS, ao_shell.data(), sizeof(int) * nao, hipMemcpyHostToDevice, s));
@@ -209,7 +240,12 @@ int eval_ao(hipStream_t s, const double* d_coords, int ng, int natm, const doubl
     FISDF_HIP(hipMemcpyAsync(b + oT, Tvec.data(), sizeof(double) * Tvec.size(),
                              hipMemcpyHostToDevice, s));
   FISDF_HIP(hipMemcpyAsync(b + oO, Toff.data(), sizeof(int) * (nimg + 1), hipMemcpyHostToDevice, s));
-  if (ng == 0) return 0;
+  if (band)
+    FISDF_HIP(hipMemcpyAsync(b + oP, ph.data(), sizeof(cplx) * ph.size(), hipMemcpyHostToDevice, s));
+  if (ng == 0) {
+    FISDF_HIP(hipStreamSynchronize(s));  // the host tables must outlive the asynchronous copies
+    return 0;
+  }
   const long nth = (long)ng * nao;
   hipLaunchKernelGGL(ao_folded_kernel, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s,
                      d_coords, ng, nao, (const int*)(b + oAS), (const int*)(b + oAM),
@@ -220,6 +256,13 @@ int eval_ao(hipStream_t s, const double* d_coords, int ng, int natm, const doubl
   // the host tables must outlive the asynchronous copies
   FISDF_HIP(hipStreamSynchronize(s));
   const long ncol = nth;
+  if (band) {
+    const long tot = ncol * nkb;
+    hipLaunchKernelGGL(bloch_band_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, F,
+                       ncol, nT, (const cplx*)(b + oP), nkb, chi);
+    FISDF_HIP(hipGetLastError());
+    return 0;
+  }
 #define FISDF_BD(x, y, z)                                                                      \
   if (kmesh[0] == x && kmesh[1] == y && kmesh[2] == z) {                                       \
     hipLaunchKernelGGL((bloch_dft_reg_kernel<x, y, z>),                                         \

@@ -784,6 +784,33 @@ int fisdf_eval_ao(fisdf_ctx* c, const void* d_coords, int ng, int natm, const do
   return 0;
 }
 
+int fisdf_eval_ao_band(fisdf_ctx* c, const void* d_coords, int ng, int natm, const double* h_atoms,
+                       int nsh, const int* h_sh_atom, const int* h_sh_l, const int* h_sh_nprim,
+                       const double* h_exps, const double* h_coefs, int nT, const int* h_tn,
+                       int nkb, const double* h_kpts, const double* a, double rcut, int nao,
+                       void* d_out) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(nkb > 0 && h_kpts != nullptr, "eval_ao_band: no band k-points");
+  StageTimer tm(c, FISDF_ST_AO);
+  int nao_sh = 0;
+  for (int i = 0; i < nsh; ++i) nao_sh += 2 * h_sh_l[i] + 1;
+  FISDF_CHECK(nao_sh == nao, "eval_ao_band: nao does not match the shells");
+  const int one[3] = {1, 1, 1};
+  Carver cv;
+  const size_t oF = cv.take(sizeof(double) * (size_t)std::max(nT, 1) * ng * nao);
+  const size_t tables = (1 << 20) + sizeof(double) * 3 * (size_t)std::max(nT, 1) +
+                        sizeof(cplx) * (size_t)std::max(nT, 1) * nkb + sizeof(int) * (nT + 2);
+  const size_t oT = cv.take(tables);
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  char* b = (char*)base;
+  int nao_out = 0;
+  FISDF_TRY(eval_ao(c->stream, (const double*)d_coords, ng, natm, h_atoms, nsh, h_sh_atom, h_sh_l,
+                    h_sh_nprim, h_exps, h_coefs, nT, h_tn, one, a, rcut, (double*)(b + oF), b + oT,
+                    tables, (cplx*)d_out, &nao_out, nkb, h_kpts));
+  return 0;
+}
+
 int fisdf_gather_points(fisdf_ctx* c, const void* x0, int nk, int ng0, int nao, const int* h_perm,
                         int nip, void* X) {
   FISDF_TRY(device_guard(c));
@@ -1772,6 +1799,47 @@ int fisdf_get_j_rows(fisdf_ctx* c, const void* Xv, const void* W0, const void* d
     FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nao, nao, nb, ONE, X + (long)i0 * nao, nao, xs,
                     T + (long)x * nk * nb * nao, nao, (long)nb * nao, ZERO,
                     vj + (long)x * nk * ds, nao, ds, nk));
+  return 0;
+}
+
+int fisdf_get_j_band_rows(fisdf_ctx* c, const void* Xv, const void* W0, const void* dmsv, int nset,
+                          int nk, int nip, int nao, const void* Xbv, int nkb, int i0, int i1,
+                          void* vjv) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(0 <= i0 && i0 <= i1 && i1 <= nip && nkb > 0, "get_j_band: bad sizes");
+  StageTimer tm(c, FISDF_ST_J);
+  const cplx* X = (const cplx*)Xv;
+  const cplx* Xb = (const cplx*)Xbv;
+  const cplx* dms = (const cplx*)dmsv;
+  cplx* vj = (cplx*)vjv;
+  const int nb = i1 - i0;
+  const long xs = (long)nip * nao, ds = (long)nao * nao;
+  if (nb == 0) {
+    FISDF_HIP(hipMemsetAsync(vj, 0, sizeof(cplx) * nset * nkb * ds, c->stream));
+    return 0;
+  }
+  Carver cv;
+  size_t oT = cv.take(sizeof(cplx) * nset * (size_t)std::max(nk, nkb) * xs);
+  size_t oR = cv.take(sizeof(cplx) * nset * nip);
+  size_t oV = cv.take(sizeof(cplx) * nset * nb);
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  cplx* T = (cplx*)((char*)base + oT);
+  cplx* rho = (cplx*)((char*)base + oR);
+  cplx* v = (cplx*)((char*)base + oV);
+  // rho_I from the k-mesh density matrices and v = W0 rho (fftisdf.py:155-159), as get_j
+  for (int x = 0; x < nset; ++x)
+    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nip, nao, nao, ONE, X, nao, xs, dms + (long)x * nk * ds,
+                    nao, ds, ZERO, T + (long)x * nk * xs, nao, xs, nk));
+  FISDF_TRY(rho_diag(c->stream, T, X, nset, nk, nip, nao, 1.0 / nk, rho));
+  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nb, 1, nip, ONE, (const cplx*)W0 + (long)i0 * nip, nip, 0,
+                  rho, 1, nip, ZERO, v, 1, nb, nset));
+  // J_k' = Xb_k'[I]^H diag(v_I) Xb_k'[I] at the band k-points (fftisdf.py:166 with kpts_band)
+  FISDF_TRY(scale_rows(c->stream, Xb, v, nset, nkb, nip, i0, nb, nao, T));
+  for (int x = 0; x < nset; ++x)
+    FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nao, nao, nb, ONE, Xb + (long)i0 * nao, nao, xs,
+                    T + (long)x * nkb * nb * nao, nao, (long)nb * nao, ZERO,
+                    vj + (long)x * nkb * ds, nao, ds, nkb));
   return 0;
 }
 

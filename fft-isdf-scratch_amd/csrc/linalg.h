@@ -62,11 +62,13 @@ int pair_product(hipStream_t s, const cplx* A, int n1, const cplx* B, int n2, in
 // half: FX holds only the first kmesh_half_count(kmesh) k (planes a <= n0/2); the others are
 // conj(FX[-k]) (time reversal)
 int kmesh_half_count(const int kmesh[3]);
-// Bloch AO values (ao.hip): F (nimg, ng, nao) f64 workspace, scratch for the small tables
+// Bloch AO values (ao.hip): F (nimg, ng, nao) f64 workspace, scratch for the small tables;
+// nkb > 0: at the nkb band k-points h_kband (any k) instead of the k-mesh, F (nT, ng, nao)
 int eval_ao(hipStream_t s, const double* d_coords, int ng, int natm, const double* h_atoms, int nsh,
             const int* h_sh_atom, const int* h_sh_l, const int* h_sh_nprim, const double* h_exps,
             const double* h_coefs, int nT, const int* h_tn, const int kmesh[3], const double a[9],
-            double rcut, double* F, void* scratch, size_t scratch_size, cplx* chi, int* h_nao);
+            double rcut, double* F, void* scratch, size_t scratch_size, cplx* chi, int* h_nao,
+            int nkb = 0, const double* h_kband = nullptr);
 int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const int* h_qs,
             const int* d_qs, int nq, int m, cplx* yT, long qs, long Is, long goff, bool half,
             unsigned long long* mon);

@@ -45,6 +45,9 @@ _SIGS = {
     "fisdf_gather_points": ([_vp, _vp, _i, _i, _i, _ip, _i, _vp], _i),
     "fisdf_eval_ao": ([_vp, _vp, _i, _i, _dp, _i, _ip, _ip, _ip, _dp, _dp, _i, _ip, _ip, _dp, _d,
                        _i, _vp], _i),
+    "fisdf_eval_ao_band": ([_vp, _vp, _i, _i, _dp, _i, _ip, _ip, _ip, _dp, _dp, _i, _ip, _i, _dp,
+                            _dp, _d, _i, _vp], _i),
+    "fisdf_get_j_band_rows": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _vp], _i),
     "fisdf_select_gram": ([_vp, _vp, _i, _i, _i, _i, _i, _vp], _i),
     "fisdf_select_pivots": ([_vp, _vp, _i, _i, _i, _d, _ip, _ip, _ip], _i),
     "fisdf_unpack_slices": ([_vp, _vp, _i, _i, C.POINTER(_l), C.POINTER(_l), _l, _vp], _i),

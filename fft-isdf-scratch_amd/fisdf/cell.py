@@ -272,6 +272,42 @@ def eval_ao_folded(cell, coords, kmesh):
     return out
 
 
+def eval_ao_band(cell, coords, kpts):
+    """Bloch AO values at arbitrary k-points (kpts_band), (nkb, ng, nao) complex128:
+    chi_k(r) = sum_T exp(i k.T) phi(r - T) over the translations of ``lattice_translations``
+    (pbc_eval_gto at band k-points [pyscf]; off the k-mesh the image folding of
+    ``eval_ao_folded`` does not apply)."""
+    coords = np.asarray(coords, float)
+    kpts = np.asarray(kpts, float).reshape(-1, 3)
+    ng = coords.shape[0]
+    nao = cell.nao_nr()
+    a = cell.lattice_vectors()
+    rc2 = cell.rcut() ** 2
+    atom_xyz = cell.atom_coords()
+    out = np.zeros((len(kpts), ng, nao), complex)
+    shells_by_atom = {}
+    for sh in cell.shells:
+        shells_by_atom.setdefault(sh[0], []).append(sh)
+    for n in lattice_translations(cell, coords):
+        T = n @ a
+        ph = np.exp(1j * kpts @ T)
+        F = np.zeros((ng, nao))
+        for ia in range(cell.natm):
+            d = coords - (atom_xyz[ia] + T)
+            r2 = np.einsum("gi,gi->g", d, d)
+            m = r2 < rc2
+            if not m.any():
+                continue
+            dm = d[m]
+            idx = np.nonzero(m)[0]
+            for (_, l, exps, cs, ao0) in shells_by_atom.get(ia, []):
+                rad = np.exp(-np.outer(r2[m], exps)) @ cs
+                angs = _real_sph(l, dm[:, 0], dm[:, 1], dm[:, 2])
+                F[idx, ao0:ao0 + NSPH[l]] += np.stack([rad * g for g in angs], axis=1)
+        out += ph[:, None, None] * F[None]
+    return out
+
+
 def eval_ao_kpts(cell, coords, kmesh, folded=None):
     """Bloch AO values chi_k(r), shape (nk, ng, nao), complex128 (pbc_eval_gto 'GTOval')."""
     if folded is None:

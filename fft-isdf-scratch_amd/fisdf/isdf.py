@@ -281,16 +281,17 @@ class InterpolativeSeparableDensityFitting:
         kpts = self.kpts if kpts is None else np.asarray(kpts)
         if kpts.ndim == 1:                                            # _check_kpts single kpt
             raise NotImplementedError
+        band = _band_of(self, kpts, kpts_band)
         vj = vk = None
         # one upload of the density matrices, K then J enqueued back to back (:404-407), one
         # read-back each at the end: no host round trip between the two
         dms, ddms = _dms_to_dev(self, dm)
         if with_k:
-            vk = _get_k_dev(self, ddms, exxdiv)
+            vk = _get_k_dev(self, ddms, exxdiv, band)
         if with_j:
-            vj = _get_j_dev(self, ddms)
+            vj = _get_j_dev(self, ddms, band)
         if vk is not None:
-            vk = _format_jks(vk.cpu().numpy(), dm)
+            vk = _format_band(vk.cpu().numpy(), dm, kpts_band, kpts)
         if vj is not None:
             vj = _finish_j(vj, dm, kpts, kpts_band)
         return vj, vk
@@ -605,24 +606,72 @@ def _dms_to_dev(df_obj, dm_kpts):
 
 
 def get_j_kpts(df_obj, dm_kpts, hermi=1, kpts=np.zeros((1, 3)), kpts_band=None, exxdiv=None):
-    """fftisdf.py:133-171."""
+    """fftisdf.py:133-171 (kpts_band: J at any band k-points, next-4)."""
     assert exxdiv is None
     dms, ddms = _dms_to_dev(df_obj, dm_kpts)
-    return _finish_j(_get_j_dev(df_obj, ddms), dm_kpts, kpts, kpts_band)
+    band = _band_of(df_obj, np.asarray(kpts), kpts_band)
+    return _finish_j(_get_j_dev(df_obj, ddms, band), dm_kpts, kpts, kpts_band)
 
 
-def _get_j_dev(df_obj, ddms):
-    """vj on the device (fftisdf.py:150-166) for device dms (nset, nk, nao, nao)."""
+def _band_of(df_obj, kpts, kpts_band):
+    """kpts_band (fftisdf.py:162-164,194-196; the reference asserts nband == nkpt): None when the
+    band k-points are the k-mesh itself, else the (nband, 3) array."""
+    if kpts_band is None:
+        return None
+    kb = np.asarray(kpts_band, float).reshape(-1, 3)
+    mesh_k = np.asarray(df_obj.kpts, float).reshape(-1, 3)
+    if kb.shape == mesh_k.shape and abs(kb - mesh_k).max() < 1e-9:
+        return None
+    return kb
+
+
+def _format_band(v, dm_kpts, kpts_band, kpts):
+    """[pyscf] df_jk._format_jks with kpts_band: v (nset, nband, nao, nao) -> the caller's
+    shape (band axis dropped for a 1-D band k-point; set axis dropped unless the dms carry one)."""
+    if kpts_band is None:
+        return _format_jks(v, dm_kpts)
+    dm = np.asarray(dm_kpts)
+    if np.ndim(kpts_band) == 1:
+        v = v[:, 0]
+    if dm.ndim < 3:
+        return v[0]
+    if dm.ndim == 3 and dm.shape[0] == np.asarray(kpts).reshape(-1, 3).shape[0]:
+        return v[0]
+    return v
+
+
+def _band_aos(df_obj, kb):
+    """AOs at the interpolation points for band k-points (device (nkb, nip, nao)), cached."""
+    st = df_obj._dev_state
+    cache = st.setdefault("band_aos", {})
+    key = kb.round(12).tobytes()
+    if key not in cache:
+        from .ao import eval_ao_band_gpu
+        pts = df_obj.cell.gen_uniform_grids(df_obj.m0)[df_obj.perm]
+        cache[key] = eval_ao_band_gpu(df_obj.device, df_obj.cell, pts, kb)
+    return cache[key]
+
+
+def _get_j_dev(df_obj, ddms, band=None):
+    """vj on the device (fftisdf.py:150-166) for device dms (nset, nk, nao, nao); band: J at
+    those k-points instead (nset, nband, nao, nao)."""
     st = df_obj._dev_state
     assert st is not None and "W0" in st, "call build() first"
     d = df_obj.device
     nset, nk, nao = ddms.shape[:3]
     nip = st["X"].shape[1]
-    vj = d.empty(ddms.shape)
     # sharded: each rank contracts its block of interpolation points, one all-reduce (:166)
     i0, i1 = d.shard(nip) if d.size > 1 else (0, nip)
-    d.ctx.call("fisdf_get_j_rows", _lib.ptr(st["X"]), _lib.ptr(st["W0"]), _lib.ptr(ddms), nset,
-               nk, nip, nao, i0, i1, _lib.ptr(vj))
+    if band is None:
+        vj = d.empty(ddms.shape)
+        d.ctx.call("fisdf_get_j_rows", _lib.ptr(st["X"]), _lib.ptr(st["W0"]), _lib.ptr(ddms),
+                   nset, nk, nip, nao, i0, i1, _lib.ptr(vj))
+    else:
+        Xb = _band_aos(df_obj, band)
+        vj = d.empty((nset, len(band), nao, nao))
+        d.ctx.call("fisdf_get_j_band_rows", _lib.ptr(st["X"]), _lib.ptr(st["W0"]),
+                   _lib.ptr(ddms), nset, nk, nip, nao, _lib.ptr(Xb), len(band), i0, i1,
+                   _lib.ptr(vj))
     if d.size > 1:  # the library runs on torch's current stream: the all-reduce is ordered
         kshard.allreduce_sum(vj, d.comm)
     return vj
@@ -633,18 +682,30 @@ def _finish_j(vj, dm_kpts, kpts, kpts_band):
     band = np.asarray(kpts if kpts_band is None else kpts_band)
     if abs(band).max() < 1e-9:                                           # :169-170
         out = out.real
-    return _format_jks(out, dm_kpts)
+    return _format_band(out, dm_kpts, kpts_band, kpts)
 
 
 def get_k_kpts(df_obj, dm_kpts, hermi=1, kpts=np.zeros((1, 3)), kpts_band=None, exxdiv=None):
-    """fftisdf.py:173-228 (+ exxdiv='ewald', next-4)."""
+    """fftisdf.py:173-228 (+ exxdiv='ewald' and kpts_band on the k-mesh, next-4)."""
     assert exxdiv in (None, "ewald")
     dms, ddms = _dms_to_dev(df_obj, dm_kpts)
-    return _format_jks(_get_k_dev(df_obj, ddms, exxdiv).cpu().numpy(), dm_kpts)
+    band = _band_of(df_obj, np.asarray(kpts), kpts_band)
+    return _format_band(_get_k_dev(df_obj, ddms, exxdiv, band).cpu().numpy(), dm_kpts, kpts_band,
+                        kpts)
 
 
-def _get_k_dev(df_obj, ddms, exxdiv=None):
-    """vk on the device (fftisdf.py:204-225) for device dms (nset, nk, nao, nao)."""
+def _get_k_dev(df_obj, ddms, exxdiv=None, band=None):
+    """vk on the device (fftisdf.py:204-225) for device dms (nset, nk, nao, nao).  band: K at
+    band k-points ON the k-mesh (rows of the k-mesh K); a band k' off the mesh needs W_q at the
+    off-mesh q = k' - k, which the k-mesh fit does not produce (NotImplementedError)."""
+    if band is not None:
+        try:
+            kidx, _ = df_obj._kidx(band)
+        except ValueError:
+            raise NotImplementedError("K at band k-points off the ISDF k-mesh (W_q exists only "
+                                      "for q on the mesh)") from None
+        vk = _get_k_dev(df_obj, ddms, exxdiv)
+        return vk[:, df_obj.device.torch.as_tensor(kidx.astype(np.int64), device=vk.device)]
     st = df_obj._dev_state
     assert st is not None and "Ws" in st, "call build() first"
     d = df_obj.device

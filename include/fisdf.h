@@ -76,6 +76,14 @@ int fisdf_eval_ao(fisdf_ctx* ctx, const void* d_coords, int ng, int natm, const 
                   const double* h_exps, const double* h_coefs, int nT, const int* h_tn,
                   const int kmesh[3], const double a[9], double rcut, int nao, void* d_out);
 
+/* Same Bloch AO values at nkb arbitrary (band) k-points h_kpts (nkb, 3), cartesian 1/bohr —
+ * the AOs at the interpolation points that get_jk(kpts_band=...) contracts.  d_out (nkb, ng, nao). */
+int fisdf_eval_ao_band(fisdf_ctx* ctx, const void* d_coords, int ng, int natm, const double* h_atoms,
+                       int nsh, const int* h_sh_atom, const int* h_sh_l, const int* h_sh_nprim,
+                       const double* h_exps, const double* h_coefs, int nT, const int* h_tn,
+                       int nkb, const double* h_kpts, const double a[9], double rcut, int nao,
+                       void* d_out);
+
 /* ---- A1: interpolation-point selection ------------------------------------
  * Replaces InterpolativeSeparableDensityFitting.select_interpolation_points
  * (fftisdf.py:357-388): x2 = sum_q Re(x0_q^* x0_q^T); x4 = x2*x2/nk; greedy pivoted
@@ -244,6 +252,13 @@ int fisdf_get_j_rows(fisdf_ctx* ctx, const void* d_X, const void* d_W0, const vo
 int fisdf_get_k_rows(fisdf_ctx* ctx, const void* d_X, const void* d_Ws, const void* d_dms,
                      int nset, int nip, int nao, const int kmesh[3], const double a[9], int i0,
                      int i1, void* d_vk);
+/* J at band k-points (get_jk kpts_band; the reference asserts nband == nkpt, fftisdf.py:164):
+ * rho and v = W0 rho from the k-mesh dms as fisdf_get_j, then J_k' = Xb_k'^H diag(v) Xb_k' with
+ * d_Xb (nkb, nip, nao) the AOs at the interpolation points for the band k-points (the q = 0 pair
+ * fit serves any k' on both sides).  d_vj (nset, nkb, nao, nao); rows [i0, i1) as above. */
+int fisdf_get_j_band_rows(fisdf_ctx* ctx, const void* d_X, const void* d_W0, const void* d_dms,
+                          int nset, int nk, int nip, int nao, const void* d_Xb, int nkb, int i0,
+                          int i1, void* d_vj);
 
 /* ---- ISDF 4-index integrals (get_eri / ao2mo surface) --------------------------
  * eri[i*n2+j][k*n4+l] = sum_IJ W_q[I,J] conj(A1[I,i]) A2[I,j] conj(A3[J,k]) A4[J,l] with

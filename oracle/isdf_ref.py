@@ -214,12 +214,15 @@ def build(xip, f_k, coord, a, kmesh, mesh, blksize=8000, progress=False, omega=N
     return dict(x=xip, w0=wq[0], wq=wq, ranks=ranks, x4=x4_k, y=y)
 
 
-def get_j_kpts(xk, w0, dms, kpts_band_is_zero=False):
-    """fftisdf.py:133-171.  dms: (nset, nk, nao, nao)."""
+def get_j_kpts(xk, w0, dms, kpts_band_is_zero=False, xband=None):
+    """fftisdf.py:133-171.  dms: (nset, nk, nao, nao).  xband (nband, nip, nao): the AOs at the
+    interpolation points for band k-points (kpts_band, which the reference asserts away at
+    :164): J there from the same v."""
     nset, nkpt, nao = dms.shape[:3]
     rho = np.einsum("kIm,kIn,xkmn->xI", xk, xk.conj(), dms, optimize=True) / nkpt  # :155-156
     v = np.einsum("IJ,xJ->xI", w0, rho, optimize=True)                            # :159
-    vj = np.einsum("kIm,kIn,xI->xkmn", xk.conj(), xk, v, optimize=True)           # :166
+    xo = xk if xband is None else xband
+    vj = np.einsum("kIm,kIn,xI->xkmn", xo.conj(), xo, v, optimize=True)           # :166
     if kpts_band_is_zero:                                                         # :169-170
         vj = vj.real
     return vj

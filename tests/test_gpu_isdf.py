@@ -155,6 +155,37 @@ def test_svd_fit(name):
     assert max(es) < JK_TOL and max(eg) < JK_TOL
 
 
+def test_kpts_band():
+    """get_jk(kpts_band=...) (next-4; the reference asserts nband == nkpt, fftisdf.py:164,196):
+    J at off-mesh band k-points vs the oracle's J from the same v with the band AOs at the
+    interpolation points; J and K at band k-points on the k-mesh are the matching rows of the
+    k-mesh result; K off the mesh raises NotImplementedError; a 1-D band k-point drops the band
+    axis ([pyscf] _format_jks)."""
+    from fisdf import cell as C
+    from oracle import isdf_ref as R
+    name = "toy333_fr"
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
+    df, o, dm = make_df(name)
+    df.build()
+    rng = np.random.default_rng(4)
+    kb = rng.uniform(-0.5, 0.5, (3, 3)) @ cell.reciprocal_vectors()
+    vj_b, vk_b = df.get_jk(dm, kpts_band=kb, with_k=False)
+    assert vk_b is None and vj_b.shape == (1, 3) + dm.shape[-2:]
+    xb = C.eval_ao_band(cell, cell.gen_uniform_grids(m0)[o["perm"]], kb)
+    ref = R.get_j_kpts(o["xip"], o["w0"], dm, xband=xb)
+    ej = abs(vj_b - ref).max()
+    print(f"{name} kpts_band off-mesh: |dJ| {ej:.2e} (max|J| {abs(ref).max():.2f})")
+    assert ej < JK_TOL
+    sel = [5, 0, 3]
+    vj2, vk2 = df.get_jk(dm, kpts_band=df.kpts[sel])
+    vj, vk = df.get_jk(dm)
+    assert abs(vj2 - vj[:, sel]).max() < 1e-12 and abs(vk2 - vk[:, sel]).max() < 1e-12
+    with pytest.raises(NotImplementedError):
+        df.get_jk(dm, kpts_band=kb, with_j=False)
+    vj1, _ = df.get_jk(dm, kpts_band=kb[1], with_k=False)
+    assert vj1.shape == (1,) + dm.shape[-2:] and abs(vj1[0] - ref[0, 1]).max() < JK_TOL
+
+
 def test_build_y_qlist():
     """fisdf_build_y_qs with a non-contiguous q-list writes y_q in list order."""
     from fisdf import _lib as L

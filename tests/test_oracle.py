@@ -213,3 +213,14 @@ def test_svd_solver_is_the_unique_solution_when_full_rank():
     zd, rd = R.svd_solve(Ad, yd)
     zp = np.linalg.pinv(Ad, rcond=1e-12) @ yd
     assert rd == 40 and abs(zd - zp).max() < 1e-9 * abs(zp).max()
+
+
+def test_eval_ao_band_matches_the_kmesh_evaluator():
+    """cell.eval_ao_band (Bloch AOs at arbitrary k, kpts_band) equals the image-folded k-mesh
+    evaluator at the mesh k-points."""
+    from fisdf import cell as C
+    cell = C.toy_cell(mesh=(8, 8, 8))
+    coords = cell.gen_uniform_grids((5, 5, 5))
+    a = C.eval_ao_kpts(cell, coords, (2, 2, 2))
+    b = C.eval_ao_band(cell, coords, C.make_kpts(cell, (2, 2, 2)))
+    assert abs(a - b).max() < 1e-13 * abs(a).max()
