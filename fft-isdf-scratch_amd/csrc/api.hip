@@ -38,6 +38,9 @@ struct fisdf_ctx {
   // per (mesh, lattice, k_q): device list of G with asymmetric Coulomb weight (asym_list)
   struct Asym { int* idx = nullptr; int n = 0; };
   std::map<std::vector<double>, Asym> asym_cache;
+  // per (mesh, k-mesh, lattice, q, omega): sqrt(coulG(k_q + G) vol / N^2) of the fit, computed
+  // once (the timed steps of a repeated build reuse them)
+  std::map<std::vector<double>, double*> wt_cache;
   int f_nk = 0, f_nip = 0, f_nb = 64;
   cplx* f_L = nullptr;      // (nk, nip, nip) raw left-looking factor (row order)
   cplx* f_Lp = nullptr;     // (nk, nip*nip) pivot-order factor, ld = rank_q
@@ -46,6 +49,8 @@ struct fisdf_ctx {
   cplx* f_Li = nullptr;     // (nk, nip, nip) L^{-1} (pivot order) = trsm_merged on the identity
   cplx* f_x4s = nullptr;    // (nk, nip, nip) staged x4_q of the factored slots
   int* f_fail_pinned = nullptr;  // unpivoted path: per-slot failure flags (host, pinned)
+  int* f_qr_pinned = nullptr;    // factored q-list + real flags (2 nk ints, pinned) and device copy
+  int* f_qr_dev = nullptr;
   double f_tol = 1e-14;
   bool f_check_fail = false, f_used_pivoted = false;
   int f_cap_nk = 0, f_cap_nip = 0;  // shape the factor buffers were allocated for
@@ -254,6 +259,10 @@ int free_factors(fisdf_ctx* c) {
   c->f_cod.clear();
   if (c->f_fail_pinned) FISDF_HIP(hipHostFree(c->f_fail_pinned));
   c->f_fail_pinned = nullptr;
+  if (c->f_qr_pinned) FISDF_HIP(hipHostFree(c->f_qr_pinned));
+  c->f_qr_pinned = nullptr;
+  if (c->f_qr_dev) FISDF_HIP(hipFree(c->f_qr_dev));
+  c->f_qr_dev = nullptr;
   if (c->f_piv) FISDF_HIP(hipFree(c->f_piv));
   if (c->f_rank_dev) FISDF_HIP(hipFree(c->f_rank_dev));
   if (c->f_rank_pinned) FISDF_HIP(hipHostFree(c->f_rank_pinned));
@@ -294,6 +303,30 @@ int select_gram(fisdf_ctx* c, const cplx* x0, int nk, int q0, int q1, int ng0, i
 bool self_conjugate(const int kmesh[3], int q) {
   const int i2 = q % kmesh[2], i1 = (q / kmesh[2]) % kmesh[1], i0 = q / (kmesh[1] * kmesh[2]);
   return (2 * i0) % kmesh[0] == 0 && (2 * i1) % kmesh[1] == 0 && (2 * i2) % kmesh[2] == 0;
+}
+
+// cached Coulomb weight of the fit for q (computed on `st` and waited for the first time, so
+// every stream may read it afterwards)
+int get_weight(fisdf_ctx* c, hipStream_t st, const int mesh[3], const int kmesh[3],
+               const double a[9], int q, double scale, const double* wt_scratch, const double** out) {
+  (void)wt_scratch;
+  std::vector<double> key = {(double)mesh[0], (double)mesh[1], (double)mesh[2], (double)kmesh[0],
+                             (double)kmesh[1], (double)kmesh[2], (double)q, c->omega, scale};
+  for (int i = 0; i < 9; ++i) key.push_back(a[i]);
+  auto it = c->wt_cache.find(key);
+  if (it == c->wt_cache.end()) {
+    CellGeom g;
+    lattice(a, g);
+    double kq[3];
+    kpoint(kmesh, g, q, kq);
+    double* w = nullptr;
+    FISDF_HIP(hipMalloc(&w, sizeof(double) * (size_t)mesh[0] * mesh[1] * mesh[2]));
+    FISDF_TRY(coulg_weight(st, mesh, g, kq, scale, 1, w, c->omega));
+    FISDF_HIP(hipStreamSynchronize(st));
+    it = c->wt_cache.emplace(key, w).first;
+  }
+  *out = it->second;
+  return 0;
 }
 
 // cached asym_list of a self-conjugate q (one synchronous count read the first time)
@@ -441,6 +474,7 @@ int fisdf_destroy(fisdf_ctx* c) {
   for (auto& e : c->events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto& kv : c->phase_cache) (void)hipFree(kv.second);
   for (auto& kv : c->asym_cache) (void)hipFree(kv.second.idx);
+  for (auto& kv : c->wt_cache) (void)hipFree(kv.second);
   if (c->f_pending) (void)hipEventSynchronize(c->ev_fac);
   free_factors(c);
   if (c->f_scratch) (void)hipFree(c->f_scratch);
@@ -1087,6 +1121,8 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   FISDF_HIP(hipMalloc(&c->f_rank_dev, sizeof(int) * nk));
   FISDF_HIP(hipHostMalloc((void**)&c->f_rank_pinned, sizeof(int) * nk, hipHostMallocDefault));
   FISDF_HIP(hipHostMalloc((void**)&c->f_fail_pinned, sizeof(int) * nk, hipHostMallocDefault));
+  FISDF_HIP(hipHostMalloc((void**)&c->f_qr_pinned, sizeof(int) * 2 * nk, hipHostMallocDefault));
+  FISDF_HIP(hipMalloc(&c->f_qr_dev, sizeof(int) * 2 * nk));
   }
   // scratch: pivoted pchol work, or the unpivoted path's rank/fail flags + block inverses
   Carver cv;
@@ -1119,21 +1155,24 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   FISDF_HIP(hipStreamWaitEvent(c->side, c->ev_x4, 0));
   StageTimer tm(c, FISDF_ST_FACTOR, c->side);
   hipStream_t s = c->side;
-  // stage the listed x4_q; self-conjugate q: x4_q = Phi[:,q]^H x4_s is real up to rounding
+  // stage the listed x4_q in one pass (self-conjugate q: x4_q = Phi[:,q]^H x4_s is real up to
+  // rounding); the unpivoted path factors its copy in f_L in place.  The pinned q-list is
+  // rewritten only here, after the previous factorisation was waited for (f_pending)
+  const bool pivoted = c->force_pivoted == 1 || (c->force_pivoted < 0 && pivoted_fit_forced()) ||
+                       c->fit_mode == FISDF_FIT_SVD;
   for (int i = 0; i < nq; ++i) {
-    FISDF_HIP(hipMemcpyAsync(c->f_x4s + i * nn, (const cplx*)x4all + (long)h_qs[i] * nn,
-                             sizeof(cplx) * nn, hipMemcpyDeviceToDevice, s));
-    if (c->f_real[i]) FISDF_TRY(zero_imag(s, c->f_x4s + i * nn, nn));
+    c->f_qr_pinned[i] = h_qs[i];
+    c->f_qr_pinned[nq + i] = c->f_real[i];
   }
-  if (c->force_pivoted == 1 || (c->force_pivoted < 0 && pivoted_fit_forced()) ||
-      c->fit_mode == FISDF_FIT_SVD) {
+  FISDF_HIP(hipMemcpyAsync(c->f_qr_dev, c->f_qr_pinned, sizeof(int) * 2 * nq, hipMemcpyHostToDevice, s));
+  FISDF_TRY(stage_x4(s, (const cplx*)x4all, c->f_qr_dev, nq, nn, c->f_x4s, pivoted ? nullptr : c->f_L));
+  if (pivoted) {
     FISDF_TRY(factor_pivoted(c, s));
     c->f_check_fail = false;
   } else {
     // full-rank fast path: unpivoted blocked Cholesky (all pivots > tol_rel * max diag is the
     // same full-rank verdict the rank-revealing pivoted factorisation gives); any matrix that
     // fails it is redone by the pivoted pchol in fisdf_factor_x4_wait
-    FISDF_HIP(hipMemcpyAsync(c->f_L, c->f_x4s, sizeof(cplx) * nk * nn, hipMemcpyDeviceToDevice, s));
     FISDF_TRY(chol_unpivoted(s, c->f_L, nip, nk, tol_rel, c->f_piv, (int*)(b + oU),
                              (int*)(b + oFl), (cplx*)(b + oWk)));
     FISDF_HIP(hipMemcpyAsync(c->f_fail_pinned, b + oFl, sizeof(int) * nk, hipMemcpyDeviceToHost, s));
@@ -1393,20 +1432,18 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   if (ready) NL = std::min(NL, 3);
   int D = pipe ? std::min(nq, c->pipe_depth > 0 ? c->pipe_depth : env_pipe_depth(NL)) : 0;
   Carver cv;
-  size_t oY[4], oU[4], oWt[4], oK[4], oTc[4];
-  size_t oYall = 0, oWall = 0;
+  size_t oY[4], oU[4], oK[4], oTc[4];
+  size_t oYall = 0;
   auto carve = [&]() {
     cv = Carver();
     for (int l = 0; l < NL; ++l) {
       if (!pipe) oY[l] = cv.take(sizeof(cplx) * rfmax * ngrid);
       oU[l] = cv.take(sizeof(cplx) * rmax * ngrid);
-      if (!pipe) oWt[l] = cv.take(sizeof(double) * ngrid);
       oK[l] = cv.take(sizeof(cplx) * (size_t)ks * rmax * rmax);
       oTc[l] = cv.take(sizeof(cplx) * rr);
     }
     if (pipe) {
       oYall = cv.take(sizeof(cplx) * (size_t)D * rfmax * ngrid);
-      oWall = cv.take(sizeof(double) * (size_t)D * ngrid);
     }
   };
   carve();
@@ -1490,28 +1527,32 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     FISDF_HIP(hipMemsetAsync(G, 0, sizeof(cplx) * nq * rr, c->stream));
   }
   // Yhat_q = FFT(y_q[:, piv] * f_q) * w_q   (:99, :113-115, :118; rows in pivot order)
-  auto fft_q = [&](hipStream_t st, int lq, cplx* Yh, double* wt) -> int {
+  // sqrt(coulG(k_q+G) vol/N^2)  (:114-115 and the Parseval 1/N of :118), cached per q
+  const double wscale = vol / ((double)ngrid * ngrid);
+  auto weight_q = [&](hipStream_t st, int lq, const double** w) {
+    return get_weight(c, st, mesh, kmesh, a, h_qs[lq], wscale, nullptr, w);
+  };
+  auto fft_q = [&](hipStream_t st, int lq, cplx* Yh) -> int {
     const int sl = s0 + lq;
     const int r = cod_of(sl) ? nip : c->f_rank[sl];
     double kq[3], kd[3];
     kpoint(kmesh, g, h_qs[lq], kq);
     for (int i = 0; i < 3; ++i) kd[i] = g.a[i][0] * kq[0] + g.a[i][1] * kq[1] + g.a[i][2] * kq[2];
+    const double* wt = nullptr;
+    FISDF_TRY(weight_q(st, lq, &wt));
     StageTimer tm(c, FISDF_ST_FFT, st);
-    // sqrt(coulG(k_q+G) vol/N^2)  (:114-115 and the Parseval 1/N of :118)
-    FISDF_TRY(coulg_weight(st, mesh, g, kq, vol / ((double)ngrid * ngrid), 1, wt, c->omega));
     FISDF_TRY(fft3d(st, yT + (long)lq * nip * ngrid, ngrid, c->f_piv + (long)sl * nip, Yh, ngrid,
                     r, mesh[0], mesh[1], mesh[2], kd, wt, nullptr));
     return 0;
   };
   // ring slot of q lq (pipelined mode)
   auto slot_y = [&](int lq) { return (cplx*)(b + oYall) + (long)(lq % D) * rfmax * ngrid; };
-  auto slot_w = [&](int lq) { return (double*)(b + oWall) + (long)(lq % D) * ngrid; };
   // FFT of q lq into its ring slot, after the lane that read the slot's previous q is done
   auto enqueue_fft = [&](int lq) -> int {
     if (lq >= nq || c->f_rank[s0 + lq] == 0) return 0;
     if (lq >= D) FISDF_HIP(hipStreamWaitEvent(fst, c->ev_free[lq % D], 0));
     if (ready) FISDF_HIP(hipStreamWaitEvent(fst, c->ev_ready[lq], 0));
-    FISDF_TRY(fft_q(fst, lq, slot_y(lq), slot_w(lq)));
+    FISDF_TRY(fft_q(fst, lq, slot_y(lq)));
     FISDF_HIP(hipEventRecord(c->ev_q[lq], fst));
     return 0;
   };
@@ -1522,7 +1563,6 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     hipStream_t st = lane_st[ln];
     cplx* Yh = pipe ? slot_y(lq) : (cplx*)(b + oY[ln]);
     cplx* U = (cplx*)(b + oU[ln]);
-    double* wt = pipe ? slot_w(lq) : (double*)(b + oWt[ln]);
     cplx* kw = (cplx*)(b + oK[ln]);
     cplx* Tc = (cplx*)(b + oTc[ln]);
     const int q = h_qs[lq];
@@ -1541,7 +1581,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       FISDF_HIP(hipStreamWaitEvent(st, c->ev_q[lq], 0));
     } else {
       if (ready) FISDF_HIP(hipStreamWaitEvent(st, c->ev_ready[lq], 0));
-      FISDF_TRY(fft_q(st, lq, Yh, wt));
+      FISDF_TRY(fft_q(st, lq, Yh));
     }
     cplx* Uq = U;  // where L^{-1} Yh lands
     if (c->f_fac_unjoined) FISDF_HIP(hipStreamWaitEvent(st, c->ev_fac, 0));  // L^-1, Q, ...
@@ -1583,6 +1623,8 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       {
         // Im(G) = Im(sum over the weight-asymmetric G only): every other (G, G') pair cancels
         const fisdf_ctx::Asym* as = nullptr;
+        const double* wt = nullptr;
+        FISDF_TRY(weight_q(st, lq, &wt));
         FISDF_TRY(get_asym(c, st, mesh, kmesh, a, q, wt, &as));
         if (as->n > 0) {
           FISDF_TRY(gather_cols(st, Uq, ngrid, r, as->idx, as->n, scratch));

@@ -71,6 +71,10 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha,
 int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cplx* C, long ldc,
          int ksplit = 1, cplx* work = nullptr, int mode = GEMM_FULL);
 
+// C[b] = alpha A[b] A[b]^H + beta C[b] (lower tiles + mirror), batched, no split-K
+int herk_batched(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, long sA,
+                 double beta, cplx* C, long ldc, long sC, int batch);
+
 // batched pivoted Cholesky of Hermitian PSD matrices (fftisdf.py:381-382, A4 factorisation)
 int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int rmax,
           double tol_rel, double tol_abs, cplx* L /*batch, n, rmax*/, int* piv /*batch, rmax*/,

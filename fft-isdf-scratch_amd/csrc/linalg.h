@@ -27,6 +27,8 @@ int gather_cols(hipStream_t s, const cplx* A, long ld, int r, const int* idx, in
 int add_imag(hipStream_t s, cplx* G, int ldg, const cplx* H, int ldh, int n);
 // zero the imaginary parts of n complex elements
 int zero_imag(hipStream_t s, cplx* a, long n);
+// x4s[i] = x4all[qr[i]] (imag zeroed where qr[nq + i] != 0), also into L if not null
+int stage_x4(hipStream_t s, const cplx* x4all, const int* qr, int nq, long nn, cplx* x4s, cplx* L);
 // Minimum-norm operator of a rank-deficient x4_q from its rank-revealing pivoted Cholesky
 // x4[P,P] ~ L L^H (L: rows of f_L, row order; piv: the pivot order; r = rank): A = P L (n x r),
 // thin QR A = Q R by shifted CholeskyQR3, M = A^+ = R^{-1} Q^H (r x n, ld ldm; columns in pivot

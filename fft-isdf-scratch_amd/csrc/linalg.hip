@@ -756,6 +756,30 @@ int zero_imag(hipStream_t s, cplx* a, long n) {
   return 0;
 }
 
+// factor staging: x4s[i] = x4all[qs[i]] (imaginary part zeroed for a self-conjugate q, whose
+// x4_q is real up to rounding) and, if L is given, the same into L (the in-place Cholesky's
+// input) — one pass instead of a copy per q plus a bulk copy
+__global__ void stage_x4_kernel(const cplx* __restrict__ x4all, const int* __restrict__ qr, int nq,
+                                long nn, cplx* __restrict__ x4s, cplx* __restrict__ L) {
+  const int i = blockIdx.y;
+  const long q = qr[i];
+  const bool re = qr[nq + i] != 0;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nn; e += (long)gridDim.x * blockDim.x) {
+    cplx v = x4all[q * nn + e];
+    if (re) v.y = 0.0;
+    x4s[(long)i * nn + e] = v;
+    if (L) L[(long)i * nn + e] = v;
+  }
+}
+
+int stage_x4(hipStream_t s, const cplx* x4all, const int* qr, int nq, long nn, cplx* x4s, cplx* L) {
+  if (nq == 0 || nn == 0) return 0;
+  hipLaunchKernelGGL(stage_x4_kernel, dim3(nblocks(nn, 256, 512), nq), dim3(256), 0, s, x4all, qr, nq,
+                     nn, x4s, L);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
 // ---- minimum-norm (complete orthogonal) operator of a rank-deficient x4_q ----------------
 namespace {
 

@@ -701,6 +701,13 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(cplx* __restrict__ W, in
   const int b = blockIdx.x;
   W += b * sW;
   Linv += (long)b * 4096;
+  // the diagonal blocks are the serial chain of the factorisation, which runs beside the y
+  // build's throughput kernels on the same CUs: raise the wave priority so the SIMD arbiter
+  // issues this chain's instructions first
+#ifndef FISDF_DIAG_PRIO
+#define FISDF_DIAG_PRIO 3
+#endif
+  __builtin_amdgcn_s_setprio(FISDF_DIAG_PRIO);
   __shared__ cplx A[64][65];
   __shared__ cplx X[64][65];
   __shared__ int bad;
@@ -827,7 +834,7 @@ int chol_unpivoted(hipStream_t s, cplx* W, int n, int batch, double tol_rel, int
   double* thr = (double*)(work + (long)batch * 4096);
   hipLaunchKernelGGL(diag_max_kernel, dim3(batch), dim3(256), 0, s, W, n, nn, tol_rel, thr, fail);
   FISDF_HIP(hipGetLastError());
-  const cplx one = cmk(1, 0), mone = cmk(-1, 0), zero = cmk(0, 0);
+  const cplx one = cmk(1, 0), zero = cmk(0, 0);
   for (int b0 = 0; b0 < n; b0 += 64) {
     const int m = std::min(64, n - b0), b1 = b0 + m;
     hipLaunchKernelGGL(chol_diag_kernel, dim3(batch), dim3(256), 0, s, W, n, nn, b0, m, thr, fail,
@@ -837,9 +844,9 @@ int chol_unpivoted(hipStream_t s, cplx* W, int n, int batch, double tol_rel, int
       // panel: W[b1:, b0:b1] <- W[b1:, b0:b1] L_bb^{-H}  (in place: one N tile, rows per WG)
       FISDF_TRY(zgemm(s, OP_N, OP_C, n - b1, m, m, one, W + (long)b1 * n + b0, n, nn, Linv, 64,
                       4096, zero, W + (long)b1 * n + b0, n, nn, batch));
-      // trailing: W[b1:, b1:] -= P P^H
-      FISDF_TRY(zgemm(s, OP_N, OP_C, n - b1, n - b1, m, mone, W + (long)b1 * n + b0, n, nn,
-                      W + (long)b1 * n + b0, n, nn, one, W + (long)b1 * n + b1, n, nn, batch));
+      // trailing: W[b1:, b1:] -= P P^H (Hermitian: lower tiles + mirror)
+      FISDF_TRY(herk_batched(s, n - b1, m, -1.0, W + (long)b1 * n + b0, n, nn, 1.0,
+                             W + (long)b1 * n + b1, n, nn, batch));
     }
   }
   hipLaunchKernelGGL(chol_finish_kernel, dim3(batch), dim3(256), 0, s, n, piv, rank, fail);

@@ -89,11 +89,10 @@ __device__ __forceinline__ void zgemm_epilogue(int M, int N, cplx alpha, cplx be
         for (int r = 0; r < 4; ++r) {
           int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
           int col = n0 + wn + ni * 16 + (lane & 15);
-          const bool mirror = HERK && (m0 + wm + mi * 16 > n0 + wn + ni * 16);
-          if (((mask >> (mi * 2 + ni)) & 1) && row < M && col < N) {
+          // HERK partials keep only the computed (lower) 16x16 blocks: herk_reduce_kernel
+          // writes their conjugate mirrors once, after the sum
+          if (((mask >> (mi * 2 + ni)) & 1) && row < M && col < N)
             Wp[(long)row * N + col] = cmk(accR[mi][ni][r], accI[mi][ni][r]);
-            if (mirror) Wp[(long)col * N + row] = cmk(accR[mi][ni][r], -accI[mi][ni][r]);
-          }
         }
     return;
   }
@@ -327,6 +326,9 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
   A += (long)bz * sA;
   B += (long)bz * sB;
   int ti = t % nMt, tj = t / nMt;
+  // GEMM_A_LOWER: M-tile i runs K = 64 (i + 1); the longest tiles of each N-panel go first so
+  // the short ones fill the end of the launch (longest-processing-time order)
+  if constexpr ((MODE & GEMM_A_LOWER) != 0) ti = nMt - 1 - ti;
   if (HERK) {
     ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
     while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
@@ -395,6 +397,9 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
                  : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
   };
   auto issue = [&](int st) {  // K-step st -> ring slot st % NS
+#ifdef FISDF_NOLOAD
+    if (st >= NS - 1) return;  // experiment: MFMA/LDS ceiling without global traffic
+#endif
     const int buf = st % NS;
     const int k0 = kbeg + st * BK;
     const unsigned la = lds0 + (unsigned)((buf * 2 + 0) * TILE) * 16u;
@@ -504,19 +509,19 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
           for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni)
-              if ((MASK >> (mi * 2 + ni)) & 1)
+              if (((MASK >> (mi * 2 + ni)) & 1) )
                 accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], accR[mi][ni], 0, 0, 0);
 #pragma unroll
           for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni)
-              if ((MASK >> (mi * 2 + ni)) & 1)
+              if (((MASK >> (mi * 2 + ni)) & 1) )
                 accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], bi[ni], accI[mi][ni], 0, 0, 0);
 #pragma unroll
           for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni)
-              if ((MASK >> (mi * 2 + ni)) & 1)
+              if (((MASK >> (mi * 2 + ni)) & 1) )
                 acc3[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(as[mi], bs[ni], acc3[mi][ni], 0, 0, 0);
           continue;
         }
@@ -524,14 +529,14 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
           for (int ni = 0; ni < 2; ++ni)
-            if ((MASK >> (mi * 2 + ni)) & 1)
+            if (((MASK >> (mi * 2 + ni)) & 1) )
               accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], accR[mi][ni], 0, 0, 0);
         if constexpr (!REONLY) {
 #pragma unroll
           for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni)
-              if ((MASK >> (mi * 2 + ni)) & 1)
+              if (((MASK >> (mi * 2 + ni)) & 1) )
                 accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], bi[ni], accI[mi][ni], 0, 0, 0);
         }
         if constexpr (!AREAL) {
@@ -539,7 +544,7 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
           for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni)
-              if ((MASK >> (mi * 2 + ni)) & 1)
+              if (((MASK >> (mi * 2 + ni)) & 1) )
                 accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[mi], bi[ni], accR[mi][ni], 0, 0, 0);
         }
         if constexpr (!AREAL && !REONLY) {
@@ -547,7 +552,7 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
           for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni)
-              if ((MASK >> (mi * 2 + ni)) & 1)
+              if (((MASK >> (mi * 2 + ni)) & 1) )
                 accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], br[ni], accI[mi][ni], 0, 0, 0);
         }
       }
@@ -593,6 +598,38 @@ __global__ void ksplit_reduce(int M, int N, int ksplit, const cplx* __restrict__
     cplx v = cmul(alpha, acc);
     if (beta.x != 0.0 || beta.y != 0.0) v = cadd(v, cmul(beta, *cp));
     *cp = v;
+  }
+}
+
+// HERK split-K reduction: C = alpha sum_s work[s] over the lower 16x16 blocks the HERK kernel
+// computed (the partials hold nothing else), and C[c][r] = conj(C[r][c]) for the strictly-lower
+// blocks — one 32x32 tile of the lower triangle per workgroup, the mirror through LDS so both
+// the partial reads and the C writes stay coalesced
+__global__ __launch_bounds__(256) void herk_reduce_kernel(int n, int ksplit,
+                                                          const cplx* __restrict__ work, double alpha,
+                                                          cplx* __restrict__ C, long ldc) {
+  __shared__ cplx tile[32][33];
+  int t = blockIdx.x, ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+  while (ti * (ti + 1) / 2 > t) --ti;
+  const int tj = t - ti * (ti + 1) / 2;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const long nn = (long)n * n;
+  for (int rr = ty; rr < 32; rr += 8) {
+    const int r = ti * 32 + rr, c = tj * 32 + tx;
+    cplx acc = cmk(0, 0);
+    const bool valid = r < n && c < n && (r >> 4) >= (c >> 4);
+    if (valid) {
+      for (int s = 0; s < ksplit; ++s) acc = cadd(acc, work[s * nn + (long)r * n + c]);
+      acc = cscale(acc, alpha);
+      C[(long)r * ldc + c] = acc;
+    }
+    tile[rr][tx] = acc;
+  }
+  __syncthreads();
+  for (int rr = ty; rr < 32; rr += 8) {  // C[tj*32 + rr][ti*32 + tx] = conj(C[ti*32 + tx][tj*32 + rr])
+    const int sr = ti * 32 + tx, sc = tj * 32 + rr;
+    if (sr < n && sc < n && (sr >> 4) > (sc >> 4)) C[(long)sc * ldc + sr] = cconj(tile[tx][rr]);
   }
 }
 
@@ -707,12 +744,27 @@ int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cpl
                              ldc, 0, ksplit, kchunk, work, EPI_NONE, nullptr);
   FISDF_HIP(hipGetLastError());
   if (ksplit > 1) {
-    long MN = (long)n * n;
-    int blocks = (int)std::min<long>((MN + 255) / 256, 4096);
-    hipLaunchKernelGGL(ksplit_reduce, dim3(blocks, 1), dim3(256), 0, s, n, n, ksplit, work,
-                       cmk(alpha, 0), cmk(0, 0), C, ldc, 0L);
+    const int t32 = (n + 31) / 32;
+    hipLaunchKernelGGL(herk_reduce_kernel, dim3(t32 * (t32 + 1) / 2), dim3(256), 0, s, n, ksplit,
+                       work, alpha, C, ldc);
     FISDF_HIP(hipGetLastError());
   }
+  return 0;
+}
+
+// C[b] = alpha A[b] A[b]^H + beta C[b] for a batch (A: n x K, lda, batch stride sA; C: n x n,
+// ldc, stride sC): lower tiles computed, upper mirrored — the blocked Cholesky's trailing
+// update (beta = 1, alpha = -1) at half the tiles of the full GEMM
+int herk_batched(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, long sA,
+                 double beta, cplx* C, long ldc, long sC, int batch) {
+  FISDF_CHECK(n >= 0 && K >= 0 && batch >= 0, "herk_batched: negative size");
+  if (n == 0 || batch == 0) return 0;
+  const int kchunk = std::max(BK, ((K + BK - 1) / BK) * BK);
+  const int nt = (n + BM - 1) / BM;
+  dim3 grid(nt * (nt + 1) / 2, 1, batch);
+  launch<OP_N, OP_C, true>(s, grid, n, n, K, cmk(alpha, 0), A, lda, sA, A, lda, sA, cmk(beta, 0), C,
+                           ldc, sC, 1, kchunk, nullptr, EPI_NONE, nullptr);
+  FISDF_HIP(hipGetLastError());
   return 0;
 }
 
