@@ -379,6 +379,13 @@ int env_pipe_depth(int lanes) {
   return v > 0 ? v : lanes + 2;
 }
 
+int num_cus(int device) {
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0)
+    n = 256;
+  return n;
+}
+
 int ensure_aux(fisdf_ctx* c) {
   if (c->ev_fork) return 0;
   FISDF_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
@@ -427,12 +434,6 @@ int pick_ksplit_herk(int n, int K, int ncu) {
   return best;
 }
 
-int num_cus(int device) {
-  int n = 0;
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0)
-    n = 256;
-  return n;
-}
 
 int pick_ksplit(int M, int N, int K) {
   long tiles = (long)((M + 63) / 64) * ((N + 63) / 64);
