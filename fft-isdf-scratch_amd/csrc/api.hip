@@ -36,8 +36,11 @@ struct fisdf_ctx {
   std::vector<int> f_qs;  // the factored q (ascending), slot i <-> q = f_qs[i]
   std::vector<char> f_real;  // slot factored as real (self-conjugate q, kmesh given)
   // per (mesh, lattice, k_q): device list of G with asymmetric Coulomb weight (asym_list)
-  struct Asym { int* idx = nullptr; int n = 0; };
+  struct Asym { int* idx = nullptr; int n = 0; double* f = nullptr; };
   std::map<std::vector<double>, Asym> asym_cache;
+  // fisdf_set_half_grid: a self-conjugate q is fitted on half the G (its Hermitian pairs), -1:
+  // environment FISDF_HALF_G (default on)
+  int half_grid = -1;
   // per (mesh, k-mesh, lattice, q, omega): sqrt(coulG(k_q + G) vol / N^2) of the fit, computed
   // once (the timed steps of a repeated build reuse them)
   std::map<std::vector<double>, double*> wt_cache;
@@ -307,11 +310,21 @@ bool self_conjugate(const int kmesh[3], int q) {
 
 // cached Coulomb weight of the fit for q (computed on `st` and waited for the first time, so
 // every stream may read it afterwards)
+// the reciprocal-lattice vector m.b = 2 k_q of a self-conjugate q
+void self_conjugate_m(const int kmesh[3], int q, int m[3]) {
+  const int i2 = q % kmesh[2], i1 = (q / kmesh[2]) % kmesh[1], i0 = q / (kmesh[1] * kmesh[2]);
+  m[0] = 2 * i0 / kmesh[0];
+  m[1] = 2 * i1 / kmesh[1];
+  m[2] = 2 * i2 / kmesh[2];
+}
+
+// half: the self-conjugate q's half-grid weight sqrt(c_G + c_G') (sqrt(c_G) on a self-paired
+// plane, 0 beyond the prefix planes), see linalg.h half_weight
 int get_weight(fisdf_ctx* c, hipStream_t st, const int mesh[3], const int kmesh[3],
-               const double a[9], int q, double scale, const double* wt_scratch, const double** out) {
-  (void)wt_scratch;
+               const double a[9], int q, double scale, bool half, const double** out) {
   std::vector<double> key = {(double)mesh[0], (double)mesh[1], (double)mesh[2], (double)kmesh[0],
-                             (double)kmesh[1], (double)kmesh[2], (double)q, c->omega, scale};
+                             (double)kmesh[1], (double)kmesh[2], (double)q, c->omega, scale,
+                             half ? 1.0 : 0.0};
   for (int i = 0; i < 9; ++i) key.push_back(a[i]);
   auto it = c->wt_cache.find(key);
   if (it == c->wt_cache.end()) {
@@ -319,13 +332,55 @@ int get_weight(fisdf_ctx* c, hipStream_t st, const int mesh[3], const int kmesh[
     lattice(a, g);
     double kq[3];
     kpoint(kmesh, g, q, kq);
+    const size_t ng = (size_t)mesh[0] * mesh[1] * mesh[2];
     double* w = nullptr;
-    FISDF_HIP(hipMalloc(&w, sizeof(double) * (size_t)mesh[0] * mesh[1] * mesh[2]));
-    FISDF_TRY(coulg_weight(st, mesh, g, kq, scale, 1, w, c->omega));
+    FISDF_HIP(hipMalloc(&w, sizeof(double) * ng));
+    if (!half) {
+      FISDF_TRY(coulg_weight(st, mesh, g, kq, scale, 1, w, c->omega));
+    } else {
+      double* cw = nullptr;
+      FISDF_HIP(hipMallocAsync((void**)&cw, sizeof(double) * ng, st));
+      FISDF_TRY(coulg_weight(st, mesh, g, kq, scale, 0, cw, c->omega));
+      int m[3];
+      self_conjugate_m(kmesh, q, m);
+      FISDF_TRY(half_weight(st, w, cw, mesh, m));
+      FISDF_HIP(hipFreeAsync(cw, st));
+    }
     FISDF_HIP(hipStreamSynchronize(st));
     it = c->wt_cache.emplace(key, w).first;
   }
   *out = it->second;
+  return 0;
+}
+
+// the half-grid asymmetric-weight list of a self-conjugate q with its Im factors (cached)
+int get_asym_half(fisdf_ctx* c, hipStream_t st, const int mesh[3], const int kmesh[3],
+                  const double a[9], int q, double scale, const fisdf_ctx::Asym** out) {
+  std::vector<double> key = {(double)mesh[0], (double)mesh[1], (double)mesh[2], (double)kmesh[0],
+                             (double)kmesh[1], (double)kmesh[2], (double)q, c->omega, scale, 1.0};
+  for (int i = 0; i < 9; ++i) key.push_back(a[i]);
+  auto it = c->asym_cache.find(key);
+  if (it == c->asym_cache.end()) {
+    CellGeom g;
+    lattice(a, g);
+    double kq[3];
+    kpoint(kmesh, g, q, kq);
+    const long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
+    fisdf_ctx::Asym as;
+    double* cw = nullptr;
+    FISDF_HIP(hipMalloc(&as.idx, sizeof(int) * (ngrid + 1)));
+    FISDF_HIP(hipMalloc(&as.f, sizeof(double) * ngrid));
+    FISDF_HIP(hipMallocAsync((void**)&cw, sizeof(double) * ngrid, st));
+    FISDF_TRY(coulg_weight(st, mesh, g, kq, scale, 0, cw, c->omega));
+    int m[3];
+    self_conjugate_m(kmesh, q, m);
+    FISDF_TRY(asym_half(st, cw, mesh, m, as.idx, as.f, as.idx + ngrid));
+    FISDF_HIP(hipFreeAsync(cw, st));
+    FISDF_HIP(hipMemcpyAsync(&as.n, as.idx + ngrid, sizeof(int), hipMemcpyDeviceToHost, st));
+    FISDF_HIP(hipStreamSynchronize(st));
+    it = c->asym_cache.emplace(key, as).first;
+  }
+  *out = &it->second;
   return 0;
 }
 
@@ -474,7 +529,10 @@ int fisdf_destroy(fisdf_ctx* c) {
   FISDF_HIP(hipStreamSynchronize(c->stream));
   for (auto& e : c->events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto& kv : c->phase_cache) (void)hipFree(kv.second);
-  for (auto& kv : c->asym_cache) (void)hipFree(kv.second.idx);
+  for (auto& kv : c->asym_cache) {
+    (void)hipFree(kv.second.idx);
+    if (kv.second.f) (void)hipFree(kv.second.f);
+  }
   for (auto& kv : c->wt_cache) (void)hipFree(kv.second);
   if (c->f_pending) (void)hipEventSynchronize(c->ev_fac);
   free_factors(c);
@@ -1191,6 +1249,12 @@ int fisdf_set_pivoted_fit(fisdf_ctx* c, int mode) {
   return 0;
 }
 
+int fisdf_set_half_grid(fisdf_ctx* c, int mode) {
+  FISDF_CHECK(c != nullptr && mode >= -1 && mode <= 1, "set_half_grid: mode must be -1, 0 or 1");
+  c->half_grid = mode;
+  return 0;
+}
+
 int fisdf_set_fit_mode(fisdf_ctx* c, int mode) {
   FISDF_CHECK(c != nullptr && mode >= FISDF_FIT_LSTSQ && mode <= FISDF_FIT_BASIC,
               "set_fit_mode: mode must be FISDF_FIT_LSTSQ, FISDF_FIT_SVD or FISDF_FIT_BASIC");
@@ -1403,9 +1467,23 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   // split-K of each q's HERK from its own rank (not the call's largest), so a q's arithmetic
   // does not depend on which other q share the call (1-GPU vs sharded builds agree bitwise)
   const int ncu = num_cus(c->device);
-  auto ks_of = [&](int r) { return ks_env > 0 ? ks_env : pick_ksplit_herk(r, (int)ngrid, ncu); };
+  auto ks_of = [&](int r, long K) { return ks_env > 0 ? ks_env : pick_ksplit_herk(r, (int)K, ncu); };
   int ks = 1;
-  for (int lq = 0; lq < nq; ++lq) ks = std::max(ks, ks_of(c->f_rank[s0 + lq]));
+  for (int lq = 0; lq < nq; ++lq) ks = std::max(ks, ks_of(c->f_rank[s0 + lq], ngrid));
+  // a self-conjugate q is fitted on the prefix planes of its Hermitian G pairs (about half the
+  // grid): Re W = sum over one member of each pair with the pair's combined weight
+  static const int half_env = [] {
+    const char* e = getenv("FISDF_HALF_G");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  const bool half_on = (c->half_grid >= 0 ? c->half_grid : half_env) != 0;
+  auto half_of = [&](int sl) { return half_on && c->f_real[sl] != 0; };
+  auto ncols_of = [&](int lq) -> long {
+    if (!half_of(s0 + lq)) return ngrid;
+    int m[3];
+    self_conjugate_m(kmesh, h_qs[lq], m);
+    return (long)half_prefix_planes(mesh[0], m[0]) * mesh[1] * mesh[2];
+  };
   const long rr = (long)rmax * rmax;
   const long sLi = (long)nblk * nb * nb;
   // q are processed on NL "lanes" (the main stream and aux streams), each with its own
@@ -1531,7 +1609,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   // sqrt(coulG(k_q+G) vol/N^2)  (:114-115 and the Parseval 1/N of :118), cached per q
   const double wscale = vol / ((double)ngrid * ngrid);
   auto weight_q = [&](hipStream_t st, int lq, const double** w) {
-    return get_weight(c, st, mesh, kmesh, a, h_qs[lq], wscale, nullptr, w);
+    return get_weight(c, st, mesh, kmesh, a, h_qs[lq], wscale, half_of(s0 + lq), w);
   };
   auto fft_q = [&](hipStream_t st, int lq, cplx* Yh) -> int {
     const int sl = s0 + lq;
@@ -1585,6 +1663,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       FISDF_TRY(fft_q(st, lq, Yh));
     }
     cplx* Uq = U;  // where L^{-1} Yh lands
+    const long ncol = ncols_of(lq);  // grid columns fitted (half for a self-conjugate q)
     if (c->f_fac_unjoined) FISDF_HIP(hipStreamWaitEvent(st, c->ev_fac, 0));  // L^-1, Q, ...
     {
       StageTimer tm(c, FISDF_ST_TRSM, st);
@@ -1594,29 +1673,29 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
         return !(e && std::string(e) == "merged");
       }();
       if (cod_of(sl)) {  // U = A^+ Yh[P]: the minimum-norm operator over all nip rows
-        FISDF_TRY(zgemm(st, OP_N, OP_N, r, (int)ngrid, nip, ONE, c->f_M + (long)sl * nn, nip, 0, Yh,
+        FISDF_TRY(zgemm(st, OP_N, OP_N, r, (int)ncol, nip, ONE, c->f_M + (long)sl * nn, nip, 0, Yh,
                         ngrid, 0, ZERO, U, ngrid, 0, 1, 1, nullptr, EPI_NONE, nullptr,
                         real_q ? GEMM_A_REAL : GEMM_FULL));
         Uq = U;
       } else if (r == nip && tri_gemm) {  // one lower-triangular GEMM with L^{-1}
-        FISDF_TRY(zgemm(st, OP_N, OP_N, nip, (int)ngrid, nip, ONE, c->f_Li + (long)sl * nn, nip, 0,
+        FISDF_TRY(zgemm(st, OP_N, OP_N, nip, (int)ncol, nip, ONE, c->f_Li + (long)sl * nn, nip, 0,
                         Yh, ngrid, 0, ZERO, U, ngrid, 0, 1, 1, nullptr, EPI_NONE, nullptr,
                         GEMM_A_LOWER | (real_q ? GEMM_A_REAL : GEMM_FULL)));
         Uq = U;
       } else if (r == nip) {  // merged block-row substitution, in place
-        FISDF_TRY(trsm_merged(st, c->f_Q + (long)sl * nn, nip, Yh, ngrid, (int)ngrid,
+        FISDF_TRY(trsm_merged(st, c->f_Q + (long)sl * nn, nip, Yh, ngrid, (int)ncol,
                               real_q ? GEMM_A_REAL : GEMM_FULL));
         Uq = Yh;
       } else {
         FISDF_TRY(trsm_blocked(st, 1, Lp, nip, 0, r, Linv, 0, nb, Yh, ngrid, 0, U, ngrid,
-                               0, (int)ngrid, 1, real_q ? 1 : 0));
+                               0, (int)ncol, 1, real_q ? 1 : 0));
       }
     }
     cplx* scratch = Uq == U ? Yh : U;
     {
       StageTimer tm(c, FISDF_ST_HERK, st);
       // G = U U^H  (:121 by Parseval)
-      FISDF_TRY(herk(st, r, (int)ngrid, 1.0, Uq, ngrid, G + lq * rr, rmax, ks_of(r), kw,
+      FISDF_TRY(herk(st, r, (int)ncol, 1.0, Uq, ngrid, G + lq * rr, rmax, ks_of(r, ncol), kw,
                      real_q ? GEMM_RE_ONLY : GEMM_FULL));
     }
     if (real_q) {
@@ -1624,14 +1703,28 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       {
         // Im(G) = Im(sum over the weight-asymmetric G only): every other (G, G') pair cancels
         const fisdf_ctx::Asym* as = nullptr;
-        const double* wt = nullptr;
-        FISDF_TRY(weight_q(st, lq, &wt));
-        FISDF_TRY(get_asym(c, st, mesh, kmesh, a, q, wt, &as));
-        if (as->n > 0) {
-          FISDF_TRY(gather_cols(st, Uq, ngrid, r, as->idx, as->n, scratch));
-          FISDF_TRY(herk(st, r, as->n, 1.0, scratch, as->n, Tc, rmax,
-                         std::min(ks_of(r), std::max(1, as->n / 256)), kw));
-          FISDF_TRY(add_imag(st, G + lq * rr, rmax, Tc, rmax, r));
+        if (half_of(sl)) {
+          // half grid: one member of each asymmetric pair, Im W = Im(U_A diag(f) U_A^H)
+          FISDF_TRY(get_asym_half(c, st, mesh, kmesh, a, q, wscale, &as));
+          if (as->n > 0) {
+            cplx* plain = scratch;
+            cplx* scaled = scratch + (long)r * as->n;
+            FISDF_TRY(gather_cols_scaled(st, Uq, ngrid, r, as->idx, nullptr, as->n, plain));
+            FISDF_TRY(gather_cols_scaled(st, Uq, ngrid, r, as->idx, as->f, as->n, scaled));
+            FISDF_TRY(zgemm(st, OP_N, OP_C, r, r, as->n, ONE, scaled, as->n, 0, plain, as->n, 0, ZERO,
+                            Tc, rmax, 0, 1, std::min(ks_of(r, ncol), std::max(1, as->n / 256)), kw));
+            FISDF_TRY(add_imag(st, G + lq * rr, rmax, Tc, rmax, r));
+          }
+        } else {
+          const double* wt = nullptr;
+          FISDF_TRY(weight_q(st, lq, &wt));
+          FISDF_TRY(get_asym(c, st, mesh, kmesh, a, q, wt, &as));
+          if (as->n > 0) {
+            FISDF_TRY(gather_cols(st, Uq, ngrid, r, as->idx, as->n, scratch));
+            FISDF_TRY(herk(st, r, as->n, 1.0, scratch, as->n, Tc, rmax,
+                           std::min(ks_of(r, ncol), std::max(1, as->n / 256)), kw));
+            FISDF_TRY(add_imag(st, G + lq * rr, rmax, Tc, rmax, r));
+          }
         }
       }
     }

@@ -24,6 +24,16 @@ int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, long ldl, long sL, in
 int asym_list(hipStream_t s, const double* w, const int mesh[3], const int m[3], int* idx,
               int* count);
 int gather_cols(hipStream_t s, const cplx* A, long ld, int r, const int* idx, int n, cplx* out);
+// self-conjugate q on half the G: the prefix planes i0 < nH hold one member of every Hermitian
+// pair G' = -G - m.b (both members on a self-paired plane); half_weight: w = sqrt of the pair's
+// combined weight (c = coulG*scale, not rooted) on the prefix, 0 beyond; asym_half: the prefix G
+// of unequal pair weights with f = (c - c')/(c + c') (1 on a self-paired plane), ascending
+int half_prefix_planes(int n0, int m0);
+int half_weight(hipStream_t s, double* w, const double* c, const int mesh[3], const int m[3]);
+int asym_half(hipStream_t s, const double* c, const int mesh[3], const int m[3], int* idx,
+              double* f, int* count);
+int gather_cols_scaled(hipStream_t s, const cplx* A, long ld, int r, const int* idx,
+                       const double* f, int n, cplx* out);
 int add_imag(hipStream_t s, cplx* G, int ldg, const cplx* H, int ldh, int n);
 // zero the imaginary parts of n complex elements
 int zero_imag(hipStream_t s, cplx* a, long n);

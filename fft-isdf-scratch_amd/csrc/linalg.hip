@@ -700,6 +700,89 @@ __global__ __launch_bounds__(1024) void asym_list_kernel(const double* __restric
   if (threadIdx.x == 0) *count = base;
 }
 
+// ---- self-conjugate q on half the G (the Hermitian pairing Zhat(G') = conj(Zhat(G)),
+// G' = -G - m.b, of a real z_q): planes i0 of the prefix [0, nH) hold one member of every pair
+// (both members of a pair inside a self-paired plane i0 == (-i0 - m0) mod n0) -----------------
+__device__ __forceinline__ long partner_index(long e, int n0, int n1, int n2, int m0, int m1,
+                                              int m2, int* i0p, int* p0p) {
+  const int i2 = (int)(e % n2), i1 = (int)((e / n2) % n1), i0 = (int)(e / ((long)n1 * n2));
+  const int p0 = ((-i0 - m0) % n0 + n0) % n0, p1 = ((-i1 - m1) % n1 + n1) % n1,
+            p2 = ((-i2 - m2) % n2 + n2) % n2;
+  *i0p = i0;
+  *p0p = p0;
+  return ((long)p0 * n1 + p1) * n2 + p2;
+}
+
+// w[e] <- sqrt(c[e] + c[e']) on strict prefix planes, sqrt(c[e]) on a self-paired plane, 0 beyond
+// the prefix (c = coulG * scale, not square-rooted), in place
+__global__ void half_weight_kernel(double* __restrict__ w, const double* __restrict__ c, int n0,
+                                   int n1, int n2, int m0, int m1, int m2, int nH) {
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= (long)n0 * n1 * n2) return;
+  int i0, p0;
+  const long pe = partner_index(e, n0, n1, n2, m0, m1, m2, &i0, &p0);
+  double v = 0.0;
+  if (i0 < nH) v = (p0 == i0) ? c[e] : c[e] + c[pe];
+  w[e] = sqrt(v);
+}
+
+// one workgroup lists the prefix G whose pair has unequal weights (ascending) with the factor
+// f = (c - c') / (c + c') of Im(G) (strict planes; 1 on a self-paired plane, where both members
+// are listed), so Im W = Im(U_A diag(f) U_A^H) over the half-grid U
+__global__ __launch_bounds__(1024) void asym_half_kernel(const double* __restrict__ c, int n0,
+                                                         int n1, int n2, int m0, int m1, int m2,
+                                                         int nH, int* __restrict__ idx,
+                                                         double* __restrict__ f,
+                                                         int* __restrict__ count) {
+  __shared__ int base;
+  __shared__ int warp_tot[16];
+  const long nprefix = (long)nH * n1 * n2;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (long e0 = 0; e0 < nprefix; e0 += blockDim.x) {
+    const long e = e0 + threadIdx.x;
+    bool flag = false;
+    double fv = 1.0;
+    if (e < nprefix) {
+      int i0, p0;
+      const long pe = partner_index(e, n0, n1, n2, m0, m1, m2, &i0, &p0);
+      const double ce = c[e], cp = c[pe];
+      flag = fabs(ce - cp) > 1e-13 * fmax(fabs(ce), fabs(cp));
+      if (p0 != i0 && flag) fv = (ce - cp) / (ce + cp);
+    }
+    const unsigned long long bal = __ballot(flag);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) warp_tot[wv] = __popcll(bal);
+    __syncthreads();
+    int off = base;
+    for (int j = 0; j < wv; ++j) off += warp_tot[j];
+    if (flag) {
+      idx[off + before] = (int)e;
+      f[off + before] = fv;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int j = 0; j < (int)(blockDim.x >> 6); ++j) t += warp_tot[j];
+      base += t;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *count = base;
+}
+
+// out[i][j] = A[i][idx[j]] * (f ? f[j] : 1)
+__global__ void gather_cols_scaled_kernel(const cplx* __restrict__ A, long ld, int r,
+                                          const int* __restrict__ idx, const double* __restrict__ f,
+                                          int n, cplx* __restrict__ out) {
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= (long)r * n) return;
+  const int i = (int)(e / n), j = (int)(e % n);
+  const cplx v = A[(long)i * ld + idx[j]];
+  out[e] = f ? cscale(v, f[j]) : v;
+}
+
 // out[i][j] = A[i][idx[j]]  (r rows of ld, n listed columns)
 __global__ void gather_cols_kernel(const cplx* __restrict__ A, long ld, int r,
                                    const int* __restrict__ idx, int n, cplx* __restrict__ out) {
@@ -736,6 +819,39 @@ int gather_cols(hipStream_t s, const cplx* A, long ld, int r, const int* idx, in
   if (e == 0) return 0;
   hipLaunchKernelGGL(gather_cols_kernel, dim3(nblocks(e, 256, 1L << 30)), dim3(256), 0, s, A, ld,
                      r, idx, n, out);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int half_prefix_planes(int n0, int m0) {
+  int nH = 0;
+  for (int i0 = 0; i0 < n0; ++i0)
+    if (i0 <= ((-i0 - m0) % n0 + n0) % n0) nH = i0 + 1;
+  return nH;
+}
+
+int half_weight(hipStream_t s, double* w, const double* c, const int mesh[3], const int m[3]) {
+  const long n = (long)mesh[0] * mesh[1] * mesh[2];
+  hipLaunchKernelGGL(half_weight_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, w, c,
+                     mesh[0], mesh[1], mesh[2], m[0], m[1], m[2], half_prefix_planes(mesh[0], m[0]));
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int asym_half(hipStream_t s, const double* c, const int mesh[3], const int m[3], int* idx,
+              double* f, int* count) {
+  hipLaunchKernelGGL(asym_half_kernel, dim3(1), dim3(1024), 0, s, c, mesh[0], mesh[1], mesh[2],
+                     m[0], m[1], m[2], half_prefix_planes(mesh[0], m[0]), idx, f, count);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int gather_cols_scaled(hipStream_t s, const cplx* A, long ld, int r, const int* idx,
+                       const double* f, int n, cplx* out) {
+  const long e = (long)r * n;
+  if (e == 0) return 0;
+  hipLaunchKernelGGL(gather_cols_scaled_kernel, dim3(nblocks(e, 256, 1L << 30)), dim3(256), 0, s, A,
+                     ld, r, idx, f, n, out);
   FISDF_HIP(hipGetLastError());
   return 0;
 }

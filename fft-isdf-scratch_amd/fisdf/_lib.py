@@ -65,6 +65,7 @@ _SIGS = {
     "fisdf_set_pivoted_fit": ([_vp, _i], _i),
     "fisdf_factor_info": ([_vp, _ip], _i),
     "fisdf_set_fit_mode": ([_vp, _i], _i),
+    "fisdf_set_half_grid": ([_vp, _i], _i),
     "fisdf_min_norm_operator": ([_vp, _vp, _i, _d, _vp, _vp, _vp, _ip, _ip], _i),
     "fisdf_min_norm_info": ([_vp, _ip], _i),
     "fisdf_set_fit_lanes": ([_vp, _i], _i),

@@ -114,6 +114,9 @@ class InterpolativeSeparableDensityFitting:
     # q with 2 k_q in the reciprocal lattice (Gamma, all q of a 2x2x2 mesh): real x4_q and
     # W_q, fitted with real-factor / real-part GEMMs (half the MFMA work)
     real_self_conjugate = True
+    # a self-conjugate q fitted over one member of each Hermitian G pair (fisdf_set_half_grid;
+    # DESIGN §3.5): None = library default (FISDF_HALF_G, on), True / False force it
+    half_grid = None
     # x4_q factorisation: None = library default (unpivoted blocked Cholesky when every x4_q
     # is numerically full rank, else the greedy pivoted one); True forces the pivoted path
     pivoted_fit = None
@@ -503,6 +506,7 @@ def build(df_obj):
     if df_obj.fit not in modes:
         raise ValueError(f"ISDF.fit must be one of {sorted(modes)}, not {df_obj.fit!r}")
     d.ctx.call("fisdf_set_fit_mode", modes[df_obj.fit])
+    d.ctx.call("fisdf_set_half_grid", -1 if df_obj.half_grid is None else int(bool(df_obj.half_grid)))
     # the side stream starts from here (x4 built); the factor chain itself is enqueued after
     # the y build, since it reads ranks back to the host part-way (a blocking copy)
     if nq:

@@ -179,6 +179,11 @@ int fisdf_factor_info(fisdf_ctx* ctx, int* h_used_pivoted);
 #define FISDF_FIT_SVD 1
 #define FISDF_FIT_BASIC 2
 int fisdf_set_fit_mode(fisdf_ctx* ctx, int mode);
+/* A self-conjugate q (real z_q: Zhat(G') = conj(Zhat(G)), G' = -G - 2 k_q) is fitted on half the
+ * grid — one member of each pair G, G' with the pair's combined Coulomb weight, the asymmetric
+ * pairs' Im(W) from a signed-weight GEMM — so its TRSM and HERK run over ~N/2 columns.
+ * mode -1: environment FISDF_HALF_G (default on), 0 off (full grid), 1 on. */
+int fisdf_set_half_grid(fisdf_ctx* ctx, int mode);
 int fisdf_min_norm_info(fisdf_ctx* ctx, int* h_nslots);
 
 /* ---- A4+A5: fit + FFT Coulomb for the factored shard q in [q0, q1) (fftisdf.py:97-121)

@@ -186,6 +186,27 @@ def test_kpts_band():
     assert vj1.shape == (1,) + dm.shape[-2:] and abs(vj1[0] - ref[0, 1]).max() < JK_TOL
 
 
+@pytest.mark.parametrize("name", ["toy222", "toy331_fr", "diamond_szv_gamma", "si_small"])
+def test_half_grid_self_conjugate(name):
+    """Self-conjugate q fitted on half the G grid (ISDF.half_grid; the Hermitian pairs
+    G' = -G - 2 k_q of a real z_q, incl. odd meshes (toy331_fr: 15^3) and both parities of 2 k_q)
+    give the full-grid W_q and the oracle's J/K."""
+    res = {}
+    for half in (0, 1):
+        df, o, dm = make_df(name)
+        df.half_grid = bool(half)
+        df.build()
+        vj, vk = df.get_jk(dm)
+        ej, ek = abs(vj - o["vj"]).max(), abs(vk - o["vk"]).max()
+        print(f"{name} half_grid={half}: |dJ|={ej:.2e} |dK|={ek:.2e}")
+        assert ej < JK_TOL and ek < JK_TOL
+        res[half] = (vj, vk, df._wq)
+    dw = abs(res[1][2] - res[0][2]).max() / abs(res[0][2]).max()
+    d = max(abs(res[1][0] - res[0][0]).max(), abs(res[1][1] - res[0][1]).max())
+    print(f"{name}: |JK(half) - JK(full)| = {d:.2e}, rel |dW| = {dw:.2e}")
+    assert d < 1e-9
+
+
 def test_build_y_qlist():
     """fisdf_build_y_qs with a non-contiguous q-list writes y_q in list order."""
     from fisdf import _lib as L
