@@ -968,10 +968,19 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
     const char* e = getenv("FISDF_YBLK_MB");
     return (e ? atol(e) : 2048L) << 20;
   }();
-  // time reversal (fisdf_set_time_reversal): fx_k only for the k-planes a <= n0/2, the
-  // others are conj(fx_{-k}) inside kmesh_y — ~45% less FX traffic at 4x4x4
+  // time reversal (fisdf_set_time_reversal): fx_k only for the representatives k <= -k, the
+  // others are conj(fx_{-k}) inside kmesh_y — 36 of 64 k at 4x4x4
   const bool half = c->time_reversal;
+  if (half && nblk > 0) {
+    // fused fx + k-mesh DFT (FISDF_Y_FUSED, default on): no fx round trip through HBM
+    bool done = false;
+    FISDF_TRY(y_fused(c->stream, X, nip, nao, f, f_kstride, nblk, kmesh, h_qs, nq, yT,
+                      (long)nip * ngrid, ngrid, g0, c->maximag + 1, &done));
+    if (done) return 0;
+  }
   const int nks = half ? kmesh_half_count(kmesh) : nk;
+  std::vector<int> runs = {0, nk};
+  if (half) FISDF_TRY(kmesh_rep_runs(kmesh, &runs));
   const long per_g = (long)nks * nip * sizeof(cplx);
   int gb = (int)std::max(64L, std::min<long>(nblk, yblk_bytes / std::max(per_g, 1L)));
   gb = std::min(gb, std::max(nblk, 1));
@@ -1008,10 +1017,15 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
     cplx* FX = (cplx*)((char*)base + o1[bi]);
     // buffer bi is free once the DFT of block blk-2 has read it
     if (nbuf == 2 && blk >= 2) FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_ybuf[2 + bi], 0));
-    // fx_k^T = X_k f_k^H  -> FX[k][I][g]   (:76, transposed layout)
-    FISDF_TRY(zgemm(c->stream, OP_N, OP_C, nip, m, nao, ONE, X, nao, (long)nip * nao,
-                    f + (long)s0 * nao, nao, f_kstride, ZERO, FX, m, nm, nks, 1, nullptr,
-                    fx_epi));
+    // fx_k^T = X_k f_k^H  -> FX[slot(k)][I][g]   (:76, transposed layout), one batched GEMM
+    // per run of consecutive stored k
+    for (size_t r = 0, slot = 0; r < runs.size(); r += 2) {
+      const int k0 = runs[r], nb = runs[r + 1] - runs[r];
+      FISDF_TRY(zgemm(c->stream, OP_N, OP_C, nip, m, nao, ONE, X + (long)k0 * nip * nao, nao,
+                      (long)nip * nao, f + (long)k0 * f_kstride + (long)s0 * nao, nao, f_kstride,
+                      ZERO, FX + (long)slot * nm, m, nm, nb, 1, nullptr, fx_epi));
+      slot += nb;
+    }
     if (nbuf == 2) {
       FISDF_HIP(hipEventRecord(c->ev_ybuf[bi], c->stream));
       FISDF_HIP(hipStreamWaitEvent(sk, c->ev_ybuf[bi], 0));
@@ -1042,7 +1056,10 @@ int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk
 // ---- A4 ---------------------------------------------------------------------
 // rank copies, pivot-order factor (identity-padded to nip so the small back-substitutions of
 // all q run as one batch), diagonal-block inverses and the merged TRSM operator, on stream s
-int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src) {
+// need_linv: the diagonal-block inverses of Lp (trsm_blocked, used only when some rank < nip;
+// the unpivoted path is full-rank by construction — a failing slot is refactored, and this
+// rerun, by factor_pivoted_slots)
+int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src, bool need_linv) {
   const int nk = c->f_nk, nip = c->f_nip, nb = c->f_nb, nblk = (nip + nb - 1) / nb;
   const long nn = (long)nip * nip;
   FISDF_HIP(hipMemcpyAsync(c->f_rank_pinned, rank_dev_src, sizeof(int) * nk, hipMemcpyDeviceToHost, s));
@@ -1052,13 +1069,14 @@ int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src) {
   // per lane before its first TRSM)
   FISDF_HIP(hipEventRecord(c->ev_chol, s));
   FISDF_TRY(gather_lp(s, c->f_L, nip, nip, c->f_piv, c->f_rank_dev, nip, c->f_Lp, nk));
-  FISDF_TRY(trinv_blocks(s, c->f_Lp, nip, nip, nn, nb, (long)nblk * nb * nb, c->f_Linv, nk));
+  if (need_linv)
+    FISDF_TRY(trinv_blocks(s, c->f_Lp, nip, nip, nn, nb, (long)nblk * nb * nb, c->f_Linv, nk));
   FISDF_TRY(build_trsm_q(s, c->f_Lp, nip, nn, c->f_Q, nk, GEMM_FULL));
   // L^{-1} by the same block-row substitution applied to the identity (the fit then applies it
   // as one lower-triangular GEMM over the grid; J/K within 2-3x of the TRSM's rounding,
   // tests/experiments/explicit_tri_inverse.py)
   FISDF_TRY(set_identity(s, c->f_Li, nip, nk));
-  FISDF_TRY(trsm_merged_batched(s, c->f_Q, nn, nip, c->f_Li, nip, nn, nip, nk));
+  FISDF_TRY(trsm_merged_batched(s, c->f_Q, nn, nip, c->f_Li, nip, nn, nip, nk, true));
   return 0;
 }
 
@@ -1083,7 +1101,7 @@ int factor_pivoted(fisdf_ctx* c, hipStream_t s) {
   FISDF_TRY(pchol(s, c->f_x4s, nip, nn, nip, nk, nip, c->f_tol, 0.0, c->f_L, c->f_piv,
                   (int*)(b + oR), (double*)(b + oD), (int*)(b + oF), (double*)(b + oW)));
   c->f_used_pivoted = true;
-  return factor_finish(c, s, (const int*)(b + oR));
+  return factor_finish(c, s, (const int*)(b + oR), true);
 }
 
 // the greedy pivoted factorisation of only the listed slots (those whose unpivoted Cholesky
@@ -1121,7 +1139,7 @@ int factor_pivoted_slots(fisdf_ctx* c, hipStream_t s, const std::vector<int>& sl
   FISDF_HIP(hipFreeAsync(L, s));
   FISDF_HIP(hipFreeAsync(P, s));
   c->f_used_pivoted = true;
-  return factor_finish(c, s, (const int*)(b + oU));
+  return factor_finish(c, s, (const int*)(b + oU), true);
 }
 
 static int ensure_side(fisdf_ctx* c) {
@@ -1235,11 +1253,14 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
     FISDF_TRY(chol_unpivoted(s, c->f_L, nip, nk, tol_rel, c->f_piv, (int*)(b + oU),
                              (int*)(b + oFl), (cplx*)(b + oWk)));
     FISDF_HIP(hipMemcpyAsync(c->f_fail_pinned, b + oFl, sizeof(int) * nk, hipMemcpyDeviceToHost, s));
-    FISDF_TRY(factor_finish(c, s, (const int*)(b + oU)));
+    FISDF_TRY(factor_finish(c, s, (const int*)(b + oU), false));
     c->f_check_fail = true;
   }
   FISDF_HIP(hipEventRecord(c->ev_fac, s));
   c->f_pending = true;
+  // experiment: FISDF_FACTOR_SERIAL=1 makes later work on the main stream wait for the chain
+  static const bool serial = getenv("FISDF_FACTOR_SERIAL") && getenv("FISDF_FACTOR_SERIAL")[0] == '1';
+  if (serial) FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_fac, 0));
   return 0;
 }
 

@@ -1,6 +1,8 @@
 #pragma once
 #include "common.h"
 
+#include <vector>
+
 namespace fisdf {
 
 struct CellGeom {
@@ -15,7 +17,7 @@ int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int ldl, long sL, int nb,
 int build_trsm_q(hipStream_t s, const cplx* Lp, int r, long sL, cplx* Q, int batch, int mode);
 int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol, int mode);
 int trsm_merged_batched(hipStream_t s, const cplx* Q, long sQ, int r, cplx* X, long ld, long sX,
-                        int ncol, int batch);
+                        int ncol, int batch, bool lower_rhs = false);
 int set_identity(hipStream_t s, cplx* X, int n, int batch);
 int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, long ldl, long sL, int r,
                  const cplx* Linv, long sLi, int nb, cplx* B, long ldb, long sB, cplx* X, long ldx,
@@ -71,9 +73,19 @@ int permute_kgm(hipStream_t s, const cplx* x0, int nq, int ng, int nao, cplx* ou
 int pair_product(hipStream_t s, const cplx* A, int n1, const cplx* B, int n2, int nip, cplx* P);
 // y_q = Phi^T (Re(Phi FX))^2 for the ascending q-list (h_qs on the host; d_qs a device copy,
 // needed only when the k-mesh has more than 64 points), written to yT[slot][I][goff + g].
-// half: FX holds only the first kmesh_half_count(kmesh) k (planes a <= n0/2); the others are
-// conj(FX[-k]) (time reversal)
+// half: FX holds only the kmesh_half_count(kmesh) representatives k <= -k (ascending k, 36 of
+// 64 at 4x4x4); the others are conj(FX[-k]) (time reversal).  kmesh_rep_runs: the
+// representatives as [begin, end) runs of consecutive k (pairs appended to runs)
 int kmesh_half_count(const int kmesh[3]);
+// Fused y build (time reversal, register k-meshes): fx_k = X_k f_k^H on MFMA for the
+// representative k, staged per 16 x 16 (I, g) tile in LDS, then the kmesh_y DFTs — no fx in
+// HBM.  X (nk, nip, nao); F = f + g0*nao with k stride fks (g rows of nao); writes
+// yT[slot][I][goff + g] for g < m.  *handled = false (nothing enqueued) for other k-meshes,
+// nk > 64, or FISDF_Y_FUSED=0.
+int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long fks, int m,
+            const int kmesh[3], const int* h_qs, int nq, cplx* yT, long qs, long Is, long goff,
+            unsigned long long* mon, bool* handled);
+int kmesh_rep_runs(const int kmesh[3], std::vector<int>* runs);
 // Bloch AO values (ao.hip): F (nimg, ng, nao) f64 workspace, scratch for the small tables;
 // nkb > 0: at the nkb band k-points h_kband (any k) instead of the k-mesh, F (nT, ng, nao)
 int eval_ao(hipStream_t s, const double* d_coords, int ng, int natm, const double* h_atoms, int nsh,

@@ -284,23 +284,41 @@ __device__ void kmesh_axis_dft(cplx* T, int CT, int ld, int nk, int na, int stri
 }
 
 // index of -k on the k-mesh (k = (a*n1 + b)*n2 + c, ascending cartesian order)
-__host__ __device__ inline int kmesh_partner(int k, int n0, int n1, int n2) {
-  const int c = k % n2, b = (k / n2) % n1, a = k / (n1 * n2);
-  return (((n0 - a) % n0) * n1 + (n1 - b) % n1) * n2 + (n2 - c) % n2;
+__host__ __device__ constexpr int kmesh_partner(int k, int n0, int n1, int n2) {
+  return (((n0 - k / (n1 * n2)) % n0) * n1 + (n1 - (k / n2) % n1) % n1) * n2 + (n2 - k % n2) % n2;
+}
+// time reversal: fx is stored for the representatives k <= -k only (36 of 64 at 4x4x4), in
+// ascending k; the slot of representative k is the number of representatives below it
+__host__ __device__ constexpr bool kmesh_is_rep(int k, int n0, int n1, int n2) {
+  return k <= kmesh_partner(k, n0, n1, n2);
+}
+__host__ __device__ constexpr int kmesh_rep_slot(int k, int n0, int n1, int n2) {
+  int s = 0;
+  for (int j = 0; j < k; ++j) s += kmesh_is_rep(j, n0, n1, n2) ? 1 : 0;
+  return s;
 }
 
 __global__ __launch_bounds__(256) void kmesh_y_kernel(
     const cplx* __restrict__ FX, long ncol, int nk, int n0, int n1, int n2,
     const int* __restrict__ qlist, int nq, int m, cplx* __restrict__ yT, long qs, long Is,
-    long goff, int CT, int nks,
+    long goff, int CT, int half,
     unsigned long long* __restrict__ mon) {
   extern __shared__ cplx sm[];
   cplx* w0 = sm;
   cplx* w1 = sm + KM_MAXN;
   cplx* w2 = sm + 2 * KM_MAXN;
   cplx* T = sm + 3 * KM_MAXN;
+  int* src = (int*)(T + (long)nk * (CT + 1));  // FX slot of k (negated - 1: conj of that slot)
   const int ld = CT + 1;
   const int tid = threadIdx.x, nthr = blockDim.x;
+  for (int k = tid; k < nk; k += nthr) {
+    if (!half) {
+      src[k] = k;
+    } else {
+      const int p = kmesh_partner(k, n0, n1, n2);
+      src[k] = k <= p ? kmesh_rep_slot(k, n0, n1, n2) : -1 - kmesh_rep_slot(p, n0, n1, n2);
+    }
+  }
   const int ns[3] = {n0, n1, n2};
   for (int a = 0; a < 3; ++a) {
     cplx* w = a == 0 ? w0 : (a == 1 ? w1 : w2);
@@ -310,6 +328,7 @@ __global__ __launch_bounds__(256) void kmesh_y_kernel(
       w[t] = cmk(cc, s);
     }
   }
+  __syncthreads();  // src is read by every thread's first tile load
   const double sc = 1.0 / sqrt((double)nk);
   const long ntiles = (ncol + CT - 1) / CT;
   // persistent over column tiles: twiddles once, U loads in flight per thread
@@ -322,12 +341,12 @@ __global__ __launch_bounds__(256) void kmesh_y_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = e0 + u * nthr + tid;
-      int k = e / CT;
       const int c = e % CT;
       const long col = c0 + c;
       const bool ok = e < tot && col < ncol;
-      const bool mirror = k >= nks;  // time reversal: fx_{-k} = conj(fx_k), only k < nks stored
-      if (mirror) k = kmesh_partner(k, n0, n1, n2);
+      int k = ok ? src[e / CT] : 0;
+      const bool mirror = k < 0;  // time reversal: fx_{-k} = conj(fx_k) of its representative
+      if (mirror) k = -1 - k;
       v[u] = FX[ok ? (long)k * ncol + col : 0];
       if (!ok) v[u] = cmk(0, 0);
       if (mirror) v[u] = cconj(v[u]);
@@ -432,12 +451,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   double mi = 0.0;
   for (int col = blockIdx.x * blockDim.x + threadIdx.x; col < ncol; col += gridDim.x * blockDim.x) {
     cplx v[NK];
-    // HALF: only the k-planes a <= N0/2 are stored; fx_{-k} = conj(fx_k) (time reversal)
-    constexpr int NKS = HALF ? (N0 / 2 + 1) * N1 * N2 : NK;
+    // HALF: only the representatives k <= -k are stored; fx_{-k} = conj(fx_k) (time reversal)
 #pragma unroll
-    for (int k = 0; k < NKS; ++k) v[k] = FX[(long)k * ncol + col];
+    for (int k = 0; k < NK; ++k)
+      if (!HALF || kmesh_is_rep(k, N0, N1, N2))
+        v[k] = FX[(long)(HALF ? kmesh_rep_slot(k, N0, N1, N2) : k) * ncol + col];
 #pragma unroll
-    for (int k = NKS; k < NK; ++k) v[k] = cconj(v[kmesh_partner(k, N0, N1, N2)]);
+    for (int k = 0; k < NK; ++k)
+      if (HALF && !kmesh_is_rep(k, N0, N1, N2)) v[k] = cconj(v[kmesh_partner(k, N0, N1, N2)]);
     // fx_s = Phi fx_k (fftisdf.py:79)
     reg_axis_dft<N0, N1 * N2, NK>(v, tw0);
     reg_axis_dft<N1, N2, NK>(v, tw1);
@@ -463,6 +484,214 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mi = fmax(mi, __shfl_xor(mi, o, 64));
   if ((threadIdx.x & 63) == 0 && mon) atomicMax(mon, (unsigned long long)__double_as_longlong(mi));
+}
+
+// Fused y build for the register k-meshes under time reversal (fftisdf.py:76-85).  One
+// workgroup per 16 (I) x 16 (g) column tile; fx_k = X_k f_k^H is formed on FP64 MFMA for the
+// representative k (K = nao, 3-multiplication complex form: t1 = Xr fr, t2 = Xi fi,
+// t3 = (Xr + Xi)(fr - fi); Re = t1 + t2, Im = t3 - t1 + t2) and never reaches HBM (the
+// unfused path writes and re-reads it: 2/3 of the y build's traffic).  The k-mesh DFTs are
+// split by k-planes a (axis 0) so that only one chunk of fx is staged in LDS at a time and two
+// workgroups fit a CU (one's MFMA phase overlaps the other's DFT phase):
+//   t_a(s) = sum_{b,c} fx(a,b,c) e^{+2 pi i (b s_b/N1 + c s_c/N2)}    (2-D DFT per plane)
+// with t_{-a} = conj(t_a) pointwise (fx_{-k} = conj(fx_k)), so only planes a <= -a are formed:
+// chunk A = the complex planes 0 < a < N0/2 (every k a representative), chunk B = the
+// self-paired planes a = 0, N0/2 (half their k; t_a real).  Then per s:
+//   fx_s(a', s) = sum_a e^{+2 pi i a a'/N0} t_a(s),  y_s = fx_s^2 (fftisdf.py:81,83),
+//   r_qa(s) = sum_a' e^{+2 pi i a' qa/N0} y_s(a', s),  y(qa, .) = 2-D DFT of r_qa (:84),
+// and y_{-q} = conj(y_q).  Tile order: XCD-aware (workgroup id & 7 = XCD), an XCD's resident
+// workgroups walk the I-tiles of one g-tile (the f tile stays in its L2).
+// mode (debug timing, FISDF_YF_MODE): bit 0 skips the MFMA phase, bit 1 the DFT + stores.
+constexpr int YF_MAXKS = 8;  // nao <= 32 per K chunk (larger nao loops over chunks)
+struct YfPlan {
+  int nA, nB;   // slots of chunk A (complex planes) and B (self-paired planes)
+  int kA[16];   // k of each slot, in the kernel's slot order
+  int kB[32];
+};
+
+template <int N1, int N2>
+__host__ __device__ constexpr int yf_inplane_partner(int bc) {
+  return ((N1 - bc / N2) % N1) * N2 + (N2 - bc % N2) % N2;
+}
+template <int N1, int N2>
+__host__ __device__ constexpr int yf_inplane_rank(int bc) {
+  int r = 0;
+  for (int j = 0; j < bc; ++j) r += j <= yf_inplane_partner<N1, N2>(j) ? 1 : 0;
+  return r;
+}
+
+// fx for the chunk's slots (wave w: slots w, w+4, ...) into buf[slot][256]
+__device__ __forceinline__ void yf_mfma_chunk(const cplx* __restrict__ X, int nip, int nao,
+                                              const cplx* __restrict__ F, long fks,
+                                              const int* ks, int nslot, int Ia, bool okI,
+                                              int ga, bool okg, int lane, int w,
+                                              cplx* __restrict__ buf) {
+  const int i16 = lane & 15, kq = lane >> 4;
+  const int nkc = (nao + 4 * YF_MAXKS - 1) / (4 * YF_MAXKS);
+  cplx a[YF_MAXKS], b[YF_MAXKS];
+  auto load = [&](int s, int c) {
+    const int k = ks[s];
+    const cplx* xa = X + ((long)k * nip + (okI ? Ia : 0)) * nao;
+    const cplx* fb = F + (long)k * fks + (long)(okg ? ga : 0) * nao;
+#pragma unroll
+    for (int kk = 0; kk < YF_MAXKS; ++kk) {
+      const int mu = c * 4 * YF_MAXKS + kk * 4 + kq;
+      const bool ok = mu < nao;
+      a[kk] = xa[ok ? mu : 0];
+      b[kk] = fb[ok ? mu : 0];
+      if (!(ok && okI)) a[kk] = cmk(0, 0);
+      if (!(ok && okg)) b[kk] = cmk(0, 0);
+    }
+  };
+  int s = w, c = 0;
+  if (s < nslot) load(s, 0);
+  f64x4 t1 = {0, 0, 0, 0}, t2 = {0, 0, 0, 0}, t3 = {0, 0, 0, 0};
+  while (s < nslot) {
+    double ar[YF_MAXKS], ai[YF_MAXKS], as[YF_MAXKS], br[YF_MAXKS], bi[YF_MAXKS], bd[YF_MAXKS];
+#pragma unroll
+    for (int kk = 0; kk < YF_MAXKS; ++kk) {
+      ar[kk] = a[kk].x; ai[kk] = a[kk].y; as[kk] = a[kk].x + a[kk].y;
+      br[kk] = b[kk].x; bi[kk] = b[kk].y; bd[kk] = b[kk].x - b[kk].y;
+    }
+    const int kvalid = min(YF_MAXKS, (nao - c * 4 * YF_MAXKS + 3) / 4);
+    // next (slot, chunk) in flight across this one's MFMAs
+    int sn = s, cn = c + 1;
+    if (cn == nkc) { sn = s + 4; cn = 0; }
+    if (sn < nslot) load(sn, cn);
+#pragma unroll
+    for (int kk = 0; kk < YF_MAXKS; ++kk) {
+      if (kk < kvalid) {
+        t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[kk], br[kk], t1, 0, 0, 0);
+        t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[kk], bi[kk], t2, 0, 0, 0);
+        t3 = __builtin_amdgcn_mfma_f64_16x16x4f64(as[kk], bd[kk], t3, 0, 0, 0);
+      }
+    }
+    if (cn == 0) {  // slot complete: C row = Il = kq + 4 r, col = gl = i16
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        buf[s * 256 + (kq + 4 * r) * 16 + i16] = cmk(t1[r] + t2[r], t3[r] - t1[r] + t2[r]);
+      t1 = f64x4{0, 0, 0, 0};
+      t2 = f64x4{0, 0, 0, 0};
+      t3 = f64x4{0, 0, 0, 0};
+    }
+    s = sn;
+    c = cn;
+  }
+}
+
+template <int N0, int N1, int N2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void y_fused_kernel(
+    const cplx* __restrict__ X, int nip, int nao, const cplx* __restrict__ F, long fks, int m,
+    int nIt, int nGt, YfPlan plan, unsigned long long qmask, cplx* __restrict__ yT, long qs,
+    long Is, long goff, int mode) {
+  constexpr int P = N1 * N2, NK = N0 * P;
+  constexpr int R = yf_inplane_rank<N1, N2>(P);         // in-plane representatives
+  constexpr int NC = (N0 - 1) / 2;                        // complex planes 1..NC (N0 <= 4: 0 or 1)
+  constexpr int NR = (N0 % 2 == 0 && N0 > 1) ? 2 : 1;     // self-paired planes 0 (, N0/2)
+  static_assert(N0 <= 4 && NC <= 1, "y_fused: k-mesh axis 0 must be <= 4");
+  extern __shared__ cplx buf[];  // [slot][256]: column c = Il * 16 + gl
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int gt = (j / nIt) * 8 + xcd, it = j % nIt;
+  if (gt >= nGt) return;
+  const int I0 = it * 16, g0 = gt * 16;
+  const int Ia = I0 + (lane & 15), ga = g0 + (lane & 15);
+  const bool okI = Ia < nip, okg = ga < m;
+  cplx tw0[N0], tw1[N1], tw2[N2];
+#pragma unroll
+  for (int t = 0; t < N0; ++t) { double sn, cs; sincospi(2.0 * t / N0, &sn, &cs); tw0[t] = cmk(cs, sn); }
+#pragma unroll
+  for (int t = 0; t < N1; ++t) { double sn, cs; sincospi(2.0 * t / N1, &sn, &cs); tw1[t] = cmk(cs, sn); }
+#pragma unroll
+  for (int t = 0; t < N2; ++t) { double sn, cs; sincospi(2.0 * t / N2, &sn, &cs); tw2[t] = cmk(cs, sn); }
+  cplx tc[NC > 0 ? P : 1];  // t_1 (complex plane)
+  double tr[NR][P];         // t_0 (, t_{N0/2})
+  // ---- chunk A: the complex plane a = 1 ----
+  if constexpr (NC > 0) {
+    if (!(mode & 1)) yf_mfma_chunk(X, nip, nao, F, fks, plan.kA, plan.nA, Ia, okI, ga, okg, lane, w, buf);
+    __syncthreads();
+#pragma unroll
+    for (int bc = 0; bc < P; ++bc) tc[bc] = (mode & 1) ? cmk(0, 0) : buf[bc * 256 + tid];
+    reg_axis_dft<N1, N2, P>(tc, tw1);
+    reg_axis_dft<N2, 1, P>(tc, tw2);
+    __syncthreads();  // buf is rewritten by chunk B
+  }
+  // ---- chunk B: the self-paired planes, half their k each ----
+  if (!(mode & 1)) yf_mfma_chunk(X, nip, nao, F, fks, plan.kB, plan.nB, Ia, okI, ga, okg, lane, w, buf);
+  __syncthreads();
+  if (mode & 2) return;
+#pragma unroll
+  for (int pi = 0; pi < NR; ++pi) {
+    cplx u[P];
+#pragma unroll
+    for (int bc = 0; bc < P; ++bc)
+      if (bc <= yf_inplane_partner<N1, N2>(bc))
+        u[bc] = (mode & 1) ? cmk(0, 0) : buf[(pi * R + yf_inplane_rank<N1, N2>(bc)) * 256 + tid];
+#pragma unroll
+    for (int bc = 0; bc < P; ++bc)
+      if (bc > yf_inplane_partner<N1, N2>(bc)) u[bc] = cconj(u[yf_inplane_partner<N1, N2>(bc)]);
+    reg_axis_dft<N1, N2, P>(u, tw1);
+    reg_axis_dft<N2, 1, P>(u, tw2);
+#pragma unroll
+    for (int bc = 0; bc < P; ++bc) tr[pi][bc] = u[bc].x;
+  }
+  // ---- per s: fx_s over axis 0, y_s = fx_s^2, r_qa = axis-0 DFT of y_s ----
+  const double sc = 1.0 / sqrt((double)NK), sc2 = sc * sc;
+  double rr[NR][P];
+  cplx rc[NC > 0 ? P : 1];
+#pragma unroll
+  for (int s = 0; s < P; ++s) {
+    double ys[N0];
+#pragma unroll
+    for (int a2 = 0; a2 < N0; ++a2) {
+      double f = tr[0][s];
+      if constexpr (NR == 2) f += (a2 & 1) ? -tr[1][s] : tr[1][s];
+      if constexpr (NC > 0) {  // 2 Re(w^{a2} t_1)
+        const cplx wv = tw0[a2 % N0];
+        f += 2.0 * (wv.x * tc[s].x - wv.y * tc[s].y);
+      }
+      ys[a2] = f * f * sc2;
+    }
+    double r0 = 0.0, rh = 0.0;
+    cplx r1 = cmk(0, 0);
+#pragma unroll
+    for (int a2 = 0; a2 < N0; ++a2) {
+      r0 += ys[a2];
+      if constexpr (NR == 2) rh += (a2 & 1) ? -ys[a2] : ys[a2];
+      if constexpr (NC > 0) r1 = cadd(r1, cscale(tw0[a2 % N0], ys[a2]));
+    }
+    rr[0][s] = r0;
+    if constexpr (NR == 2) rr[1][s] = rh;
+    if constexpr (NC > 0) rc[s] = r1;
+  }
+  // ---- output planes: y(qa, .) = 2-D DFT of r_qa; y(-q) = conj(y(q)) ----
+  const int I = I0 + (tid >> 4), g = g0 + (tid & 15);
+  if (I >= nip || g >= m) return;
+  cplx* out = yT + (long)I * Is + goff + g;
+  auto put = [&](int q, cplx v) {
+    if ((qmask >> q) & 1ull)
+      out[(long)__popcll(qmask & ((1ull << q) - 1ull)) * qs] = cmk(v.x * sc, v.y * sc);
+  };
+#pragma unroll
+  for (int pi = 0; pi < NR; ++pi) {
+    cplx u[P];
+#pragma unroll
+    for (int bc = 0; bc < P; ++bc) u[bc] = cmk(rr[pi][bc], 0.0);
+    reg_axis_dft<N1, N2, P>(u, tw1);
+    reg_axis_dft<N2, 1, P>(u, tw2);
+    const int qa = pi == 0 ? 0 : N0 / 2;
+#pragma unroll
+    for (int bc = 0; bc < P; ++bc) put(qa * P + bc, u[bc]);
+  }
+  if constexpr (NC > 0) {
+    reg_axis_dft<N1, N2, P>(rc, tw1);
+    reg_axis_dft<N2, 1, P>(rc, tw2);
+#pragma unroll
+    for (int bc = 0; bc < P; ++bc) {
+      put(P + bc, rc[bc]);
+      put((N0 - 1) * P + yf_inplane_partner<N1, N2>(bc), cconj(rc[bc]));
+    }
+  }
 }
 
 // pair densities at the interpolation points: P[I][i*n2 + j] = conj(A[I][i]) * B[I][j]
@@ -577,17 +806,19 @@ int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol,
   return 0;
 }
 
-// trsm_merged over a batch (Q and X with batch strides sQ, sX): one launch per block row
+// trsm_merged over a batch (Q and X with batch strides sQ, sX): one launch per block row.
+// lower_rhs: X is lower-triangular (the identity, for L^{-1}), so block row b only has
+// columns < b1 to compute (the rest stay zero)
 int trsm_merged_batched(hipStream_t s, const cplx* Q, long sQ, int r, cplx* X, long ld, long sX,
-                        int ncol, int batch) {
+                        int ncol, int batch, bool lower_rhs) {
   const int nblk = (r + 63) / 64;
   if (nblk == 0 || batch == 0) return 0;
   const int s0 = r - 64 * (nblk - 1);
   const cplx one = cmk(1, 0), zero = cmk(0, 0);
   for (int b = 0; b < nblk; ++b) {
     const int b0 = b == 0 ? 0 : s0 + (b - 1) * 64, m = b == 0 ? s0 : 64, b1 = b0 + m;
-    FISDF_TRY(zgemm(s, OP_N, OP_N, m, ncol, b1, one, Q + (long)b0 * r, r, sQ, X, ld, sX, zero,
-                    X + (long)b0 * ld, ld, sX, batch, 1));
+    FISDF_TRY(zgemm(s, OP_N, OP_N, m, lower_rhs ? std::min(ncol, b1) : ncol, b1, one,
+                    Q + (long)b0 * r, r, sQ, X, ld, sX, zero, X + (long)b0 * ld, ld, sX, batch, 1));
   }
   return 0;
 }
@@ -982,7 +1213,7 @@ int min_norm_operator(hipStream_t s, const cplx* L, int n, int rmax, int* piv, i
     FISDF_TRY(chol_unpivoted(s, S, r, 1, 0.0, iw, iw + r, fail + pass, cw));
     FISDF_TRY(build_trsm_q(s, S, r, rr, Qop, 1, GEMM_FULL));
     FISDF_TRY(set_identity(s, Li, r, 1));
-    FISDF_TRY(trsm_merged_batched(s, Qop, rr, r, Li, r, rr, r, 1));
+    FISDF_TRY(trsm_merged_batched(s, Qop, rr, r, Li, r, rr, r, 1, true));
     FISDF_TRY(zgemm(s, OP_N, OP_C, n, r, r, one, A, r, 0, Li, r, 0, zero, A2, r, 0, 1));
     std::swap(A, A2);
     if (pass == 0) {
@@ -1087,13 +1318,29 @@ int scale_rows(hipStream_t s, const cplx* X, const cplx* v, int nset, int nk, in
   return 0;
 }
 
-int kmesh_half_count(const int kmesh[3]) { return (kmesh[0] / 2 + 1) * kmesh[1] * kmesh[2]; }
+int kmesh_half_count(const int kmesh[3]) {
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  return nk == 0 ? 0 : kmesh_rep_slot(nk, kmesh[0], kmesh[1], kmesh[2]);
+}
+
+int kmesh_rep_runs(const int kmesh[3], std::vector<int>* runs) {
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  runs->clear();
+  for (int k = 0; k < nk;) {
+    if (!kmesh_is_rep(k, kmesh[0], kmesh[1], kmesh[2])) { ++k; continue; }
+    int e = k;
+    while (e < nk && kmesh_is_rep(e, kmesh[0], kmesh[1], kmesh[2])) ++e;
+    runs->push_back(k);
+    runs->push_back(e);
+    k = e;
+  }
+  return 0;
+}
 
 int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const int* h_qs,
             const int* d_qs, int nq, int m, cplx* yT, long qs, long Is, long goff,
             bool half, unsigned long long* mon) {
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
-  const int nks = half ? kmesh_half_count(kmesh) : nk;
   for (int i = 0; i < nq; ++i)
     FISDF_CHECK(h_qs[i] >= 0 && h_qs[i] < nk && (i == 0 || h_qs[i] > h_qs[i - 1]),
                 "kmesh_y: q-list must be ascending and inside the k-mesh");
@@ -1121,7 +1368,7 @@ int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const 
   }
   int CT = 64;
   while (CT > 8 && sizeof(cplx) * ((size_t)nk * (CT + 1) + 3 * KM_MAXN) > 64 * 1024) CT /= 2;
-  const size_t lds = sizeof(cplx) * ((size_t)nk * (CT + 1) + 3 * KM_MAXN);
+  const size_t lds = sizeof(cplx) * ((size_t)nk * (CT + 1) + 3 * KM_MAXN) + sizeof(int) * nk;
   FISDF_CHECK(lds <= 160 * 1024, "kmesh_y: k-mesh too large for the LDS tile");
   FISDF_CHECK(d_qs != nullptr, "kmesh_y: device q-list required for this k-mesh");
   const long tiles = (ncol + CT - 1) / CT;
@@ -1129,8 +1376,68 @@ int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const 
   if (tiles == 0) return 0;
   const unsigned grid = (unsigned)std::min<long>(tiles, 4096);
   hipLaunchKernelGGL(kmesh_y_kernel, dim3(grid), dim3(256), lds, s, FX, ncol, nk,
-                     kmesh[0], kmesh[1], kmesh[2], d_qs, nq, m, yT, qs, Is, goff, CT, nks, mon);
+                     kmesh[0], kmesh[1], kmesh[2], d_qs, nq, m, yT, qs, Is, goff, CT, half ? 1 : 0, mon);
   FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+bool y_fused_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FISDF_Y_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long fks, int m,
+            const int kmesh[3], const int* h_qs, int nq, cplx* yT, long qs, long Is, long goff,
+            unsigned long long* mon, bool* handled) {
+  (void)mon;  // fx_s is real by construction here (t_{-a} = conj(t_a)); nothing to monitor
+  *handled = false;
+  const int n0 = kmesh[0], n1 = kmesh[1], n2 = kmesh[2];
+  const int nk = n0 * n1 * n2, P = n1 * n2;
+  if (!y_fused_enabled() || nk > 64 || n0 > 4 || P > 16 || m <= 0 || nip <= 0) return 0;
+  for (int i = 0; i < nq; ++i)
+    FISDF_CHECK(h_qs[i] >= 0 && h_qs[i] < nk && (i == 0 || h_qs[i] > h_qs[i - 1]),
+                "y_fused: q-list must be ascending and inside the k-mesh");
+  unsigned long long qmask = 0;
+  for (int i = 0; i < nq; ++i) qmask |= 1ull << h_qs[i];
+  // slot order of the kernel: chunk A = plane 1 (if 1 < N0 - 1), all P; chunk B = planes
+  // 0 (and N0/2 if even) at their in-plane representatives bc <= -bc, ascending
+  YfPlan plan{};
+  if (n0 >= 3)
+    for (int bc = 0; bc < P; ++bc) plan.kA[plan.nA++] = P + bc;
+  const int nr = (n0 % 2 == 0 && n0 > 1) ? 2 : 1;
+  for (int pi = 0; pi < nr; ++pi) {
+    const int a = pi == 0 ? 0 : n0 / 2;
+    for (int bc = 0; bc < P; ++bc) {
+      const int b = bc / n2, c = bc % n2;
+      if (bc <= ((n1 - b) % n1) * n2 + (n2 - c) % n2) plan.kB[plan.nB++] = a * P + bc;
+    }
+  }
+  const size_t lds = sizeof(cplx) * 256 * (size_t)std::max(plan.nA, plan.nB);
+  if (lds > 80 * 1024) return 0;
+  const int nIt = (nip + 15) / 16, nGt = (m + 15) / 16;
+  const long grid = (long)nIt * ((nGt + 7) / 8) * 8;
+  FISDF_CHECK(grid < (1L << 31), "y_fused: grid too large");
+  static const int mode = getenv("FISDF_YF_MODE") ? atoi(getenv("FISDF_YF_MODE")) : 0;
+#define FISDF_YF(a, b, c)                                                                      \
+  if (n0 == a && n1 == b && n2 == c) {                                                         \
+    static bool attr = false;                                                                  \
+    if (!attr) {                                                                               \
+      FISDF_HIP(hipFuncSetAttribute((const void*)y_fused_kernel<a, b, c>,                      \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));   \
+      attr = true;                                                                             \
+    }                                                                                          \
+    hipLaunchKernelGGL((y_fused_kernel<a, b, c>), dim3((unsigned)grid), dim3(256), lds, s, X,   \
+                       nip, nao, F, fks, m, nIt, nGt, plan, qmask, yT, qs, Is, goff, mode);     \
+    FISDF_HIP(hipGetLastError());                                                              \
+    *handled = true;                                                                           \
+    return 0;                                                                                  \
+  }
+  FISDF_YF(1, 1, 1) FISDF_YF(1, 1, 2) FISDF_YF(2, 2, 2) FISDF_YF(3, 3, 1) FISDF_YF(3, 3, 3)
+  FISDF_YF(4, 4, 4) FISDF_YF(2, 2, 1) FISDF_YF(1, 2, 2) FISDF_YF(4, 4, 1) FISDF_YF(2, 2, 4)
+#undef FISDF_YF
   return 0;
 }
 

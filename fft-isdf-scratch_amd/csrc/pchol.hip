@@ -689,15 +689,16 @@ __global__ void diag_max_kernel(const cplx* __restrict__ A, int n, long sA, doub
 }
 
 // factor + invert the m x m diagonal block at (b0, b0) of W (ld n); writes L_bb (lower) in
-// place and L_bb^{-1} to Linv (64 x 64, batch stride 4096)
+// place and L_bb^{-1} to Linv (64 x 64, batch stride 4096).  Register-blocked: thread t owns
+// the 4 x 4 block (rows 4 (t >> 4), cols 4 (t & 15)) of the block in registers, so a step
+// moves only column k (and row k of the inverse) through LDS — one barrier per step, the
+// column double-buffered by step parity (the LDS-resident version spent ~200 us per block on
+// re-reading the trailing matrix each step).
 __global__ __launch_bounds__(256) void chol_diag_kernel(cplx* __restrict__ W, int n, long sW,
                                                         int b0, int m,
                                                         const double* __restrict__ thr,
                                                         int* __restrict__ fail,
                                                         cplx* __restrict__ Linv) {
-  // 256 threads: the block is loaded in one coalesced sweep (16 elements in flight per
-  // thread), every step's column scale / rank-1 update / substitution row is spread over the
-  // workgroup (the single-wave version spent ~1 ms per block on serial LDS chains)
   const int b = blockIdx.x;
   W += b * sW;
   Linv += (long)b * 4096;
@@ -708,58 +709,102 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(cplx* __restrict__ W, in
 #define FISDF_DIAG_PRIO 3
 #endif
   __builtin_amdgcn_s_setprio(FISDF_DIAG_PRIO);
-  __shared__ cplx A[64][65];
-  __shared__ cplx X[64][65];
+  __shared__ cplx Ls[64][65];  // L (inverse phase)
+  __shared__ cplx vec[2][64];  // column k of the factor / row k of the inverse, by parity
+  __shared__ double dsq[2];
   __shared__ int bad;
   const int t = threadIdx.x;
+  const int bi = t >> 4, bj = t & 15, r0 = bi * 4, c0 = bj * 4;
   if (t == 0) bad = 0;
-  {
-    cplx v[16];
+  cplx a[4][4];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int e = t + 256 * u, i = e >> 6, j = e & 63;
-      v[u] = (i < m && j < m) ? W[(long)(b0 + i) * n + b0 + j] : cmk(0, 0);
-    }
+  for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int e = t + 256 * u, i = e >> 6, j = e & 63;
-      A[i][j] = v[u];
-      X[i][j] = cmk(i == j ? 1.0 : 0.0, 0.0);
+    for (int c = 0; c < 4; ++c) {
+      const int i = r0 + r, j = c0 + c;
+      a[r][c] = (i < m && j <= i) ? W[(long)(b0 + i) * n + b0 + j] : cmk(0, 0);
     }
-  }
-  __syncthreads();
   const double th = thr[b];
+  __syncthreads();
   for (int k = 0; k < m; ++k) {
-    const double dk = A[k][k].x;
-    const double lk = sqrt(fmax(dk, 1e-300));
-    __syncthreads();  // every thread has read A[k][k] before it is overwritten
-    if (t > k && t < m) A[t][k] = cscale(A[t][k], 1.0 / lk);
-    if (t == k) A[k][k] = cmk(lk, 0.0);
-    if (t == 0 && !(dk > th)) bad = 1;
-    __syncthreads();
-    // A[i][j] -= A[i][k] conj(A[j][k]),  k < j <= i < m
-    for (int e = t; e < 4096; e += 256) {
-      const int i = e >> 6, j = e & 63;
-      if (j > k && j <= i && i < m) A[i][j] = csub(A[i][j], cmul(A[i][k], cconj(A[j][k])));
-    }
-    __syncthreads();  // the next step reads A[k+1][k+1] and column k+1
-  }
-  // inverse of the lower-triangular block: forward substitution on the identity, row k final
-  // once rows < k have been subtracted (same operation order as a per-column solve)
-  for (int k = 0; k < m; ++k) {
-    if (t < 64) X[k][t] = cscale(X[k][t], 1.0 / A[k][k].x);
-    __syncthreads();
-    for (int e = t; e < 4096; e += 256) {
-      const int i = e >> 6, c = e & 63;
-      if (i > k && i < m) X[i][c] = csub(X[i][c], cmul(A[i][k], X[k][c]));
+    const int p = k & 1, kb = k >> 2, kc = k & 3;
+    if (bj == kb && bi >= kb) {  // owners of column k publish it (rows >= k) and sqrt(A_kk)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (r0 + r >= k) vec[p][r0 + r] = a[r][kc];
+      if (bi == kb) {
+        const double dk = a[kc][kc].x;
+        dsq[p] = sqrt(fmax(dk, 1e-300));
+        if (!(dk > th)) bad = 1;
+      }
     }
     __syncthreads();
+    const double lk = dsq[p], inv = 1.0 / lk;
+    cplx li[4], lj[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      li[r] = (r0 + r > k && r0 + r < m) ? cscale(vec[p][r0 + r], inv) : cmk(0, 0);
+      lj[r] = (c0 + r > k && c0 + r < m) ? cscale(vec[p][c0 + r], inv) : cmk(0, 0);
+    }
+    // A[i][j] -= l_ik conj(l_jk),  k < j <= i
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c0 + c > k && r0 + r >= c0 + c) a[r][c] = csub(a[r][c], cmul(li[r], cconj(lj[c])));
+    if (bj == kb) {  // column k final
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (r0 + r > k) a[r][kc] = li[r];
+        else if (r0 + r == k) a[r][kc] = cmk(lk, 0.0);
+      }
+    }
   }
-  for (int e = t; e < 4096; e += 256) {
-    const int i = e >> 6, j = e & 63;
-    if (i < m && j <= i) W[(long)(b0 + i) * n + b0 + j] = A[i][j];
-    Linv[e] = (i < m && j < m) ? X[i][j] : cmk(i == j ? 1.0 : 0.0, 0.0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int i = r0 + r, j = c0 + c;
+      Ls[i][j] = a[r][c];
+      if (i < m && j <= i) W[(long)(b0 + i) * n + b0 + j] = a[r][c];
+    }
+  __syncthreads();
+  // inverse of the lower-triangular block: X = L^{-1} by right-looking forward substitution
+  // on the identity (row k final once rows < k have been subtracted; then scaled by 1/L_kk)
+  cplx x[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[r][c] = cmk(r0 + r == c0 + c ? 1.0 : 0.0, 0.0);
+  for (int k = 0; k < m; ++k) {
+    const int p = k & 1, kb = k >> 2, kr = k & 3;
+    if (bi == kb) {
+      const double d = 1.0 / Ls[k][k].x;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        x[kr][c] = cscale(x[kr][c], d);
+        vec[p][c0 + c] = x[kr][c];
+      }
+    }
+    __syncthreads();
+    cplx xk[4], lik[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) xk[c] = vec[p][c0 + c];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lik[r] = (r0 + r > k && r0 + r < m) ? Ls[r0 + r][k] : cmk(0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x[r][c] = csub(x[r][c], cmul(lik[r], xk[c]));
   }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int i = r0 + r, j = c0 + c;
+      Linv[i * 64 + j] = (i < m && j < m) ? x[r][c] : cmk(i == j ? 1.0 : 0.0, 0.0);
+    }
+  __syncthreads();
   if (t == 0 && bad) fail[b] = 1;
 }
 

@@ -207,3 +207,42 @@ def test_min_norm_operator(env, real):
     assert res < 1e-6 and np.linalg.norm(z) <= np.linalg.norm(v)
     if real:
         assert abs(M.imag).max() == 0.0
+
+
+@pytest.mark.parametrize("kmesh", [(1, 1, 3), (3, 1, 2), (2, 3, 1), (4, 4, 4)])
+def test_build_y_kmesh_paths(env, kmesh):
+    """fisdf_build_y on the generic LDS k-mesh kernel ((1,1,3), (3,1,2), (2,3,1)) and the
+    register one (4x4x4), with fx stored for every k and for the time-reversal
+    representatives k <= -k only (fisdf_set_time_reversal), against the oracle's y
+    (fftisdf.py:73-85)."""
+    torch, L, ctx = env
+    import os, sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import isdf_ref as R
+    from fisdf import cell as Cm
+    cell = Cm.toy_cell(mesh=(6, 6, 6))
+    coords = cell.gen_uniform_grids(cell.mesh)
+    chi = Cm.eval_ao_kpts(cell, coords, kmesh)            # (nk, ngrid, nao)
+    nk, ngrid, nao = chi.shape
+    pts = np.random.default_rng(5).choice(ngrid, 24, replace=False)
+    xip = np.ascontiguousarray(chi[:, pts, :])
+    phase = R.get_phase(cell.a, R.get_kpts(cell.a, kmesh), kmesh)
+    ref = R.build_y(chi, xip, phase)                       # (nk, ngrid, nip)
+    nip = xip.shape[1]
+    f, X = dev(torch, chi), dev(torch, xip)
+    yT = torch.zeros((nk, nip, ngrid), dtype=torch.complex128, device="cuda")
+    km = (C.c_int * 3)(*kmesh)
+    a = (C.c_double * 9)(*cell.a.ravel())
+    h = ngrid // 3
+    for tr in (0, 1):
+        ctx.call("fisdf_set_time_reversal", tr)
+        yT.zero_()
+        for g0, g1 in ((0, h), (h, ngrid)):  # two blocks: the g0 offset
+            ctx.call("fisdf_build_y", C.c_void_p(f.data_ptr() + g0 * nao * 16), ngrid * nao, g0,
+                     g1 - g0, ngrid, L.ptr(X), nip, nao, km, a, 0, nk, L.ptr(yT))
+        torch.cuda.synchronize()
+        y = yT.cpu().numpy().transpose(0, 2, 1)
+        rel = abs(y - ref).max() / abs(ref).max()
+        print(f"kmesh {kmesh} time_reversal={tr}: max rel |y - y_oracle| = {rel:.2e}")
+        assert rel < 1e-12
+    ctx.call("fisdf_set_time_reversal", 0)
