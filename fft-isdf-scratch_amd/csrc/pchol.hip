@@ -726,37 +726,44 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(cplx* __restrict__ W, in
     }
   const double th = thr[b];
   __syncthreads();
-  for (int k = 0; k < m; ++k) {
-    const int p = k & 1, kb = k >> 2, kc = k & 3;
-    if (bj == kb && bi >= kb) {  // owners of column k publish it (rows >= k) and sqrt(A_kk)
+  // k = 4 kb + kc with kc unrolled: register arrays are indexed with compile-time indices
+  // only (a runtime index demotes them to scratch memory)
+  for (int kb = 0; 4 * kb < m; ++kb) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (r0 + r >= k) vec[p][r0 + r] = a[r][kc];
-      if (bi == kb) {
-        const double dk = a[kc][kc].x;
-        dsq[p] = sqrt(fmax(dk, 1e-300));
-        if (!(dk > th)) bad = 1;
+    for (int kc = 0; kc < 4; ++kc) {
+      const int k = 4 * kb + kc, p = kc & 1;
+      if (k >= m) break;
+      if (bj == kb && bi >= kb) {  // owners of column k publish it (rows >= k) and sqrt(A_kk)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (r0 + r >= k) vec[p][r0 + r] = a[r][kc];
+          if (r0 + r == k) {
+            const double dk = a[r][kc].x;
+            dsq[p] = sqrt(fmax(dk, 1e-300));
+            if (!(dk > th)) bad = 1;
+          }
+        }
       }
-    }
-    __syncthreads();
-    const double lk = dsq[p], inv = 1.0 / lk;
-    cplx li[4], lj[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      li[r] = (r0 + r > k && r0 + r < m) ? cscale(vec[p][r0 + r], inv) : cmk(0, 0);
-      lj[r] = (c0 + r > k && c0 + r < m) ? cscale(vec[p][c0 + r], inv) : cmk(0, 0);
-    }
-    // A[i][j] -= l_ik conj(l_jk),  k < j <= i
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (c0 + c > k && r0 + r >= c0 + c) a[r][c] = csub(a[r][c], cmul(li[r], cconj(lj[c])));
-    if (bj == kb) {  // column k final
+      __syncthreads();
+      const double lk = dsq[p], inv = 1.0 / lk;
+      cplx li[4], lj[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (r0 + r > k) a[r][kc] = li[r];
-        else if (r0 + r == k) a[r][kc] = cmk(lk, 0.0);
+        li[r] = (r0 + r > k && r0 + r < m) ? cscale(vec[p][r0 + r], inv) : cmk(0, 0);
+        lj[r] = (c0 + r > k && c0 + r < m) ? cscale(vec[p][c0 + r], inv) : cmk(0, 0);
+      }
+      // A[i][j] -= l_ik conj(l_jk),  k < j <= i
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c0 + c > k && r0 + r >= c0 + c) a[r][c] = csub(a[r][c], cmul(li[r], cconj(lj[c])));
+      if (bj == kb) {  // column k final
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (r0 + r > k) a[r][kc] = li[r];
+          else if (r0 + r == k) a[r][kc] = cmk(lk, 0.0);
+        }
       }
     }
   }
@@ -776,26 +783,30 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(cplx* __restrict__ W, in
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int c = 0; c < 4; ++c) x[r][c] = cmk(r0 + r == c0 + c ? 1.0 : 0.0, 0.0);
-  for (int k = 0; k < m; ++k) {
-    const int p = k & 1, kb = k >> 2, kr = k & 3;
-    if (bi == kb) {
-      const double d = 1.0 / Ls[k][k].x;
+  for (int kb = 0; 4 * kb < m; ++kb) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        x[kr][c] = cscale(x[kr][c], d);
-        vec[p][c0 + c] = x[kr][c];
+    for (int kr = 0; kr < 4; ++kr) {
+      const int k = 4 * kb + kr, p = kr & 1;
+      if (k >= m) break;
+      if (bi == kb) {
+        const double d = 1.0 / Ls[k][k].x;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          x[kr][c] = cscale(x[kr][c], d);
+          vec[p][c0 + c] = x[kr][c];
+        }
       }
+      __syncthreads();
+      cplx xk[4], lik[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) xk[c] = vec[p][c0 + c];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lik[r] = (r0 + r > k && r0 + r < m) ? Ls[r0 + r][k] : cmk(0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x[r][c] = csub(x[r][c], cmul(lik[r], xk[c]));
     }
-    __syncthreads();
-    cplx xk[4], lik[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) xk[c] = vec[p][c0 + c];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) lik[r] = (r0 + r > k && r0 + r < m) ? Ls[r0 + r][k] : cmk(0, 0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) x[r][c] = csub(x[r][c], cmul(lik[r], xk[c]));
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r)
