@@ -48,6 +48,7 @@ struct fisdf_ctx {
   cplx* f_L = nullptr;      // (nk, nip, nip) raw left-looking factor (row order)
   cplx* f_Lp = nullptr;     // (nk, nip*nip) pivot-order factor, ld = rank_q
   cplx* f_Linv = nullptr;   // (nk, nblk*nb*nb)
+  bool f_q_partial_last = false;  // f_Q over [0,64),[64,128),.. (unpivoted) or partial block first
   cplx* f_Q = nullptr;      // (nk, nip, nip) block-row operator of trsm_merged (build_trsm_q)
   cplx* f_Li = nullptr;     // (nk, nip, nip) L^{-1} (pivot order) = trsm_merged on the identity
   cplx* f_x4s = nullptr;    // (nk, nip, nip) staged x4_q of the factored slots
@@ -936,11 +937,10 @@ int fisdf_build_x4(fisdf_ctx* c, const void* Xv, int nip, int nao, const int kme
   // x2_k = X_k^* X_k^T  (:38)
   FISDF_TRY(zgemm(c->stream, OP_R, OP_T, nip, nip, nao, ONE, X, nao, (long)nip * nao, X, nao,
                   (long)nip * nao, ZERO, X2k, nip, nn, nk));
-  // x2_s = Phi x2_k  (:41), must be real (:43)
+  // x2_s = Phi x2_k  (:41), must be real (:43), squared in the GEMM's epilogue:
+  // x4_s = x2_s * x2_s (:45), recording max|Im x2_s|
   FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nn, nk, ONE, phase, nk, 0, X2k, nn, 0, ZERO, X2s, nn,
-                  0, 1));
-  // x4_s = x2_s * x2_s (:45); records max|Im x2_s|
-  FISDF_TRY(csquare(c->stream, X2s, nk * nn, c->maximag + 0));
+                  0, 1, 1, nullptr, EPI_CSQUARE, c->maximag + 0));
   // x4_k = Phi^H x4_s (:46)
   FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nk, nn, nk, ONE, phase, nk, 0, X2s, nn, 0, ZERO,
                   (cplx*)x4v, nn, 0, 1));
@@ -1059,7 +1059,11 @@ int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk
 // need_linv: the diagonal-block inverses of Lp (trsm_blocked, used only when some rank < nip;
 // the unpivoted path is full-rank by construction — a failing slot is refactored, and this
 // rerun, by factor_pivoted_slots)
-int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src, bool need_linv) {
+// blkinv: the diagonal-block inverses the unpivoted Cholesky kept (chol_unpivoted keep_blocks),
+// reused for the block-row operator over the partial-last partition; nullptr recomputes them
+// over the partial-first one (pivoted factors)
+int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src, bool need_linv,
+                  const cplx* blkinv = nullptr) {
   const int nk = c->f_nk, nip = c->f_nip, nb = c->f_nb, nblk = (nip + nb - 1) / nb;
   const long nn = (long)nip * nip;
   FISDF_HIP(hipMemcpyAsync(c->f_rank_pinned, rank_dev_src, sizeof(int) * nk, hipMemcpyDeviceToHost, s));
@@ -1071,12 +1075,17 @@ int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src, bool nee
   FISDF_TRY(gather_lp(s, c->f_L, nip, nip, c->f_piv, c->f_rank_dev, nip, c->f_Lp, nk));
   if (need_linv)
     FISDF_TRY(trinv_blocks(s, c->f_Lp, nip, nip, nn, nb, (long)nblk * nb * nb, c->f_Linv, nk));
-  FISDF_TRY(build_trsm_q(s, c->f_Lp, nip, nn, c->f_Q, nk, GEMM_FULL));
+  c->f_q_partial_last = blkinv != nullptr;
+  if (blkinv)
+    FISDF_TRY(build_trsm_q_blocks(s, c->f_Lp, nip, nn, blkinv, c->f_Q, nk));
+  else
+    FISDF_TRY(build_trsm_q(s, c->f_Lp, nip, nn, c->f_Q, nk, GEMM_FULL));
   // L^{-1} by the same block-row substitution applied to the identity (the fit then applies it
   // as one lower-triangular GEMM over the grid; J/K within 2-3x of the TRSM's rounding,
   // tests/experiments/explicit_tri_inverse.py)
   FISDF_TRY(set_identity(s, c->f_Li, nip, nk));
-  FISDF_TRY(trsm_merged_batched(s, c->f_Q, nn, nip, c->f_Li, nip, nn, nip, nk, true));
+  FISDF_TRY(trsm_merged_batched(s, c->f_Q, nn, nip, c->f_Li, nip, nn, nip, nk, true,
+                                c->f_q_partial_last));
   return 0;
 }
 
@@ -1209,7 +1218,7 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   cv.take(sizeof(double) * (size_t)nk * (1 + nip));
   size_t oU = cv.take(sizeof(int) * nk);                                   // unpivoted rank
   size_t oFl = cv.take(sizeof(int) * nk);                                  // unpivoted fail
-  size_t oWk = cv.take(sizeof(cplx) * (size_t)nk * 4096 + sizeof(double) * nk);
+  size_t oWk = cv.take(sizeof(cplx) * (size_t)((nip + 63) / 64) * nk * 4096 + sizeof(double) * nk);
   if (cv.off > c->f_scratch_size) {
     if (c->f_scratch) FISDF_HIP(hipFree(c->f_scratch));
     FISDF_HIP(hipMalloc(&c->f_scratch, cv.off));
@@ -1251,9 +1260,9 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
     // same full-rank verdict the rank-revealing pivoted factorisation gives); any matrix that
     // fails it is redone by the pivoted pchol in fisdf_factor_x4_wait
     FISDF_TRY(chol_unpivoted(s, c->f_L, nip, nk, tol_rel, c->f_piv, (int*)(b + oU),
-                             (int*)(b + oFl), (cplx*)(b + oWk)));
+                             (int*)(b + oFl), (cplx*)(b + oWk), true));
     FISDF_HIP(hipMemcpyAsync(c->f_fail_pinned, b + oFl, sizeof(int) * nk, hipMemcpyDeviceToHost, s));
-    FISDF_TRY(factor_finish(c, s, (const int*)(b + oU), false));
+    FISDF_TRY(factor_finish(c, s, (const int*)(b + oU), false, (const cplx*)(b + oWk)));
     c->f_check_fail = true;
   }
   FISDF_HIP(hipEventRecord(c->ev_fac, s));
@@ -1705,7 +1714,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
         Uq = U;
       } else if (r == nip) {  // merged block-row substitution, in place
         FISDF_TRY(trsm_merged(st, c->f_Q + (long)sl * nn, nip, Yh, ngrid, (int)ncol,
-                              real_q ? GEMM_A_REAL : GEMM_FULL));
+                              real_q ? GEMM_A_REAL : GEMM_FULL, c->f_q_partial_last));
         Uq = Yh;
       } else {
         FISDF_TRY(trsm_blocked(st, 1, Lp, nip, 0, r, Linv, 0, nb, Yh, ngrid, 0, U, ngrid,
@@ -1779,12 +1788,15 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     }
     bool all_full = rmax == nip;
     for (int lq = 0; lq < nq && all_full; ++lq) all_full = c->f_rank[s0 + lq] == nip;
-    if (all_full) {  // with L^{-1} at hand: T = G L^{-1}, W_PP = L^{-H} T (two batched GEMMs)
+    if (all_full) {
+      // with L^{-1} at hand, two batched GEMMs whose A = L^{-H} is upper triangular (each
+      // M-tile starts its K loop at its own row: half the flops of dense GEMMs):
+      //   S = L^{-H} G,  W_PP = L^{-H} S^H  (= L^{-H} G L^{-1}, G Hermitian)
       const cplx* Lf = c->f_Li + (long)s0 * nn;
-      FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nip, nip, nip, ONE, G, rmax, rr, Lf, nip, nn, ZERO,
-                      S, rmax, rr, nq, 1));
-      FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nip, nip, nip, ONE, Lf, nip, nn, S, rmax, rr, ZERO,
-                      T, rmax, rr, nq, 1));
+      FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nip, nip, nip, ONE, Lf, nip, nn, G, rmax, rr, ZERO,
+                      S, rmax, rr, nq, 1, nullptr, EPI_NONE, nullptr, GEMM_A_UPPER));
+      FISDF_TRY(zgemm(c->stream, OP_C, OP_C, nip, nip, nip, ONE, Lf, nip, nn, S, rmax, rr, ZERO,
+                      T, rmax, rr, nq, 1, nullptr, EPI_NONE, nullptr, GEMM_A_UPPER));
     } else {
       FISDF_TRY(trsm_blocked(c->stream, 0, Lp0, nip, nn, rmax, Li0, sLi, nb, G, rmax, rr,
                              T, rmax, rr, rmax, nq));

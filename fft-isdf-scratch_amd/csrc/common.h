@@ -55,13 +55,16 @@ enum Op { OP_N = 0, OP_T = 1, OP_R = 2 /*conj only*/, OP_C = 3 /*conj-transpose*
 // strides sA/sB/sC per batch in complex elements. ksplit>1 uses `work` (ksplit*M*N cplx).
 // epilogues: EPI_STREAM: C = alpha acc (beta = 0) with non-temporal stores (a large output
 // read back only much later, e.g. the y build's fx blocks)
-enum Epi { EPI_NONE = 0, EPI_STREAM = 2 };
+// EPI_CSQUARE: C = (alpha acc)^2 elementwise (beta = 0), max |Im(alpha acc)| recorded in *mon
+enum Epi { EPI_NONE = 0, EPI_STREAM = 2, EPI_CSQUARE = 4 };
 // arithmetic modes (MFMA work skipped): GEMM_A_REAL: Im(op(A)) is taken as zero (2 of the 4
 // real MFMAs per complex block); GEMM_RE_ONLY: only Re(C) is formed (Im(C) written as 0).
 // Supported for (N,N), (C,N) and the HERK; other op pairs require mode 0.
 // GEMM_A_LOWER: op(A) = A (OP_N) is lower triangular: each M-tile stops its K loop at the
 // tile's last row (the zero upper part is never read or multiplied).
-enum GemmMode { GEMM_FULL = 0, GEMM_A_REAL = 1, GEMM_RE_ONLY = 2, GEMM_A_LOWER = 4 };
+// GEMM_A_UPPER: op(A) = A^H (OP_C) is upper triangular (A lower): each M-tile starts its K loop
+// at its own first row (no split-K)
+enum GemmMode { GEMM_FULL = 0, GEMM_A_REAL = 1, GEMM_RE_ONLY = 2, GEMM_A_LOWER = 4, GEMM_A_UPPER = 8 };
 int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha,
           const cplx* A, long lda, long sA, const cplx* B, long ldb, long sB, cplx beta,
           cplx* C, long ldc, long sC, int batch, int ksplit = 1, cplx* work = nullptr,
@@ -83,7 +86,7 @@ int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int
 
 // unpivoted blocked Cholesky (full-rank fast path); see pchol.hip
 int chol_unpivoted(hipStream_t s, cplx* W, int n, int batch, double tol_rel, int* piv, int* rank,
-                   int* fail, cplx* work);
+                   int* fail, cplx* work, bool keep_blocks = false);
 // selection pivots from the real Gram Re(X2)^2*scale (blocked, real; n <= 4096): *handled=false
 // otherwise.  work: n*n + 17*n + 1 doubles; piv (rmax), rank (1), flags (1) device.
 int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rmax, double tol,

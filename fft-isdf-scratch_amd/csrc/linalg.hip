@@ -94,6 +94,20 @@ __global__ __launch_bounds__(64) void trinv_into_kernel(const cplx* __restrict__
     if (j < m) Q[(long)(b0 + i) * ldq + b0 + j] = Xs[i][j];
 }
 
+// Q[b0:b0+m, b0:b0+m] = Bi[blk] (the kept inverse of diagonal block blk = blockIdx.x, rows
+// [64 blk, 64 blk + m)): the diagonal blocks of the partial-last block-row operator
+__global__ __launch_bounds__(256) void place_blkinv_kernel(const cplx* __restrict__ Bi, int r,
+                                                           int batch, cplx* __restrict__ Q, long sQ) {
+  const int blk = blockIdx.x, b = blockIdx.y;
+  const int b0 = 64 * blk, m = min(64, r - b0);
+  const cplx* src = Bi + ((long)blk * batch + b) * 4096;
+  cplx* dst = Q + b * sQ + (long)b0 * r + b0;
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int i = e >> 6, j = e & 63;
+    if (i < m && j < m) dst[(long)i * r + j] = src[e];
+  }
+}
+
 // W[b][piv[b][s]][piv[b][t]] = Wpp[b][s][t] for s,t < rank[b]   (W zeroed beforehand)
 __global__ void scatter_w_kernel(const cplx* __restrict__ Wpp, int ldw, long sW,
                                  const int* __restrict__ piv, const int* __restrict__ rank,
@@ -502,7 +516,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 // and y_{-q} = conj(y_q).  Tile order: XCD-aware (workgroup id & 7 = XCD), an XCD's resident
 // workgroups walk the I-tiles of one g-tile (the f tile stays in its L2).
 // mode (debug timing, FISDF_YF_MODE): bit 0 skips the MFMA phase, bit 1 the DFT + stores.
-constexpr int YF_MAXKS = 8;  // nao <= 32 per K chunk (larger nao loops over chunks)
+constexpr int YF_MAXKS = 7;  // nao <= 28 per K chunk (larger nao loops over chunks)
 struct YfPlan {
   int nA, nB;   // slots of chunk A (complex planes) and B (self-paired planes)
   int kA[16];   // k of each slot, in the kernel's slot order
@@ -522,49 +536,43 @@ __host__ __device__ constexpr int yf_inplane_rank(int bc) {
 
 // fx for the chunk's slots (wave w: slots w, w+4, ...) into buf[slot][256]
 __device__ __forceinline__ void yf_mfma_chunk(const cplx* __restrict__ X, int nip, int nao,
-                                              const cplx* __restrict__ F, long fks,
+                                              const cplx* __restrict__ F, long fks, int m,
                                               const int* ks, int nslot, int Ia, bool okI,
                                               int ga, bool okg, int lane, int w,
                                               cplx* __restrict__ buf) {
   const int i16 = lane & 15, kq = lane >> 4;
   const int nkc = (nao + 4 * YF_MAXKS - 1) / (4 * YF_MAXKS);
-  cplx a[YF_MAXKS], b[YF_MAXKS];
-  auto load = [&](int s, int c) {
+  // two explicit operand buffers: the loads of the next (slot, K-chunk) are in flight across
+  // this one's MFMAs with no register rotation between iterations
+  cplx a0[YF_MAXKS], b0[YF_MAXKS], a1[YF_MAXKS], b1[YF_MAXKS];
+  // Branch-free operand loads: rows past nip / m are clamped to the last valid row (their
+  // columns are never stored) and K past nao to its last element, with the A operand zeroed at
+  // use (a select after the load made the compiler wait for the next slot's loads right after
+  // issuing them, before this slot's MFMAs, exposing the full load latency every slot).  The
+  // slot index is wave-uniform, so ks[s] is a scalar load.
+  const int Ic = min(Ia, nip - 1), gc = min(ga, m - 1);
+  (void)okI;
+  (void)okg;
+  auto load = [&](cplx (&a)[YF_MAXKS], cplx (&b)[YF_MAXKS], int s, int c) {
     const int k = ks[s];
-    const cplx* xa = X + ((long)k * nip + (okI ? Ia : 0)) * nao;
-    const cplx* fb = F + (long)k * fks + (long)(okg ? ga : 0) * nao;
+    const cplx* xa = X + ((long)k * nip + Ic) * nao;
+    const cplx* fb = F + (long)k * fks + (long)gc * nao;
 #pragma unroll
     for (int kk = 0; kk < YF_MAXKS; ++kk) {
-      const int mu = c * 4 * YF_MAXKS + kk * 4 + kq;
-      const bool ok = mu < nao;
-      a[kk] = xa[ok ? mu : 0];
-      b[kk] = fb[ok ? mu : 0];
-      if (!(ok && okI)) a[kk] = cmk(0, 0);
-      if (!(ok && okg)) b[kk] = cmk(0, 0);
+      const int mu = min(c * 4 * YF_MAXKS + kk * 4 + kq, nao - 1);
+      a[kk] = xa[mu];
+      b[kk] = fb[mu];
     }
   };
-  int s = w, c = 0;
-  if (s < nslot) load(s, 0);
   f64x4 t1 = {0, 0, 0, 0}, t2 = {0, 0, 0, 0}, t3 = {0, 0, 0, 0};
-  while (s < nslot) {
-    double ar[YF_MAXKS], ai[YF_MAXKS], as[YF_MAXKS], br[YF_MAXKS], bi[YF_MAXKS], bd[YF_MAXKS];
+  auto mma = [&](const cplx (&a)[YF_MAXKS], const cplx (&b)[YF_MAXKS], int s, int c, int cn) {
 #pragma unroll
     for (int kk = 0; kk < YF_MAXKS; ++kk) {
-      ar[kk] = a[kk].x; ai[kk] = a[kk].y; as[kk] = a[kk].x + a[kk].y;
-      br[kk] = b[kk].x; bi[kk] = b[kk].y; bd[kk] = b[kk].x - b[kk].y;
-    }
-    const int kvalid = min(YF_MAXKS, (nao - c * 4 * YF_MAXKS + 3) / 4);
-    // next (slot, chunk) in flight across this one's MFMAs
-    int sn = s, cn = c + 1;
-    if (cn == nkc) { sn = s + 4; cn = 0; }
-    if (sn < nslot) load(sn, cn);
-#pragma unroll
-    for (int kk = 0; kk < YF_MAXKS; ++kk) {
-      if (kk < kvalid) {
-        t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[kk], br[kk], t1, 0, 0, 0);
-        t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[kk], bi[kk], t2, 0, 0, 0);
-        t3 = __builtin_amdgcn_mfma_f64_16x16x4f64(as[kk], bd[kk], t3, 0, 0, 0);
-      }
+      const bool ok = c * 4 * YF_MAXKS + kk * 4 + kq < nao;
+      const double ar = ok ? a[kk].x : 0.0, ai = ok ? a[kk].y : 0.0, br = b[kk].x, bi = b[kk].y;
+      t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, br, t1, 0, 0, 0);
+      t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, bi, t2, 0, 0, 0);
+      t3 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar + ai, br - bi, t3, 0, 0, 0);
     }
     if (cn == 0) {  // slot complete: C row = Il = kq + 4 r, col = gl = i16
 #pragma unroll
@@ -574,8 +582,31 @@ __device__ __forceinline__ void yf_mfma_chunk(const cplx* __restrict__ X, int ni
       t2 = f64x4{0, 0, 0, 0};
       t3 = f64x4{0, 0, 0, 0};
     }
+  };
+  auto next = [&](int s, int c, int& sn, int& cn) {
+    sn = s;
+    cn = c + 1;
+    if (cn == nkc) { sn = s + 4; cn = 0; }
+  };
+  // the next loads are issued unconditionally (past the last slot they re-read a valid one and
+  // are never used): a conditional load made the compiler's wait counts conservative on the
+  // path that issued them, draining the next slot's loads before this slot's MFMAs
+  int s = __builtin_amdgcn_readfirstlane(w), c = 0, sn, cn;
+  if (s >= nslot) return;
+  load(a0, b0, s, 0);
+  for (;;) {
+    next(s, c, sn, cn);
+    load(a1, b1, min(sn, nslot - 1), sn < nslot ? cn : 0);
+    mma(a0, b0, s, c, cn);
     s = sn;
     c = cn;
+    if (s >= nslot) break;
+    next(s, c, sn, cn);
+    load(a0, b0, min(sn, nslot - 1), sn < nslot ? cn : 0);
+    mma(a1, b1, s, c, cn);
+    s = sn;
+    c = cn;
+    if (s >= nslot) break;
   }
 }
 
@@ -608,7 +639,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   double tr[NR][P];         // t_0 (, t_{N0/2})
   // ---- chunk A: the complex plane a = 1 ----
   if constexpr (NC > 0) {
-    if (!(mode & 1)) yf_mfma_chunk(X, nip, nao, F, fks, plan.kA, plan.nA, Ia, okI, ga, okg, lane, w, buf);
+    if (!(mode & 1)) yf_mfma_chunk(X, nip, nao, F, fks, m, plan.kA, plan.nA, Ia, okI, ga, okg, lane, w, buf);
     __syncthreads();
 #pragma unroll
     for (int bc = 0; bc < P; ++bc) tc[bc] = (mode & 1) ? cmk(0, 0) : buf[bc * 256 + tid];
@@ -617,7 +648,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __syncthreads();  // buf is rewritten by chunk B
   }
   // ---- chunk B: the self-paired planes, half their k each ----
-  if (!(mode & 1)) yf_mfma_chunk(X, nip, nao, F, fks, plan.kB, plan.nB, Ia, okI, ga, okg, lane, w, buf);
+  if (!(mode & 1)) yf_mfma_chunk(X, nip, nao, F, fks, m, plan.kB, plan.nB, Ia, okI, ga, okg, lane, w, buf);
   __syncthreads();
   if (mode & 2) return;
 #pragma unroll
@@ -790,16 +821,37 @@ int build_trsm_q(hipStream_t s, const cplx* Lp, int r, long sL, cplx* Q, int bat
   return 0;
 }
 
+// The same operator over the partition [0, 64), [64, 128), ..., [64 (nblk-1), r) (partial block
+// last) from the diagonal-block inverses the unpivoted Cholesky kept (chol_unpivoted with
+// keep_blocks: block k at Bi + k*batch*4096, ld 64): no triangular inverse is recomputed.
+int build_trsm_q_blocks(hipStream_t s, const cplx* Lp, int r, long sL, const cplx* Bi, cplx* Q,
+                        int batch) {
+  const int nblk = (r + 63) / 64;
+  if (nblk == 0 || batch == 0) return 0;
+  const long rr = (long)r * r;
+  hipLaunchKernelGGL(place_blkinv_kernel, dim3(nblk, batch), dim3(256), 0, s, Bi, r, batch, Q, rr);
+  FISDF_HIP(hipGetLastError());
+  const cplx mone = cmk(-1, 0), zero = cmk(0, 0);
+  for (int b = 1; b < nblk; ++b) {
+    const int b0 = 64 * b, m = std::min(64, r - b0);
+    FISDF_TRY(zgemm(s, OP_N, OP_N, m, b0, m, mone, Bi + (long)b * batch * 4096, 64, 4096,
+                    Lp + (long)b0 * r, r, sL, zero, Q + (long)b0 * r, r, rr, batch, 1));
+  }
+  return 0;
+}
+
 // X = L^{-1} X in place for X (r x ncol, ld): one GEMM per block row with the Q of
 // build_trsm_q, X[b] = Q[b, :b1] X[:b1] — each workgroup owns whole columns (M <= 64), so
 // it reads all of X[:b1] for its columns before its epilogue overwrites X[b].
-int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol, int mode) {
+int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol, int mode,
+                bool partial_last) {
   const int nblk = (r + 63) / 64;
   if (nblk == 0) return 0;
-  const int s0 = r - 64 * (nblk - 1);
+  const int s0 = partial_last ? 64 : r - 64 * (nblk - 1);
   const cplx one = cmk(1, 0), zero = cmk(0, 0);
   for (int b = 0; b < nblk; ++b) {
-    const int b0 = b == 0 ? 0 : s0 + (b - 1) * 64, m = b == 0 ? s0 : 64, b1 = b0 + m;
+    const int b0 = b == 0 ? 0 : s0 + (b - 1) * 64;
+    const int m = std::min(b == 0 ? s0 : 64, r - b0), b1 = b0 + m;
     FISDF_TRY(zgemm(s, OP_N, OP_N, m, ncol, b1, one, Q + (long)b0 * r, r, 0, X, ld, 0, zero,
                     X + (long)b0 * ld, ld, 0, 1, 1, nullptr, EPI_NONE, nullptr, mode));
   }
@@ -810,13 +862,14 @@ int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol,
 // lower_rhs: X is lower-triangular (the identity, for L^{-1}), so block row b only has
 // columns < b1 to compute (the rest stay zero)
 int trsm_merged_batched(hipStream_t s, const cplx* Q, long sQ, int r, cplx* X, long ld, long sX,
-                        int ncol, int batch, bool lower_rhs) {
+                        int ncol, int batch, bool lower_rhs, bool partial_last) {
   const int nblk = (r + 63) / 64;
   if (nblk == 0 || batch == 0) return 0;
-  const int s0 = r - 64 * (nblk - 1);
+  const int s0 = partial_last ? 64 : r - 64 * (nblk - 1);
   const cplx one = cmk(1, 0), zero = cmk(0, 0);
   for (int b = 0; b < nblk; ++b) {
-    const int b0 = b == 0 ? 0 : s0 + (b - 1) * 64, m = b == 0 ? s0 : 64, b1 = b0 + m;
+    const int b0 = b == 0 ? 0 : s0 + (b - 1) * 64;
+    const int m = std::min(b == 0 ? s0 : 64, r - b0), b1 = b0 + m;
     FISDF_TRY(zgemm(s, OP_N, OP_N, m, lower_rhs ? std::min(ncol, b1) : ncol, b1, one,
                     Q + (long)b0 * r, r, sQ, X, ld, sX, zero, X + (long)b0 * ld, ld, sX, batch, 1));
   }

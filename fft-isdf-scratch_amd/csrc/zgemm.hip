@@ -115,6 +115,27 @@ __device__ __forceinline__ void zgemm_epilogue(int M, int N, cplx alpha, cplx be
         }
     return;
   }
+  if (epi == EPI_CSQUARE) {  // C = (alpha acc)^2 elementwise; max |Im(alpha acc)| -> *mon
+    double mx = 0.0;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
+          int col = n0 + wn + ni * 16 + (lane & 15);
+          if (((mask >> (mi * 2 + ni)) & 1) && row < M && col < N) {
+            const cplx v = cmul(alpha, cmk(accR[mi][ni][r], accI[mi][ni][r]));
+            mx = fmax(mx, fabs(v.y));
+            C[(long)row * ldc + col] = cmul(v, v);
+          }
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0 && mon) atomicMax(mon, (unsigned long long)__double_as_longlong(mx));
+    return;
+  }
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -336,9 +357,10 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
     tj = t - ti * (ti + 1) / 2;
   }
   const int m0 = ti * BM, n0 = tj * BN;
-  const int kbeg = split * kchunk;
+  int kbeg = split * kchunk;
   int kend = min(K, kbeg + kchunk);
   if constexpr ((MODE & GEMM_A_LOWER) != 0) kend = min(kend, m0 + BM);  // A[m][k] = 0 for k > m
+  if constexpr ((MODE & GEMM_A_UPPER) != 0) kbeg = max(kbeg, m0);        // A[m][k] = 0 for k < m
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // wave -> sub-tile: the role rotates with the tile so idle roles spread over the SIMDs.
@@ -674,9 +696,12 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
           long sC, int batch, int ksplit, cplx* work, int epi, unsigned long long* mon, int mode) {
   FISDF_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 0, "zgemm: negative size");
   FISDF_CHECK(opA >= 0 && opA < 4 && opB >= 0 && opB < 4, "zgemm: bad op");
-  FISDF_CHECK(mode >= 0 && mode <= 7, "zgemm: bad mode");
-  FISDF_CHECK(mode == GEMM_FULL || (opB == OP_N && (opA == OP_N || opA == OP_C)),
+  FISDF_CHECK(mode >= 0 && mode <= 8, "zgemm: bad mode");
+  FISDF_CHECK(mode == GEMM_FULL || mode == GEMM_A_UPPER ||
+                  (opB == OP_N && (opA == OP_N || opA == OP_C)),
               "zgemm: real modes are implemented for (N,N) and (C,N) only");
+  FISDF_CHECK(mode != GEMM_A_UPPER || (opA == OP_C && ksplit <= 1),
+              "zgemm: GEMM_A_UPPER is implemented for op(A) = A^H without split-K");
   FISDF_CHECK(!(mode & GEMM_A_LOWER) || (opA == OP_N && opB == OP_N && !(mode & GEMM_RE_ONLY)),
               "zgemm: GEMM_A_LOWER is implemented for (N,N), optionally with GEMM_A_REAL");
   if (M == 0 || N == 0 || batch == 0) return 0;
@@ -703,6 +728,7 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
   FISDF_MCASE(0, 0, 1) FISDF_MCASE(0, 0, 2) FISDF_MCASE(0, 0, 3)
   FISDF_MCASE(0, 0, 4) FISDF_MCASE(0, 0, 5)
   FISDF_MCASE(3, 0, 1) FISDF_MCASE(3, 0, 2) FISDF_MCASE(3, 0, 3)
+  FISDF_MCASE(3, 0, 8) FISDF_MCASE(3, 3, 8)
 #undef FISDF_MCASE
   if (mode == GEMM_FULL) switch (opA * 4 + opB) {
     FISDF_CASE(0, 0) FISDF_CASE(0, 1) FISDF_CASE(0, 2) FISDF_CASE(0, 3)

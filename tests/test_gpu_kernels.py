@@ -209,12 +209,14 @@ def test_min_norm_operator(env, real):
         assert abs(M.imag).max() == 0.0
 
 
-@pytest.mark.parametrize("kmesh", [(1, 1, 3), (3, 1, 2), (2, 3, 1), (4, 4, 4)])
-def test_build_y_kmesh_paths(env, kmesh):
+@pytest.mark.parametrize("kmesh,npts", [((1, 1, 3), 24), ((3, 1, 2), 24), ((2, 3, 1), 24),
+                                        ((4, 4, 4), 24), ((4, 4, 4), 200)])
+def test_build_y_kmesh_paths(env, kmesh, npts):
     """fisdf_build_y on the generic LDS k-mesh kernel ((1,1,3), (3,1,2), (2,3,1)) and the
-    register one (4x4x4), with fx stored for every k and for the time-reversal
-    representatives k <= -k only (fisdf_set_time_reversal), against the oracle's y
-    (fftisdf.py:73-85)."""
+    register / fused one (4x4x4; 200 points = 13 I-tiles, more than one I-group of the fused
+    kernel's tile order, the last one partial), with fx stored for every k and for the
+    time-reversal representatives k <= -k only (fisdf_set_time_reversal), against the oracle's
+    y (fftisdf.py:73-85)."""
     torch, L, ctx = env
     import os, sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -224,7 +226,7 @@ def test_build_y_kmesh_paths(env, kmesh):
     coords = cell.gen_uniform_grids(cell.mesh)
     chi = Cm.eval_ao_kpts(cell, coords, kmesh)            # (nk, ngrid, nao)
     nk, ngrid, nao = chi.shape
-    pts = np.random.default_rng(5).choice(ngrid, 24, replace=False)
+    pts = np.random.default_rng(5).choice(ngrid, npts, replace=False)
     xip = np.ascontiguousarray(chi[:, pts, :])
     phase = R.get_phase(cell.a, R.get_kpts(cell.a, kmesh), kmesh)
     ref = R.build_y(chi, xip, phase)                       # (nk, ngrid, nip)
