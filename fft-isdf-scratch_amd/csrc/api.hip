@@ -1860,19 +1860,18 @@ int fisdf_build_ws_qs(fisdf_ctx* c, const void* Wqv, const int* h_qs, const doub
     }
   }
   Carver cv;
-  size_t oT = cv.take(sizeof(cplx) * nk * nn);
   size_t oP = cv.take(sizeof(cplx) * ph.size());
   void* base;
   FISDF_TRY(arena_get(c, cv.off, &base));
-  cplx* tmp = (cplx*)((char*)base + oT);
   cplx* dph = (cplx*)((char*)base + oP);
   FISDF_HIP(hipMemcpyAsync(dph, ph.data(), sizeof(cplx) * ph.size(), hipMemcpyHostToDevice,
                            c->stream));
-  // ws = Phi W (:205), real part * sqrt(nk) (:207).  With time-reversal representatives the
-  // partner -q contributes conj(Phi[R,q] W_q), so Re(.) of the pair is 2 Re(Phi[R,q] W_q): wt = 2.
-  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nn, nq, ONE, dph, nq, 0, (const cplx*)Wqv, nn, 0,
-                  ZERO, tmp, nn, 0, 1));
-  FISDF_TRY(real_part(c->stream, tmp, std::sqrt((double)nk), (cplx*)Wsv, nk * nn, nullptr));
+  // ws = Phi W (:205), real part * sqrt(nk) (:207) in the GEMM's epilogue.  With time-reversal
+  // representatives the partner -q contributes conj(Phi[R,q] W_q), so Re(.) of the pair is
+  // 2 Re(Phi[R,q] W_q): wt = 2.
+  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nn, nq, cmk(std::sqrt((double)nk), 0), dph, nq, 0,
+                  (const cplx*)Wqv, nn, 0, ZERO, (cplx*)Wsv, nn, 0, 1, 1, nullptr, EPI_REAL,
+                  nullptr));
   FISDF_HIP(hipStreamSynchronize(c->stream));  // ph staging
   return 0;
 }
@@ -2055,17 +2054,16 @@ int fisdf_get_k_rows(fisdf_ctx* c, const void* Xv, const void* Wsv, const void* 
                     ZERO, T, nao, ba, nk));
     FISDF_TRY(zgemm(c->stream, OP_N, OP_T, nb, nip, nao, ONE, T, nao, ba, X, nao, xs, ZERO, B1,
                     nip, bn, nk));
-    // rho_s = Phi rho_k (:215), real (:216)
+    // rho_s = Phi rho_k (:215), real (:216), and V_s = W_s * rho_s^T (:219) for the block rows,
+    // both in the GEMM's epilogue (EPI_WSRHO: Re(W_s) Re(.), max |Im rho_s| recorded)
     FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, bn, nk, ONE, phase, nk, 0, B1, bn, 0, ZERO, B2, bn,
-                    0, 1));
-    FISDF_TRY(real_part(c->stream, B2, 1.0, B2, nk * bn, c->maximag + 2));
-    // V_s = W_s * rho_s^T (:219), block rows
-    FISDF_TRY(ws_times_rho_rows(c->stream, Ws, B2, nk, nip, i0, nb, B1));
+                    0, 1, 1, (cplx*)(Ws + (long)i0 * nip), EPI_WSRHO, c->maximag + 2, GEMM_FULL,
+                    (long)nip * nip));
     // V_k = Phi^T V_s (:222)
-    FISDF_TRY(zgemm(c->stream, OP_T, OP_N, nk, bn, nk, ONE, phase, nk, 0, B1, bn, 0, ZERO, B2, bn,
+    FISDF_TRY(zgemm(c->stream, OP_T, OP_N, nk, bn, nk, ONE, phase, nk, 0, B2, bn, 0, ZERO, B1, bn,
                     0, 1));
     // K_k (block part) = X_k[I]^H (V_k[I, :] X_k)  (:225)
-    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nb, nao, nip, ONE, B2, nip, bn, X, nao, xs, ZERO, T,
+    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nb, nao, nip, ONE, B1, nip, bn, X, nao, xs, ZERO, T,
                     nao, ba, nk));
     FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nao, nao, nb, ONE, Xb, nao, xs, T, nao, ba, ZERO,
                     vk + (long)x * nk * ds, nao, ds, nk));

@@ -56,7 +56,9 @@ enum Op { OP_N = 0, OP_T = 1, OP_R = 2 /*conj only*/, OP_C = 3 /*conj-transpose*
 // epilogues: EPI_STREAM: C = alpha acc (beta = 0) with non-temporal stores (a large output
 // read back only much later, e.g. the y build's fx blocks)
 // EPI_CSQUARE: C = (alpha acc)^2 elementwise (beta = 0), max |Im(alpha acc)| recorded in *mon
-enum Epi { EPI_NONE = 0, EPI_STREAM = 2, EPI_CSQUARE = 4 };
+// EPI_REAL: C = Re(alpha acc) + 0i; EPI_WSRHO: C = Re(aux) Re(alpha acc) + 0i with aux passed
+// as `work` (row stride ldaux); both record max |Im(alpha acc)| in *mon (nullable)
+enum Epi { EPI_NONE = 0, EPI_STREAM = 2, EPI_CSQUARE = 4, EPI_REAL = 5, EPI_WSRHO = 6 };
 // arithmetic modes (MFMA work skipped): GEMM_A_REAL: Im(op(A)) is taken as zero (2 of the 4
 // real MFMAs per complex block); GEMM_RE_ONLY: only Re(C) is formed (Im(C) written as 0).
 // Supported for (N,N), (C,N) and the HERK; other op pairs require mode 0.
@@ -68,7 +70,8 @@ enum GemmMode { GEMM_FULL = 0, GEMM_A_REAL = 1, GEMM_RE_ONLY = 2, GEMM_A_LOWER =
 int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha,
           const cplx* A, long lda, long sA, const cplx* B, long ldb, long sB, cplx beta,
           cplx* C, long ldc, long sC, int batch, int ksplit = 1, cplx* work = nullptr,
-          int epi = EPI_NONE, unsigned long long* mon = nullptr, int mode = GEMM_FULL);
+          int epi = EPI_NONE, unsigned long long* mon = nullptr, int mode = GEMM_FULL,
+          long ldaux = 0);
 
 // C = alpha A A^H (Hermitian rank-K update; lower tiles computed, upper mirrored)
 int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cplx* C, long ldc,

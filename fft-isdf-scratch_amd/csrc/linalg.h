@@ -60,15 +60,11 @@ int conj_transpose(hipStream_t s, const cplx* A, int n, long sA, cplx* B, int ba
 int coulg_weight(hipStream_t s, const int mesh[3], const CellGeom& g, const double k[3],
                  double scale, int take_sqrt, double* w, double omega = 0.0);
 int square_real(hipStream_t s, const cplx* in, cplx* out, long n, unsigned long long* maximag);
-int real_part(hipStream_t s, const cplx* in, double scale, cplx* out, long n,
-              unsigned long long* maximag);
 int csquare(hipStream_t s, cplx* a, long n, unsigned long long* maximag);
 int rho_diag(hipStream_t s, const cplx* T, const cplx* X, int nset, int nk, int nip, int nao,
              double scale, cplx* rho);
 int scale_rows(hipStream_t s, const cplx* X, const cplx* v, int nset, int nk, int nip, int i0,
                int nb, int nao, cplx* Xv);
-int ws_times_rho_rows(hipStream_t s, const cplx* ws, const cplx* rhoT, int nimg, int nip, int i0,
-                      int nb, cplx* V);
 int gather_points(hipStream_t s, const cplx* x0, int nk, int ng0, int nao, const int* perm,
                   int nip, cplx* X);
 int square_scale(hipStream_t s, const cplx* in, double sc, cplx* out, long n);

@@ -201,48 +201,28 @@ __global__ void square_real_kernel(const cplx* __restrict__ in, cplx* __restrict
 }
 
 // out[R,I,J] = scale * Re(in[R,I,J]) (+0i);  records max |Im|
-__global__ void real_part_kernel(const cplx* __restrict__ in, double scale, cplx* __restrict__ out,
-                                 long n, unsigned long long* __restrict__ maximag) {
-  double mi = 0.0;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
-    cplx v = in[e];
-    out[e] = cmk(v.x * scale, 0.0);
-    mi = fmax(mi, fabs(v.y));
+// rho[x, I] = scale * sum_{k,n} T[x,k,I,n] conj(X[k,I,n]): one wave per (x, I), lanes over the
+// (k, n) pairs, fixed-order shuffle reduction (one thread per (x, I) left 10 waves on the chip)
+__global__ __launch_bounds__(64) void rho_diag_kernel(const cplx* __restrict__ T,
+                                                      const cplx* __restrict__ X, int nset, int nk,
+                                                      int nip, int nao, double scale,
+                                                      cplx* __restrict__ rho) {
+  const long e = blockIdx.x;
+  if (e >= (long)nset * nip) return;
+  const int x = (int)(e / nip), I = (int)(e % nip), lane = threadIdx.x;
+  double sr = 0, si = 0;
+  for (int t = lane; t < nk * nao; t += 64) {
+    const int k = t / nao, n = t - k * nao;
+    const cplx a = T[(((long)x * nk + k) * nip + I) * nao + n], b = X[((long)k * nip + I) * nao + n];
+    sr += a.x * b.x + a.y * b.y;
+    si += a.y * b.x - a.x * b.y;
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mi = fmax(mi, __shfl_xor(mi, o, 64));
-  if ((threadIdx.x & 63) == 0 && maximag) atomicMax(maximag, (unsigned long long)__double_as_longlong(mi));
-}
-
-// V[R,I,J] = Ws[R,I,J] * Re(rho[R,J,I])   (fftisdf.py:219)
-// V[R][i][j] = Re(ws[R][i0+i][j]) * Re(rhoT[R][i][j]) for a block of nb rows (fftisdf.py:219
-// with rho_s transposed at its source, so the product is element-wise)
-__global__ void ws_times_rho_rows_kernel(const cplx* __restrict__ ws, const cplx* __restrict__ rhoT,
-                                         int nimg, int nip, int i0, int nb, cplx* __restrict__ V) {
-  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  const long per = (long)nb * nip;
-  if (e >= (long)nimg * per) return;
-  const long R = e / per, r = e % per;
-  V[e] = cmk(ws[R * nip * nip + (long)i0 * nip + r].x * rhoT[e].x, 0.0);
-}
-
-// rho[x,I] = scale * sum_k sum_n T[x,k,I,n] conj(X[k,I,n])
-__global__ void rho_diag_kernel(const cplx* __restrict__ T, const cplx* __restrict__ X, int nset,
-                                int nk, int nip, int nao, double scale, cplx* __restrict__ rho) {
-  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  if (e >= (long)nset * nip) return;
-  int x = (int)(e / nip), I = (int)(e % nip);
-  double sr = 0, si = 0;
-  for (int k = 0; k < nk; ++k) {
-    const cplx* t = T + (((long)x * nk + k) * nip + I) * nao;
-    const cplx* xr = X + ((long)k * nip + I) * nao;
-    for (int n = 0; n < nao; ++n) {
-      cplx a = t[n], b = xr[n];
-      sr += a.x * b.x + a.y * b.y;
-      si += a.y * b.x - a.x * b.y;
-    }
+  for (int o = 32; o > 0; o >>= 1) {
+    sr += __shfl_xor(sr, o, 64);
+    si += __shfl_xor(si, o, 64);
   }
-  rho[e] = cmk(sr * scale, si * scale);
+  if (lane == 0) rho[e] = cmk(sr * scale, si * scale);
 }
 
 // Xv[x,k,I,n] = v[x,I] * X[k,I,n]
@@ -614,7 +594,7 @@ template <int N0, int N1, int N2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void y_fused_kernel(
     const cplx* __restrict__ X, int nip, int nao, const cplx* __restrict__ F, long fks, int m,
     int nIt, int nGt, YfPlan plan, unsigned long long qmask, cplx* __restrict__ yT, long qs,
-    long Is, long goff, int mode) {
+    long Is, long goff, int mode, int gpair) {
   constexpr int P = N1 * N2, NK = N0 * P;
   constexpr int R = yf_inplane_rank<N1, N2>(P);         // in-plane representatives
   constexpr int NC = (N0 - 1) / 2;                        // complex planes 1..NC (N0 <= 4: 0 or 1)
@@ -622,8 +602,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   static_assert(N0 <= 4 && NC <= 1, "y_fused: k-mesh axis 0 must be <= 4");
   extern __shared__ cplx buf[];  // [slot][256]: column c = Il * 16 + gl
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // XCD x walks its g-tiles (gt = x mod 8) in groups of gpair: within a group the I-tiles go
+  // slowest, so the workgroups of one I-tile (same X panels) run back to back
   const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-  const int gt = (j / nIt) * 8 + xcd, it = j % nIt;
+  const int grp = j / (nIt * gpair), rem = j - grp * nIt * gpair;
+  const int it = rem / gpair, gt = (grp * gpair + rem % gpair) * 8 + xcd;
   if (gt >= nGt) return;
   const int I0 = it * 16, g0 = gt * 16;
   const int Ia = I0 + (lane & 15), ga = g0 + (lane & 15);
@@ -1325,15 +1308,6 @@ int square_real(hipStream_t s, const cplx* in, cplx* out, long n, unsigned long 
   return 0;
 }
 
-int real_part(hipStream_t s, const cplx* in, double scale, cplx* out, long n,
-              unsigned long long* maximag) {
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(real_part_kernel, dim3(nblocks(n, 256, 8192)), dim3(256), 0, s, in, scale,
-                     out, n, maximag);
-  FISDF_HIP(hipGetLastError());
-  return 0;
-}
-
 int csquare(hipStream_t s, cplx* a, long n, unsigned long long* maximag) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(csquare_kernel, dim3(nblocks(n, 256, 8192)), dim3(256), 0, s, a, n, maximag);
@@ -1345,18 +1319,9 @@ int rho_diag(hipStream_t s, const cplx* T, const cplx* X, int nset, int nk, int 
              double scale, cplx* rho) {
   long n = (long)nset * nip;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(rho_diag_kernel, dim3(nblocks(n, 64, 1L << 30)), dim3(64), 0, s, T, X, nset,
+  FISDF_CHECK(n < (1L << 31), "rho_diag: too many rows");
+  hipLaunchKernelGGL(rho_diag_kernel, dim3((unsigned)n), dim3(64), 0, s, T, X, nset,
                      nk, nip, nao, scale, rho);
-  FISDF_HIP(hipGetLastError());
-  return 0;
-}
-
-int ws_times_rho_rows(hipStream_t s, const cplx* ws, const cplx* rhoT, int nimg, int nip, int i0,
-                      int nb, cplx* V) {
-  long n = (long)nimg * nb * nip;
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(ws_times_rho_rows_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s,
-                     ws, rhoT, nimg, nip, i0, nb, V);
   FISDF_HIP(hipGetLastError());
   return 0;
 }
@@ -1471,7 +1436,8 @@ int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long 
   const size_t lds = sizeof(cplx) * 256 * (size_t)std::max(plan.nA, plan.nB);
   if (lds > 80 * 1024) return 0;
   const int nIt = (nip + 15) / 16, nGt = (m + 15) / 16;
-  const long grid = (long)nIt * ((nGt + 7) / 8) * 8;
+  static const int gpair = std::max(1, getenv("FISDF_YF_GPAIR") ? atoi(getenv("FISDF_YF_GPAIR")) : 1);
+  const long grid = (long)nIt * ((nGt + 8 * gpair - 1) / (8 * gpair)) * gpair * 8;
   FISDF_CHECK(grid < (1L << 31), "y_fused: grid too large");
   static const int mode = getenv("FISDF_YF_MODE") ? atoi(getenv("FISDF_YF_MODE")) : 0;
 #define FISDF_YF(a, b, c)                                                                      \
@@ -1483,7 +1449,7 @@ int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long 
       attr = true;                                                                             \
     }                                                                                          \
     hipLaunchKernelGGL((y_fused_kernel<a, b, c>), dim3((unsigned)grid), dim3(256), lds, s, X,   \
-                       nip, nao, F, fks, m, nIt, nGt, plan, qmask, yT, qs, Is, goff, mode);     \
+                       nip, nao, F, fks, m, nIt, nGt, plan, qmask, yT, qs, Is, goff, mode, gpair); \
     FISDF_HIP(hipGetLastError());                                                              \
     *handled = true;                                                                           \
     return 0;                                                                                  \

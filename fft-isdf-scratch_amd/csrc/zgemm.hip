@@ -76,7 +76,8 @@ template <bool HERK>
 __device__ __forceinline__ void zgemm_epilogue(int M, int N, cplx alpha, cplx beta,
                                                cplx* __restrict__ C, long ldc, long sC, int ksplit,
                                                int split, int bz, cplx* __restrict__ work, int epi,
-                                               unsigned long long* __restrict__ mon, int m0, int n0,
+                                               unsigned long long* __restrict__ mon, long ldaux,
+                                               int m0, int n0,
                                                int wm, int wn, int lane, int mask,
                                                const f64x4 (&accR)[2][2], const f64x4 (&accI)[2][2]) {
   if (ksplit > 1) {
@@ -113,6 +114,30 @@ __device__ __forceinline__ void zgemm_epilogue(int M, int N, cplx alpha, cplx be
             __builtin_nontemporal_store(v.y, cp + 1);
           }
         }
+    return;
+  }
+  if (epi == EPI_REAL || epi == EPI_WSRHO) {
+    // EPI_REAL: C = Re(alpha acc) + 0i; EPI_WSRHO: C = Re(aux[row][col]) Re(alpha acc) + 0i
+    // (aux = work, row stride ldaux); both record max |Im(alpha acc)| in *mon
+    double mx = 0.0;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int row = m0 + wm + mi * 16 + (lane >> 4) + 4 * r;
+          int col = n0 + wn + ni * 16 + (lane & 15);
+          if (((mask >> (mi * 2 + ni)) & 1) && row < M && col < N) {
+            const cplx v = cmul(alpha, cmk(accR[mi][ni][r], accI[mi][ni][r]));
+            mx = fmax(mx, fabs(v.y));
+            const double f = epi == EPI_WSRHO ? work[(long)row * ldaux + col].x : 1.0;
+            C[(long)row * ldc + col] = cmk(f * v.x, 0.0);
+          }
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0 && mon) atomicMax(mon, (unsigned long long)__double_as_longlong(mx));
     return;
   }
   if (epi == EPI_CSQUARE) {  // C = (alpha acc)^2 elementwise; max |Im(alpha acc)| -> *mon
@@ -172,7 +197,7 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx al
                                                     const cplx* __restrict__ B, long ldb, long sB,
                                                     cplx beta, cplx* __restrict__ C, long ldc, long sC,
                                                     int ksplit, int kchunk, cplx* __restrict__ work,
-                                                    int epi, unsigned long long* __restrict__ mon,
+                                                    int epi, unsigned long long* __restrict__ mon, long ldaux,
                                                     int nMt, int ntile, int ntot) {
   constexpr bool AK = !(OPA & 1);  // A stored [m][k]
   constexpr bool BKc = (OPB & 1);  // B stored [n][k]
@@ -296,7 +321,7 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx al
       const int r0 = m0 + wm + mi * 16, c0 = n0 + wn + ni * 16;
       mask |= (r0 < M && c0 < N && !(HERK && c0 > r0) ? 1 : 0) << (mi * 2 + ni);
     }
-  zgemm_epilogue<HERK>(M, N, alpha, beta, C, ldc, sC, ksplit, split, bz, work, epi, mon, m0, n0, wm,
+  zgemm_epilogue<HERK>(M, N, alpha, beta, C, ldc, sC, ksplit, split, bz, work, epi, mon, ldaux, m0, n0, wm,
                        wn, lane, mask, accR, accI);
 }
 
@@ -328,7 +353,7 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
                                                          const cplx* __restrict__ B, long ldb, long sB,
                                                          cplx beta, cplx* __restrict__ C, long ldc, long sC,
                                                          int ksplit, int kchunk, cplx* __restrict__ work,
-                                                         int epi, unsigned long long* __restrict__ mon,
+                                                         int epi, unsigned long long* __restrict__ mon, long ldaux,
                                                          int nMt, int ntile, int ntot) {
   constexpr bool AK = !(OPA & 1);  // A stored [m][k]
   constexpr bool BKc = (OPB & 1);  // B stored [n][k]
@@ -603,7 +628,7 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
         }
   }
 
-  zgemm_epilogue<HERK>(M, N, alpha, beta, C, ldc, sC, ksplit, split, bz, work, epi, mon, m0, n0, wm,
+  zgemm_epilogue<HERK>(M, N, alpha, beta, C, ldc, sC, ksplit, split, bz, work, epi, mon, ldaux, m0, n0, wm,
                        wn, lane, mask, accR, accI);
 }
 
@@ -667,7 +692,7 @@ int gemm_variant() {
 template <int OPA, int OPB, bool HERK = false, int MODE = GEMM_FULL>
 void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cplx* A, long lda,
             long sA, const cplx* B, long ldb, long sB, cplx beta, cplx* C, long ldc, long sC,
-            int ksplit, int kchunk, cplx* work, int epi, unsigned long long* mon) {
+            int ksplit, int kchunk, cplx* work, int epi, unsigned long long* mon, long ldaux) {
   // grid = (N-tiles or triangle tiles, M-tiles, z-slices) -> padded 1-D XCD-aware order
   const int nMt = HERK ? 1 : (int)grid.y;
   const int ntile = (int)(grid.x * (HERK ? 1 : grid.y));
@@ -678,22 +703,23 @@ void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cpl
   if ((gemm_variant() == 1 || MODE != GEMM_FULL) && kchunk <= 4 * BK)
     hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, 2>), dim3((unsigned)(8 * per)),
                        dim3(256), 0, s, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
-                       ksplit, kchunk, work, epi, mon, nMt, ntile, (int)ntot);
+                       ksplit, kchunk, work, epi, mon, ldaux, nMt, ntile, (int)ntot);
   else if (gemm_variant() == 1 || MODE != GEMM_FULL)
     hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, NST>), dim3((unsigned)(8 * per)), dim3(256), 0,
                        s, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk,
-                       work, epi, mon, nMt, ntile, (int)ntot);
+                       work, epi, mon, ldaux, nMt, ntile, (int)ntot);
   else
     hipLaunchKernelGGL((zgemm_kernel<OPA, OPB, HERK>), dim3((unsigned)(8 * per)), dim3(256), 0, s, M,
                        N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work,
-                       epi, mon, nMt, ntile, (int)ntot);
+                       epi, mon, ldaux, nMt, ntile, (int)ntot);
 }
 
 }  // namespace
 
 int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, const cplx* A,
           long lda, long sA, const cplx* B, long ldb, long sB, cplx beta, cplx* C, long ldc,
-          long sC, int batch, int ksplit, cplx* work, int epi, unsigned long long* mon, int mode) {
+          long sC, int batch, int ksplit, cplx* work, int epi, unsigned long long* mon, int mode,
+          long ldaux) {
   FISDF_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 0, "zgemm: negative size");
   FISDF_CHECK(opA >= 0 && opA < 4 && opB >= 0 && opB < 4, "zgemm: bad op");
   FISDF_CHECK(mode >= 0 && mode <= 8, "zgemm: bad mode");
@@ -718,12 +744,12 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
 #define FISDF_CASE(a, b)                                                                      \
   case a * 4 + b:                                                                             \
     launch<a, b>(s, grid, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit,   \
-                 kchunk, work, epi, mon);                                                     \
+                 kchunk, work, epi, mon, ldaux);                                              \
     break;
 #define FISDF_MCASE(a, b, m)                                                                  \
   if (opA == a && opB == b && mode == m) {                                                    \
     launch<a, b, false, m>(s, grid, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, \
-                           ksplit, kchunk, work, epi, mon);                                   \
+                           ksplit, kchunk, work, epi, mon, ldaux);                            \
   }
   FISDF_MCASE(0, 0, 1) FISDF_MCASE(0, 0, 2) FISDF_MCASE(0, 0, 3)
   FISDF_MCASE(0, 0, 4) FISDF_MCASE(0, 0, 5)
@@ -764,10 +790,10 @@ int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cpl
   if (mode == GEMM_RE_ONLY)  // C = Re(A A^H): 2 of the 4 MFMAs per complex block
     launch<OP_N, OP_C, true, GEMM_RE_ONLY>(s, grid, n, n, K, cmk(alpha, 0), A, lda, 0, A, lda, 0,
                                            cmk(0, 0), C, ldc, 0, ksplit, kchunk, work, EPI_NONE,
-                                           nullptr);
+                                           nullptr, 0);
   else
     launch<OP_N, OP_C, true>(s, grid, n, n, K, cmk(alpha, 0), A, lda, 0, A, lda, 0, cmk(0, 0), C,
-                             ldc, 0, ksplit, kchunk, work, EPI_NONE, nullptr);
+                             ldc, 0, ksplit, kchunk, work, EPI_NONE, nullptr, 0);
   FISDF_HIP(hipGetLastError());
   if (ksplit > 1) {
     const int t32 = (n + 31) / 32;
@@ -789,7 +815,7 @@ int herk_batched(hipStream_t s, int n, int K, double alpha, const cplx* A, long 
   const int nt = (n + BM - 1) / BM;
   dim3 grid(nt * (nt + 1) / 2, 1, batch);
   launch<OP_N, OP_C, true>(s, grid, n, n, K, cmk(alpha, 0), A, lda, sA, A, lda, sA, cmk(beta, 0), C,
-                           ldc, sC, 1, kchunk, nullptr, EPI_NONE, nullptr);
+                           ldc, sC, 1, kchunk, nullptr, EPI_NONE, nullptr, 0);
   FISDF_HIP(hipGetLastError());
   return 0;
 }
