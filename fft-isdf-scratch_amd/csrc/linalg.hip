@@ -522,8 +522,7 @@ __device__ __forceinline__ void yf_mfma_chunk(const cplx* __restrict__ X, int ni
                                               cplx* __restrict__ buf) {
   const int i16 = lane & 15, kq = lane >> 4;
   const int nkc = (nao + 4 * YF_MAXKS - 1) / (4 * YF_MAXKS);
-  // two explicit operand buffers: the loads of the next (slot, K-chunk) are in flight across
-  // this one's MFMAs with no register rotation between iterations
+  // explicit operand buffers (no register rotation between iterations)
   cplx a0[YF_MAXKS], b0[YF_MAXKS], a1[YF_MAXKS], b1[YF_MAXKS];
   // Branch-free operand loads: rows past nip / m are clamped to the last valid row (their
   // columns are never stored) and K past nao to its last element, with the A operand zeroed at
@@ -568,25 +567,32 @@ __device__ __forceinline__ void yf_mfma_chunk(const cplx* __restrict__ X, int ni
     cn = c + 1;
     if (cn == nkc) { sn = s + 4; cn = 0; }
   };
-  // the next loads are issued unconditionally (past the last slot they re-read a valid one and
-  // are never used): a conditional load made the compiler's wait counts conservative on the
-  // path that issued them, draining the next slot's loads before this slot's MFMAs
-  int s = __builtin_amdgcn_readfirstlane(w), c = 0, sn, cn;
+  // two operand buffers: the loads run one (slot, K-chunk) item ahead of the MFMAs (three, two
+  // items ahead, spill 22 VGPRs at 256 and measured slower: 6.3 vs 5.1 ms MFMA phase).  The
+  // loads are issued unconditionally (past the last slot they re-read a valid one and are never
+  // used): a conditional load made the compiler's wait counts conservative on the path that
+  // issued them, draining the next slot's loads before this slot's MFMAs
+  int s = __builtin_amdgcn_readfirstlane(w), c = 0, sl, cl;
   if (s >= nslot) return;
+  auto load_item = [&](cplx (&a)[YF_MAXKS], cplx (&b)[YF_MAXKS], int si, int ci) {
+    load(a, b, min(si, nslot - 1), si < nslot ? ci : 0);
+  };
+  auto step = [&](cplx (&al)[YF_MAXKS], cplx (&bl)[YF_MAXKS], const cplx (&am)[YF_MAXKS],
+                  const cplx (&bm)[YF_MAXKS]) {
+    load_item(al, bl, sl, cl);
+    next(sl, cl, sl, cl);
+    int sn, cn;
+    next(s, c, sn, cn);
+    mma(am, bm, s, c, cn);
+    s = sn;
+    c = cn;
+    return s < nslot;
+  };
   load(a0, b0, s, 0);
+  next(s, c, sl, cl);
   for (;;) {
-    next(s, c, sn, cn);
-    load(a1, b1, min(sn, nslot - 1), sn < nslot ? cn : 0);
-    mma(a0, b0, s, c, cn);
-    s = sn;
-    c = cn;
-    if (s >= nslot) break;
-    next(s, c, sn, cn);
-    load(a0, b0, min(sn, nslot - 1), sn < nslot ? cn : 0);
-    mma(a1, b1, s, c, cn);
-    s = sn;
-    c = cn;
-    if (s >= nslot) break;
+    if (!step(a1, b1, a0, b0)) break;
+    if (!step(a0, b0, a1, b1)) break;
   }
 }
 
@@ -620,35 +626,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   for (int t = 0; t < N2; ++t) { double sn, cs; sincospi(2.0 * t / N2, &sn, &cs); tw2[t] = cmk(cs, sn); }
   cplx tc[NC > 0 ? P : 1];  // t_1 (complex plane)
   double tr[NR][P];         // t_0 (, t_{N0/2})
+  // chunk B first: during the MFMA phase of chunk A only the real tr (NR x P doubles) is live,
+  // not the complex tc (the registers the MFMA phase's operand prefetch needs)
+  // ---- chunk B: the self-paired planes, half their k each ----
+  if (!(mode & 1)) yf_mfma_chunk(X, nip, nao, F, fks, m, plan.kB, plan.nB, Ia, okI, ga, okg, lane, w, buf);
+  __syncthreads();
+  if (!(mode & 2)) {
+#pragma unroll
+    for (int pi = 0; pi < NR; ++pi) {
+      cplx u[P];
+#pragma unroll
+      for (int bc = 0; bc < P; ++bc)
+        if (bc <= yf_inplane_partner<N1, N2>(bc))
+          u[bc] = (mode & 1) ? cmk(0, 0) : buf[(pi * R + yf_inplane_rank<N1, N2>(bc)) * 256 + tid];
+#pragma unroll
+      for (int bc = 0; bc < P; ++bc)
+        if (bc > yf_inplane_partner<N1, N2>(bc)) u[bc] = cconj(u[yf_inplane_partner<N1, N2>(bc)]);
+      reg_axis_dft<N1, N2, P>(u, tw1);
+      reg_axis_dft<N2, 1, P>(u, tw2);
+#pragma unroll
+      for (int bc = 0; bc < P; ++bc) tr[pi][bc] = u[bc].x;
+    }
+  }
   // ---- chunk A: the complex plane a = 1 ----
   if constexpr (NC > 0) {
+    __syncthreads();  // buf is rewritten by chunk A
     if (!(mode & 1)) yf_mfma_chunk(X, nip, nao, F, fks, m, plan.kA, plan.nA, Ia, okI, ga, okg, lane, w, buf);
     __syncthreads();
+    if (mode & 2) return;
 #pragma unroll
     for (int bc = 0; bc < P; ++bc) tc[bc] = (mode & 1) ? cmk(0, 0) : buf[bc * 256 + tid];
     reg_axis_dft<N1, N2, P>(tc, tw1);
     reg_axis_dft<N2, 1, P>(tc, tw2);
-    __syncthreads();  // buf is rewritten by chunk B
   }
-  // ---- chunk B: the self-paired planes, half their k each ----
-  if (!(mode & 1)) yf_mfma_chunk(X, nip, nao, F, fks, m, plan.kB, plan.nB, Ia, okI, ga, okg, lane, w, buf);
-  __syncthreads();
   if (mode & 2) return;
-#pragma unroll
-  for (int pi = 0; pi < NR; ++pi) {
-    cplx u[P];
-#pragma unroll
-    for (int bc = 0; bc < P; ++bc)
-      if (bc <= yf_inplane_partner<N1, N2>(bc))
-        u[bc] = (mode & 1) ? cmk(0, 0) : buf[(pi * R + yf_inplane_rank<N1, N2>(bc)) * 256 + tid];
-#pragma unroll
-    for (int bc = 0; bc < P; ++bc)
-      if (bc > yf_inplane_partner<N1, N2>(bc)) u[bc] = cconj(u[yf_inplane_partner<N1, N2>(bc)]);
-    reg_axis_dft<N1, N2, P>(u, tw1);
-    reg_axis_dft<N2, 1, P>(u, tw2);
-#pragma unroll
-    for (int bc = 0; bc < P; ++bc) tr[pi][bc] = u[bc].x;
-  }
   // ---- per s: fx_s over axis 0, y_s = fx_s^2, r_qa = axis-0 DFT of y_s ----
   const double sc = 1.0 / sqrt((double)NK), sc2 = sc * sc;
   double rr[NR][P];
@@ -1436,7 +1447,7 @@ int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long 
   const size_t lds = sizeof(cplx) * 256 * (size_t)std::max(plan.nA, plan.nB);
   if (lds > 80 * 1024) return 0;
   const int nIt = (nip + 15) / 16, nGt = (m + 15) / 16;
-  static const int gpair = std::max(1, getenv("FISDF_YF_GPAIR") ? atoi(getenv("FISDF_YF_GPAIR")) : 1);
+  static const int gpair = std::max(1, getenv("FISDF_YF_GPAIR") ? atoi(getenv("FISDF_YF_GPAIR")) : 4);
   const long grid = (long)nIt * ((nGt + 8 * gpair - 1) / (8 * gpair)) * gpair * 8;
   FISDF_CHECK(grid < (1L << 31), "y_fused: grid too large");
   static const int mode = getenv("FISDF_YF_MODE") ? atoi(getenv("FISDF_YF_MODE")) : 0;
