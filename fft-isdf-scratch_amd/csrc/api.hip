@@ -48,7 +48,6 @@ struct fisdf_ctx {
   cplx* f_L = nullptr;      // (nk, nip, nip) raw left-looking factor (row order)
   cplx* f_Lp = nullptr;     // (nk, nip*nip) pivot-order factor, ld = rank_q
   cplx* f_Linv = nullptr;   // (nk, nblk*nb*nb)
-  bool f_q_partial_last = false;  // f_Q over [0,64),[64,128),.. (unpivoted) or partial block first
   cplx* f_Q = nullptr;      // (nk, nip, nip) block-row operator of trsm_merged (build_trsm_q)
   cplx* f_Li = nullptr;     // (nk, nip, nip) L^{-1} (pivot order) = trsm_merged on the identity
   cplx* f_x4s = nullptr;    // (nk, nip, nip) staged x4_q of the factored slots
@@ -1059,11 +1058,7 @@ int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk
 // need_linv: the diagonal-block inverses of Lp (trsm_blocked, used only when some rank < nip;
 // the unpivoted path is full-rank by construction — a failing slot is refactored, and this
 // rerun, by factor_pivoted_slots)
-// blkinv: the diagonal-block inverses the unpivoted Cholesky kept (chol_unpivoted keep_blocks),
-// reused for the block-row operator over the partial-last partition; nullptr recomputes them
-// over the partial-first one (pivoted factors)
-int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src, bool need_linv,
-                  const cplx* blkinv = nullptr) {
+int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src, bool need_linv) {
   const int nk = c->f_nk, nip = c->f_nip, nb = c->f_nb, nblk = (nip + nb - 1) / nb;
   const long nn = (long)nip * nip;
   FISDF_HIP(hipMemcpyAsync(c->f_rank_pinned, rank_dev_src, sizeof(int) * nk, hipMemcpyDeviceToHost, s));
@@ -1075,17 +1070,12 @@ int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src, bool nee
   FISDF_TRY(gather_lp(s, c->f_L, nip, nip, c->f_piv, c->f_rank_dev, nip, c->f_Lp, nk));
   if (need_linv)
     FISDF_TRY(trinv_blocks(s, c->f_Lp, nip, nip, nn, nb, (long)nblk * nb * nb, c->f_Linv, nk));
-  c->f_q_partial_last = blkinv != nullptr;
-  if (blkinv)
-    FISDF_TRY(build_trsm_q_blocks(s, c->f_Lp, nip, nn, blkinv, c->f_Q, nk));
-  else
-    FISDF_TRY(build_trsm_q(s, c->f_Lp, nip, nn, c->f_Q, nk, GEMM_FULL));
+  FISDF_TRY(build_trsm_q(s, c->f_Lp, nip, nn, c->f_Q, nk, GEMM_FULL));
   // L^{-1} by the same block-row substitution applied to the identity (the fit then applies it
   // as one lower-triangular GEMM over the grid; J/K within 2-3x of the TRSM's rounding,
   // tests/experiments/explicit_tri_inverse.py)
   FISDF_TRY(set_identity(s, c->f_Li, nip, nk));
-  FISDF_TRY(trsm_merged_batched(s, c->f_Q, nn, nip, c->f_Li, nip, nn, nip, nk, true,
-                                c->f_q_partial_last));
+  FISDF_TRY(trsm_merged_batched(s, c->f_Q, nn, nip, c->f_Li, nip, nn, nip, nk, true));
   return 0;
 }
 
@@ -1218,7 +1208,7 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   cv.take(sizeof(double) * (size_t)nk * (1 + nip));
   size_t oU = cv.take(sizeof(int) * nk);                                   // unpivoted rank
   size_t oFl = cv.take(sizeof(int) * nk);                                  // unpivoted fail
-  size_t oWk = cv.take(sizeof(cplx) * (size_t)((nip + 63) / 64) * nk * 4096 + sizeof(double) * nk);
+  size_t oWk = cv.take(sizeof(cplx) * (size_t)nk * 4096 + sizeof(double) * nk);
   if (cv.off > c->f_scratch_size) {
     if (c->f_scratch) FISDF_HIP(hipFree(c->f_scratch));
     FISDF_HIP(hipMalloc(&c->f_scratch, cv.off));
@@ -1260,9 +1250,9 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
     // same full-rank verdict the rank-revealing pivoted factorisation gives); any matrix that
     // fails it is redone by the pivoted pchol in fisdf_factor_x4_wait
     FISDF_TRY(chol_unpivoted(s, c->f_L, nip, nk, tol_rel, c->f_piv, (int*)(b + oU),
-                             (int*)(b + oFl), (cplx*)(b + oWk), true));
+                             (int*)(b + oFl), (cplx*)(b + oWk)));
     FISDF_HIP(hipMemcpyAsync(c->f_fail_pinned, b + oFl, sizeof(int) * nk, hipMemcpyDeviceToHost, s));
-    FISDF_TRY(factor_finish(c, s, (const int*)(b + oU), false, (const cplx*)(b + oWk)));
+    FISDF_TRY(factor_finish(c, s, (const int*)(b + oU), false));
     c->f_check_fail = true;
   }
   FISDF_HIP(hipEventRecord(c->ev_fac, s));
@@ -1714,7 +1704,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
         Uq = U;
       } else if (r == nip) {  // merged block-row substitution, in place
         FISDF_TRY(trsm_merged(st, c->f_Q + (long)sl * nn, nip, Yh, ngrid, (int)ncol,
-                              real_q ? GEMM_A_REAL : GEMM_FULL, c->f_q_partial_last));
+                              real_q ? GEMM_A_REAL : GEMM_FULL));
         Uq = Yh;
       } else {
         FISDF_TRY(trsm_blocked(st, 1, Lp, nip, 0, r, Linv, 0, nb, Yh, ngrid, 0, U, ngrid,

@@ -89,7 +89,7 @@ int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int
 
 // unpivoted blocked Cholesky (full-rank fast path); see pchol.hip
 int chol_unpivoted(hipStream_t s, cplx* W, int n, int batch, double tol_rel, int* piv, int* rank,
-                   int* fail, cplx* work, bool keep_blocks = false);
+                   int* fail, cplx* work);
 // selection pivots from the real Gram Re(X2)^2*scale (blocked, real; n <= 4096): *handled=false
 // otherwise.  work: n*n + 17*n + 1 doubles; piv (rmax), rank (1), flags (1) device.
 int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rmax, double tol,

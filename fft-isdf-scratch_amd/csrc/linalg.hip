@@ -64,48 +64,67 @@ __global__ __launch_bounds__(64) void trinv_blocks_kernel(const cplx* __restrict
 }
 
 // Same inverses for the partition [0, s0), [s0, s0+64), ... written straight into the
-// diagonal blocks of Q (ld = ldq) — the block-row operator of trsm_merged.
-__global__ __launch_bounds__(64) void trinv_into_kernel(const cplx* __restrict__ Lp, int r,
-                                                        int ldl, long sL, int s0,
-                                                        cplx* __restrict__ Q, int ldq, long sQ) {
+// diagonal blocks of Q (ld = ldq) — the block-row operator of trsm_merged.  Register-blocked
+// like chol_diag_kernel's inverse phase: 256 threads, thread t owns the 4 x 4 block (rows
+// 4 (t >> 4), cols 4 (t & 15)) of X = L_bb^{-1}, built by right-looking forward substitution
+// on the identity (row k final once rows < k are subtracted, then scaled by 1 / L_kk) with one
+// barrier per row.  (The one-wave column-serial version ran 6 ms at C3 beside the y build.)
+__global__ __launch_bounds__(256) void trinv_into_kernel(const cplx* __restrict__ Lp, int r,
+                                                         int ldl, long sL, int s0,
+                                                         cplx* __restrict__ Q, int ldq, long sQ) {
   __shared__ cplx Ls[64][65];
-  __shared__ cplx Xs[64][65];
+  __shared__ cplx vec[2][64];
   Lp += blockIdx.y * sL;
   Q += blockIdx.y * sQ;
   const int blk = blockIdx.x;
   const int b0 = blk == 0 ? 0 : s0 + (blk - 1) * 64;
   const int m = blk == 0 ? s0 : min(64, r - b0);
-  const int j = threadIdx.x;
-  for (int i = 0; i < m; ++i)
-    if (j < m) Ls[i][j] = Lp[(long)(b0 + i) * ldl + b0 + j];
+  const int t = threadIdx.x, bi = t >> 4, bj = t & 15, r0 = bi * 4, c0 = bj * 4;
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int i = e >> 6, j = e & 63;
+    Ls[i][j] = (i < m && j <= i) ? Lp[(long)(b0 + i) * ldl + b0 + j] : cmk(0, 0);
+  }
   __syncthreads();
-  if (j < m) {
-    for (int i = 0; i < m; ++i) {
-      cplx sacc = cmk(i == j ? 1.0 : 0.0, 0.0);
-      for (int t = j; t < i; ++t) sacc = csub(sacc, cmul(Ls[i][t], Xs[t][j]));
-      cplx d = Ls[i][i];
-      double den = d.x * d.x + d.y * d.y;
-      Xs[i][j] = i < j ? cmk(0, 0)
-                       : cmk((sacc.x * d.x + sacc.y * d.y) / den, (sacc.y * d.x - sacc.x * d.y) / den);
+  cplx x[4][4];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[rr][c] = cmk(r0 + rr == c0 + c ? 1.0 : 0.0, 0.0);
+  // k = 4 kb + kr with kr unrolled: register arrays keep compile-time indices
+  for (int kb = 0; 4 * kb < m; ++kb) {
+#pragma unroll
+    for (int kr = 0; kr < 4; ++kr) {
+      const int k = 4 * kb + kr, p = kr & 1;
+      if (k >= m) break;
+      if (bi == kb) {
+        const cplx d = Ls[k][k];
+        const double den = d.x * d.x + d.y * d.y;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const cplx v = x[kr][c];
+          x[kr][c] = cmk((v.x * d.x + v.y * d.y) / den, (v.y * d.x - v.x * d.y) / den);
+          vec[p][c0 + c] = x[kr][c];
+        }
+      }
+      __syncthreads();
+      cplx xk[4], lik[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) xk[c] = vec[p][c0 + c];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) lik[rr] = (r0 + rr > k && r0 + rr < m) ? Ls[r0 + rr][k] : cmk(0, 0);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x[rr][c] = csub(x[rr][c], cmul(lik[rr], xk[c]));
     }
   }
-  __syncthreads();
-  for (int i = 0; i < m; ++i)
-    if (j < m) Q[(long)(b0 + i) * ldq + b0 + j] = Xs[i][j];
-}
-
-// Q[b0:b0+m, b0:b0+m] = Bi[blk] (the kept inverse of diagonal block blk = blockIdx.x, rows
-// [64 blk, 64 blk + m)): the diagonal blocks of the partial-last block-row operator
-__global__ __launch_bounds__(256) void place_blkinv_kernel(const cplx* __restrict__ Bi, int r,
-                                                           int batch, cplx* __restrict__ Q, long sQ) {
-  const int blk = blockIdx.x, b = blockIdx.y;
-  const int b0 = 64 * blk, m = min(64, r - b0);
-  const cplx* src = Bi + ((long)blk * batch + b) * 4096;
-  cplx* dst = Q + b * sQ + (long)b0 * r + b0;
-  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
-    const int i = e >> 6, j = e & 63;
-    if (i < m && j < m) dst[(long)i * r + j] = src[e];
-  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int i = r0 + rr, j = c0 + c;
+      if (i < m && j < m) Q[(long)(b0 + i) * ldq + b0 + j] = x[rr][c];
+    }
 }
 
 // W[b][piv[b][s]][piv[b][t]] = Wpp[b][s][t] for s,t < rank[b]   (W zeroed beforehand)
@@ -802,7 +821,7 @@ int build_trsm_q(hipStream_t s, const cplx* Lp, int r, long sL, cplx* Q, int bat
   if (nblk == 0 || batch == 0) return 0;
   const int s0 = r - 64 * (nblk - 1);
   const long rr = (long)r * r;
-  hipLaunchKernelGGL(trinv_into_kernel, dim3(nblk, batch), dim3(64), 0, s, Lp, r, r, sL, s0, Q, r,
+  hipLaunchKernelGGL(trinv_into_kernel, dim3(nblk, batch), dim3(256), 0, s, Lp, r, r, sL, s0, Q, r,
                      rr);
   FISDF_HIP(hipGetLastError());
   const cplx mone = cmk(-1, 0), zero = cmk(0, 0);
@@ -815,33 +834,13 @@ int build_trsm_q(hipStream_t s, const cplx* Lp, int r, long sL, cplx* Q, int bat
   return 0;
 }
 
-// The same operator over the partition [0, 64), [64, 128), ..., [64 (nblk-1), r) (partial block
-// last) from the diagonal-block inverses the unpivoted Cholesky kept (chol_unpivoted with
-// keep_blocks: block k at Bi + k*batch*4096, ld 64): no triangular inverse is recomputed.
-int build_trsm_q_blocks(hipStream_t s, const cplx* Lp, int r, long sL, const cplx* Bi, cplx* Q,
-                        int batch) {
-  const int nblk = (r + 63) / 64;
-  if (nblk == 0 || batch == 0) return 0;
-  const long rr = (long)r * r;
-  hipLaunchKernelGGL(place_blkinv_kernel, dim3(nblk, batch), dim3(256), 0, s, Bi, r, batch, Q, rr);
-  FISDF_HIP(hipGetLastError());
-  const cplx mone = cmk(-1, 0), zero = cmk(0, 0);
-  for (int b = 1; b < nblk; ++b) {
-    const int b0 = 64 * b, m = std::min(64, r - b0);
-    FISDF_TRY(zgemm(s, OP_N, OP_N, m, b0, m, mone, Bi + (long)b * batch * 4096, 64, 4096,
-                    Lp + (long)b0 * r, r, sL, zero, Q + (long)b0 * r, r, rr, batch, 1));
-  }
-  return 0;
-}
-
 // X = L^{-1} X in place for X (r x ncol, ld): one GEMM per block row with the Q of
 // build_trsm_q, X[b] = Q[b, :b1] X[:b1] — each workgroup owns whole columns (M <= 64), so
 // it reads all of X[:b1] for its columns before its epilogue overwrites X[b].
-int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol, int mode,
-                bool partial_last) {
+int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol, int mode) {
   const int nblk = (r + 63) / 64;
   if (nblk == 0) return 0;
-  const int s0 = partial_last ? 64 : r - 64 * (nblk - 1);
+  const int s0 = r - 64 * (nblk - 1);
   const cplx one = cmk(1, 0), zero = cmk(0, 0);
   for (int b = 0; b < nblk; ++b) {
     const int b0 = b == 0 ? 0 : s0 + (b - 1) * 64;
@@ -856,10 +855,10 @@ int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol,
 // lower_rhs: X is lower-triangular (the identity, for L^{-1}), so block row b only has
 // columns < b1 to compute (the rest stay zero)
 int trsm_merged_batched(hipStream_t s, const cplx* Q, long sQ, int r, cplx* X, long ld, long sX,
-                        int ncol, int batch, bool lower_rhs, bool partial_last) {
+                        int ncol, int batch, bool lower_rhs) {
   const int nblk = (r + 63) / 64;
   if (nblk == 0 || batch == 0) return 0;
-  const int s0 = partial_last ? 64 : r - 64 * (nblk - 1);
+  const int s0 = r - 64 * (nblk - 1);
   const cplx one = cmk(1, 0), zero = cmk(0, 0);
   for (int b = 0; b < nblk; ++b) {
     const int b0 = b == 0 ? 0 : s0 + (b - 1) * 64;

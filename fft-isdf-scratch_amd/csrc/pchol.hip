@@ -881,28 +881,24 @@ int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int
 // Unpivoted blocked Cholesky of batch n x n Hermitian matrices W (in place, ld n, batch stride
 // n*n; lower triangle = L on return).  fail[b] = 1 if a pivot <= tol_rel*max(diag) (the caller
 // falls back to pchol); piv = identity, rank = n (0 if failed).  work: batch*(4096 cplx) +
-// batch doubles; keep_blocks: nblk*batch*(4096 cplx) + batch doubles, and the inverse of
-// diagonal block k (rows [64k, 64k+64), identity-padded) stays at work + k*batch*4096 — the
-// block inverses the L^{-1} assembly (build_trsm_q_blocks) reuses
+// batch doubles.
 int chol_unpivoted(hipStream_t s, cplx* W, int n, int batch, double tol_rel, int* piv, int* rank,
-                   int* fail, cplx* work, bool keep_blocks) {
+                   int* fail, cplx* work) {
   FISDF_CHECK(n > 0 && batch > 0, "chol_unpivoted: bad sizes");
   const long nn = (long)n * n;
-  const int nkeep = keep_blocks ? (n + 63) / 64 : 1;
   cplx* Linv = work;
-  double* thr = (double*)(work + (long)nkeep * batch * 4096);
+  double* thr = (double*)(work + (long)batch * 4096);
   hipLaunchKernelGGL(diag_max_kernel, dim3(batch), dim3(256), 0, s, W, n, nn, tol_rel, thr, fail);
   FISDF_HIP(hipGetLastError());
   const cplx one = cmk(1, 0), zero = cmk(0, 0);
   for (int b0 = 0; b0 < n; b0 += 64) {
     const int m = std::min(64, n - b0), b1 = b0 + m;
-    cplx* Lb = keep_blocks ? Linv + (long)(b0 / 64) * batch * 4096 : Linv;
     hipLaunchKernelGGL(chol_diag_kernel, dim3(batch), dim3(256), 0, s, W, n, nn, b0, m, thr, fail,
-                       Lb);
+                       Linv);
     FISDF_HIP(hipGetLastError());
     if (b1 < n) {
       // panel: W[b1:, b0:b1] <- W[b1:, b0:b1] L_bb^{-H}  (in place: one N tile, rows per WG)
-      FISDF_TRY(zgemm(s, OP_N, OP_C, n - b1, m, m, one, W + (long)b1 * n + b0, n, nn, Lb, 64,
+      FISDF_TRY(zgemm(s, OP_N, OP_C, n - b1, m, m, one, W + (long)b1 * n + b0, n, nn, Linv, 64,
                       4096, zero, W + (long)b1 * n + b0, n, nn, batch));
       // trailing: W[b1:, b1:] -= P P^H (Hermitian: lower tiles + mirror)
       FISDF_TRY(herk_batched(s, n - b1, m, -1.0, W + (long)b1 * n + b0, n, nn, 1.0,
