@@ -137,19 +137,27 @@ struct Carver {
 
 // Asynchronous upload of a small host int array: staged through a pinned buffer whose reuse
 // waits for the previous copy (no host sync on the stream).
-int upload_ints(fisdf_ctx* c, const int* h, int n, int* d) {
-  if (n <= 0) return 0;
+// host -> device through the context's pinned staging buffer, asynchronous on the main stream;
+// the buffer is reused once the previous staged copy has completed (ev_stage)
+int upload_bytes(fisdf_ctx* c, const void* h, size_t bytes, void* d) {
+  if (bytes == 0) return 0;
   if (!c->ev_stage) FISDF_HIP(hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
   FISDF_HIP(hipEventSynchronize(c->ev_stage));
-  if ((size_t)n > c->stage_cap) {
+  if (bytes > c->stage_cap) {
     if (c->stage_pinned) FISDF_HIP(hipHostFree(c->stage_pinned));
-    FISDF_HIP(hipHostMalloc((void**)&c->stage_pinned, sizeof(int) * n, hipHostMallocDefault));
-    c->stage_cap = n;
+    c->stage_pinned = nullptr;
+    c->stage_cap = 0;
+    FISDF_HIP(hipHostMalloc((void**)&c->stage_pinned, bytes, hipHostMallocDefault));
+    c->stage_cap = bytes;
   }
-  std::memcpy(c->stage_pinned, h, sizeof(int) * n);
-  FISDF_HIP(hipMemcpyAsync(d, c->stage_pinned, sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
+  std::memcpy(c->stage_pinned, h, bytes);
+  FISDF_HIP(hipMemcpyAsync(d, c->stage_pinned, bytes, hipMemcpyHostToDevice, c->stream));
   FISDF_HIP(hipEventRecord(c->ev_stage, c->stream));
   return 0;
+}
+
+int upload_ints(fisdf_ctx* c, const int* h, int n, int* d) {
+  return n <= 0 ? 0 : upload_bytes(c, h, sizeof(int) * (size_t)n, d);
 }
 
 struct StageTimer {
@@ -1854,15 +1862,13 @@ int fisdf_build_ws_qs(fisdf_ctx* c, const void* Wqv, const int* h_qs, const doub
   void* base;
   FISDF_TRY(arena_get(c, cv.off, &base));
   cplx* dph = (cplx*)((char*)base + oP);
-  FISDF_HIP(hipMemcpyAsync(dph, ph.data(), sizeof(cplx) * ph.size(), hipMemcpyHostToDevice,
-                           c->stream));
+  FISDF_TRY(upload_bytes(c, ph.data(), sizeof(cplx) * ph.size(), dph));
   // ws = Phi W (:205), real part * sqrt(nk) (:207) in the GEMM's epilogue.  With time-reversal
   // representatives the partner -q contributes conj(Phi[R,q] W_q), so Re(.) of the pair is
   // 2 Re(Phi[R,q] W_q): wt = 2.
   FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nn, nq, cmk(std::sqrt((double)nk), 0), dph, nq, 0,
                   (const cplx*)Wqv, nn, 0, ZERO, (cplx*)Wsv, nn, 0, 1, 1, nullptr, EPI_REAL,
                   nullptr));
-  FISDF_HIP(hipStreamSynchronize(c->stream));  // ph staging
   return 0;
 }
 
