@@ -981,8 +981,13 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
   if (half && nblk > 0) {
     // fused fx + k-mesh DFT (FISDF_Y_FUSED, default on): no fx round trip through HBM
     bool done = false;
-    FISDF_TRY(y_fused(c->stream, X, nip, nao, f, f_kstride, nblk, kmesh, h_qs, nq, yT,
-                      (long)nip * ngrid, ngrid, g0, c->maximag + 1, &done));
+    const size_t yw = y_fused_workspace(kmesh, nip, nao, nblk);
+    if (yw) {
+      void* wb = nullptr;
+      FISDF_TRY(arena_get(c, yw, &wb));
+      FISDF_TRY(y_fused(c->stream, X, nip, nao, f, f_kstride, nblk, kmesh, h_qs, nq, yT,
+                        (long)nip * ngrid, ngrid, g0, c->maximag + 1, (cplx*)wb, yw, &done));
+    }
     if (done) return 0;
   }
   const int nks = half ? kmesh_half_count(kmesh) : nk;

@@ -534,9 +534,9 @@ __host__ __device__ constexpr int yf_inplane_rank(int bc) {
 }
 
 // fx for the chunk's slots (wave w: slots w, w+4, ...) into buf[slot][256]
-__device__ __forceinline__ void yf_mfma_chunk(const cplx* __restrict__ X, int nip, int nao,
-                                              const cplx* __restrict__ F, long fks, int m,
-                                              const int* ks, int nslot, int Ia, bool okI,
+__device__ __forceinline__ void yf_mfma_chunk(const cplx* __restrict__ XT, int nip, int nao,
+                                              const cplx* __restrict__ FT, int m, int sbase,
+                                              int nslot, int Ia, bool okI,
                                               int ga, bool okg, int lane, int w,
                                               cplx* __restrict__ buf) {
   const int i16 = lane & 15, kq = lane >> 4;
@@ -551,21 +551,26 @@ __device__ __forceinline__ void yf_mfma_chunk(const cplx* __restrict__ X, int ni
   const int Ic = min(Ia, nip - 1), gc = min(ga, m - 1);
   (void)okI;
   (void)okg;
+  // operands from the mu-major copies XT[slot][mu][I], FT[slot][mu][g] (yf_transpose_kernel):
+  // at a fixed mu the 16 rows of a fragment are 256 contiguous bytes, so one load instruction
+  // moves 4 x 256 B in full 128-B lines instead of 16 rows x 64 B (half lines) from the
+  // [k][row][mu] layouts (which kept the L1/TA path busier than the MFMA pipe)
   auto load = [&](cplx (&a)[YF_MAXKS], cplx (&b)[YF_MAXKS], int s, int c) {
-    const int k = ks[s];
-    const cplx* xa = X + ((long)k * nip + Ic) * nao;
-    const cplx* fb = F + (long)k * fks + (long)gc * nao;
+    const long sl = (long)(sbase + s) * nao;
+    const cplx* xa = XT + sl * nip + Ic;
+    const cplx* fb = FT + sl * m + gc;
 #pragma unroll
     for (int kk = 0; kk < YF_MAXKS; ++kk) {
       const int mu = min(c * 4 * YF_MAXKS + kk * 4 + kq, nao - 1);
-      a[kk] = xa[mu];
-      b[kk] = fb[mu];
+      a[kk] = xa[(long)mu * nip];
+      b[kk] = fb[(long)mu * m];
     }
   };
   f64x4 t1 = {0, 0, 0, 0}, t2 = {0, 0, 0, 0}, t3 = {0, 0, 0, 0};
   auto mma = [&](const cplx (&a)[YF_MAXKS], const cplx (&b)[YF_MAXKS], int s, int c, int cn) {
 #pragma unroll
     for (int kk = 0; kk < YF_MAXKS; ++kk) {
+      if (c * 4 * YF_MAXKS + kk * 4 >= nao) break;  // wave-uniform: a K step past nao
       const bool ok = c * 4 * YF_MAXKS + kk * 4 + kq < nao;
       const double ar = ok ? a[kk].x : 0.0, ai = ok ? a[kk].y : 0.0, br = b[kk].x, bi = b[kk].y;
       t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, br, t1, 0, 0, 0);
@@ -587,7 +592,8 @@ __device__ __forceinline__ void yf_mfma_chunk(const cplx* __restrict__ X, int ni
     if (cn == nkc) { sn = s + 4; cn = 0; }
   };
   // two operand buffers: the loads run one (slot, K-chunk) item ahead of the MFMAs (three, two
-  // items ahead, spill 22 VGPRs at 256 and measured slower: 6.3 vs 5.1 ms MFMA phase).  The
+  // items ahead, spill 22 VGPRs at 256 and measured slower: 6.3 vs 5.1 ms MFMA phase; four
+  // buffers of half-slot items (K chunks of 16) fit in 233 VGPRs and measured 5.7 ms).  The
   // loads are issued unconditionally (past the last slot they re-read a valid one and are never
   // used): a conditional load made the compiler's wait counts conservative on the path that
   // issued them, draining the next slot's loads before this slot's MFMAs
@@ -615,9 +621,33 @@ __device__ __forceinline__ void yf_mfma_chunk(const cplx* __restrict__ X, int ni
   }
 }
 
+// dst[j][mu][r] = src[k_j * kstride + r * nao + mu] for r < nrow: the plan's k (slot j: chunk A's
+// k, then chunk B's) in mu-major order for the fused kernel's fragment loads.  One workgroup per
+// (64-row block, slot): the block's 64 x nao elements (contiguous) are read coalesced into LDS
+// and written out row-contiguous per mu.
+__global__ __launch_bounds__(256) void yf_transpose_kernel(const cplx* __restrict__ src,
+                                                           long kstride, int nrow, int nao,
+                                                           YfPlan plan, cplx* __restrict__ dst) {
+  extern __shared__ cplx tile[];  // [64][nao + 1]
+  const int j = blockIdx.y;
+  const int k = j < plan.nA ? plan.kA[j] : plan.kB[j - plan.nA];
+  const int r0 = blockIdx.x * 64, nr = min(64, nrow - r0), ld = nao + 1;
+  const cplx* sp = src + (long)k * kstride + (long)r0 * nao;
+  for (int e = threadIdx.x; e < nr * nao; e += 256) {
+    const int r = e / nao, mu = e - r * nao;
+    tile[r * ld + mu] = sp[e];
+  }
+  __syncthreads();
+  cplx* dp = dst + (long)j * nao * nrow + r0;
+  for (int e = threadIdx.x; e < nao * 64; e += 256) {
+    const int mu = e >> 6, r = e & 63;
+    if (r < nr) dp[(long)mu * nrow + r] = tile[r * ld + mu];
+  }
+}
+
 template <int N0, int N1, int N2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void y_fused_kernel(
-    const cplx* __restrict__ X, int nip, int nao, const cplx* __restrict__ F, long fks, int m,
+    const cplx* __restrict__ XT, int nip, int nao, const cplx* __restrict__ FT, int m,
     int nIt, int nGt, YfPlan plan, unsigned long long qmask, cplx* __restrict__ yT, long qs,
     long Is, long goff, int mode, int gpair) {
   constexpr int P = N1 * N2, NK = N0 * P;
@@ -648,7 +678,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // chunk B first: during the MFMA phase of chunk A only the real tr (NR x P doubles) is live,
   // not the complex tc (the registers the MFMA phase's operand prefetch needs)
   // ---- chunk B: the self-paired planes, half their k each ----
-  if (!(mode & 1)) yf_mfma_chunk(X, nip, nao, F, fks, m, plan.kB, plan.nB, Ia, okI, ga, okg, lane, w, buf);
+  if (!(mode & 1)) yf_mfma_chunk(XT, nip, nao, FT, m, plan.nA, plan.nB, Ia, okI, ga, okg, lane, w, buf);
   __syncthreads();
   if (!(mode & 2)) {
 #pragma unroll
@@ -670,7 +700,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // ---- chunk A: the complex plane a = 1 ----
   if constexpr (NC > 0) {
     __syncthreads();  // buf is rewritten by chunk A
-    if (!(mode & 1)) yf_mfma_chunk(X, nip, nao, F, fks, m, plan.kA, plan.nA, Ia, okI, ga, okg, lane, w, buf);
+    if (!(mode & 1)) yf_mfma_chunk(XT, nip, nao, FT, m, 0, plan.nA, Ia, okI, ga, okg, lane, w, buf);
     __syncthreads();
     if (mode & 2) return;
 #pragma unroll
@@ -1417,9 +1447,19 @@ bool y_fused_enabled() {
   return on;
 }
 
+size_t y_fused_workspace(const int kmesh[3], int nip, int nao, int m) {
+  const int n0 = kmesh[0], P = kmesh[1] * kmesh[2];
+  if (!y_fused_enabled() || n0 * P > 64 || n0 > 4 || P > 16 || m <= 0 || nip <= 0 || nao > 128)
+    return 0;
+  const int nr = (n0 % 2 == 0 && n0 > 1) ? 2 : 1;
+  int nslot = n0 >= 3 ? P : 0;  // chunk A + chunk B (in-plane representatives), upper bound
+  nslot += nr * P;
+  return sizeof(cplx) * (size_t)nslot * nao * ((size_t)nip + m);
+}
+
 int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long fks, int m,
             const int kmesh[3], const int* h_qs, int nq, cplx* yT, long qs, long Is, long goff,
-            unsigned long long* mon, bool* handled) {
+            unsigned long long* mon, cplx* work, size_t work_bytes, bool* handled) {
   (void)mon;  // fx_s is real by construction here (t_{-a} = conj(t_a)); nothing to monitor
   *handled = false;
   const int n0 = kmesh[0], n1 = kmesh[1], n2 = kmesh[2];
@@ -1444,7 +1484,26 @@ int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long 
     }
   }
   const size_t lds = sizeof(cplx) * 256 * (size_t)std::max(plan.nA, plan.nB);
-  if (lds > 80 * 1024) return 0;
+  if (lds > 80 * 1024 || nao > 128) return 0;
+  // mu-major copies of the plan's k: XT [slot][mu][I], FT [slot][mu][g]
+  const int nsl = plan.nA + plan.nB;
+  FISDF_CHECK(work && work_bytes >= sizeof(cplx) * (size_t)nsl * nao * ((size_t)nip + m),
+              "y_fused: workspace too small");
+  cplx* XT = work;
+  cplx* FT = work + (size_t)nsl * nao * nip;
+  const size_t tl = sizeof(cplx) * 64 * (size_t)(nao + 1);
+  static bool tattr = false;
+  if (!tattr) {  // nao up to 128: 64 x 129 x 16 B of LDS
+    FISDF_HIP(hipFuncSetAttribute((const void*)yf_transpose_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 132 * 1024));
+    tattr = true;
+  }
+  hipLaunchKernelGGL(yf_transpose_kernel, dim3((nip + 63) / 64, nsl), dim3(256), tl, s, X,
+                     (long)nip * nao, nip, nao, plan, XT);
+  FISDF_HIP(hipGetLastError());
+  hipLaunchKernelGGL(yf_transpose_kernel, dim3((m + 63) / 64, nsl), dim3(256), tl, s, F, fks, m,
+                     nao, plan, FT);
+  FISDF_HIP(hipGetLastError());
   const int nIt = (nip + 15) / 16, nGt = (m + 15) / 16;
   static const int gpair = std::max(1, getenv("FISDF_YF_GPAIR") ? atoi(getenv("FISDF_YF_GPAIR")) : 4);
   const long grid = (long)nIt * ((nGt + 8 * gpair - 1) / (8 * gpair)) * gpair * 8;
@@ -1458,8 +1517,8 @@ int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long 
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));   \
       attr = true;                                                                             \
     }                                                                                          \
-    hipLaunchKernelGGL((y_fused_kernel<a, b, c>), dim3((unsigned)grid), dim3(256), lds, s, X,   \
-                       nip, nao, F, fks, m, nIt, nGt, plan, qmask, yT, qs, Is, goff, mode, gpair); \
+    hipLaunchKernelGGL((y_fused_kernel<a, b, c>), dim3((unsigned)grid), dim3(256), lds, s, XT,  \
+                       nip, nao, FT, m, nIt, nGt, plan, qmask, yT, qs, Is, goff, mode, gpair);   \
     FISDF_HIP(hipGetLastError());                                                              \
     *handled = true;                                                                           \
     return 0;                                                                                  \
