@@ -45,8 +45,8 @@ PEAK_FP64_TFLOPS = 78.6  # MI355X FP64 matrix (= vector) dense peak, MI355X_MICR
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=3)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-q", type=int, default=4, help="q-points fitted in the CPU sample")
