@@ -934,6 +934,13 @@ int fisdf_build_x4(fisdf_ctx* c, const void* Xv, int nip, int nao, const int kme
   FISDF_TRY(get_phase(c, kmesh, a, &phase));
   const cplx* X = (const cplx*)Xv;
   const long nn = (long)nip * nip;
+  if (nk == 1) {
+    // Gamma only: Phi = 1, so x2_s = x2_k and x4 = x2_s^2 (:45) straight from the x2 GEMM's
+    // epilogue with the reality monitor of :43 (the two Phi GEMMs would run with M = 1)
+    FISDF_TRY(zgemm(c->stream, OP_R, OP_T, nip, nip, nao, ONE, X, nao, 0, X, nao, 0, ZERO,
+                    (cplx*)x4v, nip, 0, 1, 1, nullptr, EPI_CSQUARE, c->maximag + 0));
+    return 0;
+  }
   Carver cv;
   size_t o1 = cv.take(sizeof(cplx) * nk * nn);
   size_t o2 = cv.take(sizeof(cplx) * nk * nn);
@@ -2053,16 +2060,24 @@ int fisdf_get_k_rows(fisdf_ctx* c, const void* Xv, const void* Wsv, const void* 
     // (:211-212, transposed at the source so :219's product is element-wise)
     FISDF_TRY(zgemm(c->stream, OP_R, OP_T, nb, nao, nao, cmk(1.0 / nk, 0), Xb, nao, xs, dm, nao, ds,
                     ZERO, T, nao, ba, nk));
-    FISDF_TRY(zgemm(c->stream, OP_N, OP_T, nb, nip, nao, ONE, T, nao, ba, X, nao, xs, ZERO, B1,
-                    nip, bn, nk));
-    // rho_s = Phi rho_k (:215), real (:216), and V_s = W_s * rho_s^T (:219) for the block rows,
-    // both in the GEMM's epilogue (EPI_WSRHO: Re(W_s) Re(.), max |Im rho_s| recorded)
-    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, bn, nk, ONE, phase, nk, 0, B1, bn, 0, ZERO, B2, bn,
-                    0, 1, 1, (cplx*)(Ws + (long)i0 * nip), EPI_WSRHO, c->maximag + 2, GEMM_FULL,
-                    (long)nip * nip));
-    // V_k = Phi^T V_s (:222)
-    FISDF_TRY(zgemm(c->stream, OP_T, OP_N, nk, bn, nk, ONE, phase, nk, 0, B2, bn, 0, ZERO, B1, bn,
-                    0, 1));
+    if (nk == 1) {
+      // Gamma only (Phi = 1): rho_s = Re(rho_k) (:215-216) and V = W_s * rho_s^T (:219) in this
+      // GEMM's epilogue; V_k = V_s (:222)
+      FISDF_TRY(zgemm(c->stream, OP_N, OP_T, nb, nip, nao, ONE, T, nao, ba, X, nao, xs, ZERO, B1,
+                      nip, bn, 1, 1, (cplx*)(Ws + (long)i0 * nip), EPI_WSRHO, c->maximag + 2,
+                      GEMM_FULL, (long)nip));
+    } else {
+      FISDF_TRY(zgemm(c->stream, OP_N, OP_T, nb, nip, nao, ONE, T, nao, ba, X, nao, xs, ZERO, B1,
+                      nip, bn, nk));
+      // rho_s = Phi rho_k (:215), real (:216), and V_s = W_s * rho_s^T (:219) for the block
+      // rows, both in the GEMM's epilogue (EPI_WSRHO: Re(W_s) Re(.), max |Im rho_s| recorded)
+      FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, bn, nk, ONE, phase, nk, 0, B1, bn, 0, ZERO, B2,
+                      bn, 0, 1, 1, (cplx*)(Ws + (long)i0 * nip), EPI_WSRHO, c->maximag + 2,
+                      GEMM_FULL, (long)nip * nip));
+      // V_k = Phi^T V_s (:222)
+      FISDF_TRY(zgemm(c->stream, OP_T, OP_N, nk, bn, nk, ONE, phase, nk, 0, B2, bn, 0, ZERO, B1,
+                      bn, 0, 1));
+    }
     // K_k (block part) = X_k[I]^H (V_k[I, :] X_k)  (:225)
     FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nb, nao, nip, ONE, B1, nip, bn, X, nao, xs, ZERO, T,
                     nao, ba, nk));
