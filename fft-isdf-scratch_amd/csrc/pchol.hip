@@ -505,12 +505,12 @@ __device__ __forceinline__ bool sc_better(double v2, int i2, double v, int i) {
 }
 
 __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
-    const cplx* __restrict__ X2, double scale, int n, int rmax, double tol, int RW,
+    const cplx* __restrict__ X2, double scale, int n, int rmax, double tol, int RW, int K, int tpr,
     int* __restrict__ piv, int* __restrict__ rank, u32x4* __restrict__ rec,
     double* __restrict__ Lg, int* __restrict__ err) {
   extern __shared__ double sm[];
-  double* Lr = sm;                    // RW x rmax, row-major
-  double* Lp = Lr + (long)RW * rmax;  // pivot row L[p, :j]
+  double* Lr = sm;                    // RW x K, row-major (columns >= K only in the global L)
+  double* Lp = Lr + (long)RW * K;     // pivot row L[p, :j]
   double* dd = Lp + rmax;             // residual diagonal of the owned rows
   double* w0 = dd + RW;               // x4[p, owned rows]
   __shared__ double s_v[SC_THREADS / 64];
@@ -617,20 +617,24 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
     // ---- column j ----
     {
       const double sq = sqrt(dp), inv = 1.0 / sq;
-      const int r = tid >> 3, part = tid & 7;
+      const int r = tid / tpr, part = tid & (tpr - 1);
       if (r < nr) {
-        const double* lr = Lr + (long)r * rmax;
+        const double* lr = Lr + (long)r * K;
+        const int jl = min(j, K);
         double a0 = 0.0, a1 = 0.0;
         int c = part;
-        for (; c + 8 < j; c += 16) {
+        for (; c + tpr < jl; c += 2 * tpr) {
           a0 += lr[c] * Lp[c];
-          a1 += lr[c + 8] * Lp[c + 8];
+          a1 += lr[c + tpr] * Lp[c + tpr];
         }
-        if (c < j) a0 += lr[c] * Lp[c];
+        if (c < jl) a0 += lr[c] * Lp[c];
+        if (j > K) {  // this workgroup's own entries past the LDS columns, written by earlier steps
+          const double* lg = Lg + (long)(r0 + r) * rmax;
+          for (c = K + part; c < j; c += tpr)
+            a1 += __hip_atomic_load(lg + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * Lp[c];
+        }
         double acc = a0 + a1;
-        acc += __shfl_xor(acc, 1, 64);
-        acc += __shfl_xor(acc, 2, 64);
-        acc += __shfl_xor(acc, 4, 64);
+        for (int o = 1; o < tpr; o <<= 1) acc += __shfl_xor(acc, o, 64);
         if (part == 0) {
           const int i = r0 + r;
           double l = 0.0;
@@ -641,7 +645,7 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
             l = (w0[r] - acc) * inv;
             dd[r] -= l * l;
           }
-          Lr[(long)r * rmax + j] = l;
+          if (j < K) Lr[(long)r * K + j] = l;
           __hip_atomic_store(&Lg[(long)i * rmax + j], l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -937,13 +941,34 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
     const char* e = getenv("FISDF_SEL_WGS");
     return e ? atoi(e) : 0;
   }();
+  // read per call (tests switch them): FISDF_SEL_HYBRID=0 disables the LDS + global split,
+  // FISDF_SEL_LDS_COLS=k forces it with at most k LDS columns
+  const char* eh = getenv("FISDF_SEL_HYBRID");
+  const bool hybrid = !(eh && eh[0] == '0');
+  const char* ek = getenv("FISDF_SEL_LDS_COLS");
+  const int kcap = ek ? atoi(ek) : 0;
+  constexpr size_t kLds = 150 * 1024;
   int G = wgs_env > 0 ? wgs_env : 128;
   G = std::min({G, ncu, (n + 7) / 8});
   if (G < 1) return 0;
-  const int RW = (n + G - 1) / G;
+  int RW = (n + G - 1) / G;
   G = (n + RW - 1) / RW;
-  const size_t lds = sizeof(double) * ((size_t)RW * rmax + rmax + 2 * (size_t)RW);
-  if (lds > 150 * 1024 || RW > SC_MAXRW) return 0;
+  int K = rmax, tpr = 8;
+  size_t lds = sizeof(double) * ((size_t)RW * rmax + rmax + 2 * (size_t)RW);
+  if ((lds > kLds || kcap > 0) && hybrid && wgs_env <= 0) {
+    // the owned L rows do not fit: one workgroup per CU, the first K columns in LDS and the
+    // rest read back (agent-coherent) from the global L; 16 threads per row when RW <= 16
+    G = std::min(ncu, (n + 7) / 8);
+    RW = (n + G - 1) / G;
+    G = (n + RW - 1) / RW;
+    K = (int)(((long)(kLds / sizeof(double)) - rmax - 2L * RW) / RW);
+    if (kcap > 0) K = std::min(K, kcap);
+    if (K < 16) return 0;
+    K = std::min(K, rmax);
+    tpr = RW <= SC_THREADS / 16 ? 16 : 8;
+    lds = sizeof(double) * ((size_t)RW * K + rmax + 2 * (size_t)RW);
+  }
+  if (lds > kLds || RW > SC_MAXRW) return 0;
   // scratch in the caller's work area (n*n doubles): records, global L, error flag
   u32x4* rec = (u32x4*)work;
   double* Lg = work + 4 * G;
@@ -955,11 +980,11 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
   static bool attr = false;
   if (!attr) {
     FISDF_HIP(hipFuncSetAttribute((const void*)pchol_select_coop,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
     attr = true;
   }
   void* args[] = {(void*)&X2, (void*)&scale, (void*)&n,   (void*)&rmax, (void*)&tol, (void*)&RW,
-                  (void*)&piv, (void*)&rank, (void*)&rec, (void*)&Lg,   (void*)&err};
+                  (void*)&K,   (void*)&tpr,   (void*)&piv, (void*)&rank, (void*)&rec, (void*)&Lg,   (void*)&err};
   const hipError_t e = hipLaunchCooperativeKernel((const void*)pchol_select_coop, dim3(G),
                                                   dim3(SC_THREADS), args, (unsigned)lds, s);
   static const bool dbg = getenv("FISDF_SEL_DEBUG") != nullptr;
@@ -972,7 +997,7 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
   int h_err = 0;
   FISDF_HIP(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, s));
   FISDF_HIP(hipStreamSynchronize(s));
-  if (dbg) fprintf(stderr, "[fisdf] cooperative selection G=%d RW=%d lds=%zu err=%d\n", G, RW, lds, h_err);
+  if (dbg) fprintf(stderr, "[fisdf] cooperative selection G=%d RW=%d K=%d tpr=%d lds=%zu err=%d\n", G, RW, K, tpr, lds, h_err);
   *handled = h_err == 0;
   return 0;
 }

@@ -265,18 +265,24 @@ def test_x4_and_y_parity(name):
 
 @pytest.mark.parametrize("name", ["toy222", "diamond_szv_gamma", "si_small"])
 def test_selection_paths_agree(name, monkeypatch):
-    """The cooperative left-looking selection (default) and the blocked right-looking one
-    (FISDF_SEL_COOP=0) pick the same pivots as dpstrf on these cases."""
+    """The cooperative left-looking selection (default), its split form with only the first
+    K columns of the owned L rows in LDS (forced here with FISDF_SEL_LDS_COLS; the default when
+    the rows do not fit, as in C5) and the blocked right-looking one (FISDF_SEL_COOP=0) pick
+    the same pivots as dpstrf on these cases."""
     perms = {}
-    for coop in ("1", "0"):
-        monkeypatch.setenv("FISDF_SEL_COOP", coop)
+    for mode, env in (("coop", {"FISDF_SEL_COOP": "1"}),
+                      ("split", {"FISDF_SEL_COOP": "1", "FISDF_SEL_LDS_COLS": "20"}),
+                      ("blocked", {"FISDF_SEL_COOP": "0"})):
+        monkeypatch.delenv("FISDF_SEL_LDS_COLS", raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         df, o, dm = make_df(name, inject=False)
         df.build()
-        perms[coop] = df.perm.copy()
-    print(f"{name}: coop == blocked: {np.array_equal(perms['1'], perms['0'])}, "
-          f"coop == dpstrf: {np.array_equal(perms['1'], o['perm'])}")
-    assert np.array_equal(perms["1"], perms["0"])
-    assert np.array_equal(perms["1"], o["perm"])
+        perms[mode] = df.perm.copy()
+    print(f"{name}: " + ", ".join(f"{m} == dpstrf: {np.array_equal(p, o['perm'])}"
+                                  for m, p in perms.items()))
+    for m, p in perms.items():
+        assert np.array_equal(p, o["perm"]), m
 
 
 @pytest.mark.parametrize("name", ["toy222", "diamond_szv_gamma"])
