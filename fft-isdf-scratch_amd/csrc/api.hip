@@ -50,6 +50,7 @@ struct fisdf_ctx {
   cplx* f_Linv = nullptr;   // (nk, nblk*nb*nb)
   cplx* f_Q = nullptr;      // (nk, nip, nip) block-row operator of trsm_merged (build_trsm_q)
   cplx* f_Li = nullptr;     // (nk, nip, nip) L^{-1} (pivot order) = trsm_merged on the identity
+  cplx* f_ksw = nullptr;    // split-K partials of that substitution (kFacSplitElems)
   cplx* f_x4s = nullptr;    // (nk, nip, nip) staged x4_q of the factored slots
   int* f_fail_pinned = nullptr;  // unpivoted path: per-slot failure flags (host, pinned)
   int* f_qr_pinned = nullptr;    // factored q-list + real flags (2 nk ints, pinned) and device copy
@@ -261,6 +262,8 @@ int free_factors(fisdf_ctx* c) {
   c->f_Q = nullptr;
   if (c->f_Li) FISDF_HIP(hipFree(c->f_Li));
   c->f_Li = nullptr;
+  if (c->f_ksw) FISDF_HIP(hipFree(c->f_ksw));
+  c->f_ksw = nullptr;
   if (c->f_x4s) FISDF_HIP(hipFree(c->f_x4s));
   c->f_x4s = nullptr;
   if (c->f_M) FISDF_HIP(hipFree(c->f_M));
@@ -1078,6 +1081,9 @@ int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk
 // need_linv: the diagonal-block inverses of Lp (trsm_blocked, used only when some rank < nip;
 // the unpivoted path is full-rank by construction — a failing slot is refactored, and this
 // rerun, by factor_pivoted_slots)
+// split-K workspace of the L^{-1} substitution: <= 256 tiles of 64 x 64 partials
+constexpr long kFacSplitElems = 256L * 64 * 64;
+
 int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src, bool need_linv) {
   const int nk = c->f_nk, nip = c->f_nip, nb = c->f_nb, nblk = (nip + nb - 1) / nb;
   const long nn = (long)nip * nip;
@@ -1095,7 +1101,8 @@ int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src, bool nee
   // as one lower-triangular GEMM over the grid; J/K within 2-3x of the TRSM's rounding,
   // tests/experiments/explicit_tri_inverse.py)
   FISDF_TRY(set_identity(s, c->f_Li, nip, nk));
-  FISDF_TRY(trsm_merged_batched(s, c->f_Q, nn, nip, c->f_Li, nip, nn, nip, nk, true));
+  FISDF_TRY(trsm_merged_batched(s, c->f_Q, nn, nip, c->f_Li, nip, nn, nip, nk, true, c->f_ksw,
+                                 kFacSplitElems));
   return 0;
 }
 
@@ -1213,6 +1220,7 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   FISDF_HIP(hipMalloc(&c->f_Linv, sizeof(cplx) * (size_t)nk * nblk * nb * nb));
   FISDF_HIP(hipMalloc(&c->f_Q, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_Li, sizeof(cplx) * nk * nn));
+  FISDF_HIP(hipMalloc(&c->f_ksw, sizeof(cplx) * kFacSplitElems));
   FISDF_HIP(hipMalloc(&c->f_piv, sizeof(int) * (size_t)nk * nip));
   FISDF_HIP(hipMalloc(&c->f_rank_dev, sizeof(int) * nk));
   FISDF_HIP(hipHostMalloc((void**)&c->f_rank_pinned, sizeof(int) * nk, hipHostMallocDefault));

@@ -17,7 +17,8 @@ int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int ldl, long sL, int nb,
 int build_trsm_q(hipStream_t s, const cplx* Lp, int r, long sL, cplx* Q, int batch, int mode);
 int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol, int mode);
 int trsm_merged_batched(hipStream_t s, const cplx* Q, long sQ, int r, cplx* X, long ld, long sX,
-                        int ncol, int batch, bool lower_rhs = false);
+                        int ncol, int batch, bool lower_rhs = false, cplx* work = nullptr,
+                        long work_elems = 0);
 int set_identity(hipStream_t s, cplx* X, int n, int batch);
 int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, long ldl, long sL, int r,
                  const cplx* Linv, long sLi, int nb, cplx* B, long ldb, long sB, cplx* X, long ldx,

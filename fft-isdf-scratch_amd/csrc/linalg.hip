@@ -884,8 +884,11 @@ int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol,
 // trsm_merged over a batch (Q and X with batch strides sQ, sX): one launch per block row.
 // lower_rhs: X is lower-triangular (the identity, for L^{-1}), so block row b only has
 // columns < b1 to compute (the rest stay zero)
+// work (work_elems cplx, may be null): split-K partials for block rows whose grid would leave
+// most CUs idle (a small batch: each 64 x 64 tile otherwise runs its whole K = b1 alone); the
+// partials are reduced by a later kernel, so the in-place update stays safe
 int trsm_merged_batched(hipStream_t s, const cplx* Q, long sQ, int r, cplx* X, long ld, long sX,
-                        int ncol, int batch, bool lower_rhs) {
+                        int ncol, int batch, bool lower_rhs, cplx* work, long work_elems) {
   const int nblk = (r + 63) / 64;
   if (nblk == 0 || batch == 0) return 0;
   const int s0 = r - 64 * (nblk - 1);
@@ -893,8 +896,15 @@ int trsm_merged_batched(hipStream_t s, const cplx* Q, long sQ, int r, cplx* X, l
   for (int b = 0; b < nblk; ++b) {
     const int b0 = b == 0 ? 0 : s0 + (b - 1) * 64;
     const int m = std::min(b == 0 ? s0 : 64, r - b0), b1 = b0 + m;
-    FISDF_TRY(zgemm(s, OP_N, OP_N, m, lower_rhs ? std::min(ncol, b1) : ncol, b1, one,
-                    Q + (long)b0 * r, r, sQ, X, ld, sX, zero, X + (long)b0 * ld, ld, sX, batch, 1));
+    const int nc = lower_rhs ? std::min(ncol, b1) : ncol;
+    const long tiles = (long)((nc + 63) / 64) * batch;
+    int ks = 1;
+    if (work && tiles < 128 && b1 >= 256) {
+      ks = (int)std::min<long>({256 / tiles, b1 / 128, 16});
+      while (ks > 1 && (long)ks * batch * m * nc > work_elems) --ks;
+    }
+    FISDF_TRY(zgemm(s, OP_N, OP_N, m, nc, b1, one, Q + (long)b0 * r, r, sQ, X, ld, sX, zero,
+                    X + (long)b0 * ld, ld, sX, batch, std::max(ks, 1), ks > 1 ? work : nullptr));
   }
   return 0;
 }
