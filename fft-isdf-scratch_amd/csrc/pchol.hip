@@ -713,7 +713,10 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(cplx* __restrict__ W, in
 #define FISDF_DIAG_PRIO 3
 #endif
   __builtin_amdgcn_s_setprio(FISDF_DIAG_PRIO);
-  __shared__ cplx Ls[64][65];  // L (inverse phase)
+  // inverse phase: L in the lower triangle of Ls, X = L^{-1} (lower) transposed into its upper
+  // triangle — X(i, j), j <= i, at Ls[j][i + 1] — so the block needs one 64 x 65 array
+  __shared__ cplx Ls[64][65];
+  __shared__ cplx Ts[3][16][17];
   __shared__ cplx vec[2][64];  // column k of the factor / row k of the inverse, by parity
   __shared__ double dsq[2];
   __shared__ int bad;
@@ -780,45 +783,57 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(cplx* __restrict__ W, in
       if (i < m && j <= i) W[(long)(b0 + i) * n + b0 + j] = a[r][c];
     }
   __syncthreads();
-  // inverse of the lower-triangular block: X = L^{-1} by right-looking forward substitution
-  // on the identity (row k final once rows < k have been subtracted; then scaled by 1/L_kk)
-  cplx x[4][4];
+  // inverse of the lower-triangular block, 16 x 16 blocked: wave w inverts diagonal block w by
+  // forward substitution (all four in the same 16 barrier steps), then the off-diagonal blocks
+  // by block diagonals, X_ij = -X_ii sum_{k=j}^{i-1} L_ik X_kj (d = i - j = 1, 2, 3: two
+  // barriers each) — 22 barrier steps instead of 64
+  {
+    const int w = t >> 6, lane = t & 63, rr = lane >> 2, cc = (lane & 3) * 4, o = 16 * w;
+    cplx x[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) x[r][c] = cmk(r0 + r == c0 + c ? 1.0 : 0.0, 0.0);
-  for (int kb = 0; 4 * kb < m; ++kb) {
-#pragma unroll
-    for (int kr = 0; kr < 4; ++kr) {
-      const int k = 4 * kb + kr, p = kr & 1;
-      if (k >= m) break;
-      if (bi == kb) {
-        const double d = 1.0 / Ls[k][k].x;
+    for (int c = 0; c < 4; ++c) x[c] = cmk(rr == cc + c ? 1.0 : 0.0, 0.0);
+    for (int k = 0; k < 16; ++k) {
+      if (rr == k) {
+        const double d = o + k < m ? 1.0 / Ls[o + k][o + k].x : 1.0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          x[kr][c] = cscale(x[kr][c], d);
-          vec[p][c0 + c] = x[kr][c];
+          x[c] = cscale(x[c], d);
+          if (cc + c <= k) Ls[o + cc + c][o + k + 1] = x[c];
         }
       }
       __syncthreads();
-      cplx xk[4], lik[4];
+      if (rr > k) {
+        const cplx l = Ls[o + rr][o + k];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) xk[c] = vec[p][c0 + c];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) lik[r] = (r0 + r > k && r0 + r < m) ? Ls[r0 + r][k] : cmk(0, 0);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) x[r][c] = csub(x[r][c], cmul(lik[r], xk[c]));
+        for (int c = 0; c < 4; ++c)
+          if (cc + c <= k) x[c] = csub(x[c], cmul(l, Ls[o + cc + c][o + k + 1]));
+      }
     }
   }
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int i = r0 + r, j = c0 + c;
-      Linv[i * 64 + j] = (i < m && j < m) ? x[r][c] : cmk(i == j ? 1.0 : 0.0, 0.0);
+  {
+    const int r = t >> 4, cidx = t & 15;
+    for (int d = 1; d < 4; ++d) {
+      for (int j = 0; j + d < 4; ++j) {  // T_j = sum_{k=j}^{i-1} L_ik X_kj, i = j + d
+        const int i = j + d;
+        cplx acc = cmk(0, 0);
+        for (int l = 16 * j + cidx; l < 16 * i; ++l)  // X(l, c) = 0 for c > l
+          acc = cadd(acc, cmul(Ls[16 * i + r][l], Ls[16 * j + cidx][l + 1]));
+        Ts[j][r][cidx] = acc;
+      }
+      __syncthreads();
+      for (int j = 0; j + d < 4; ++j) {  // X_ij = -X_ii T_j
+        const int i = j + d;
+        cplx acc = cmk(0, 0);
+        for (int l = 0; l <= r; ++l) acc = cadd(acc, cmul(Ls[16 * i + l][16 * i + r + 1], Ts[j][l][cidx]));
+        Ls[16 * j + cidx][16 * i + r + 1] = cmk(-acc.x, -acc.y);
+      }
+      __syncthreads();
     }
+  }
+  for (int e = t; e < 4096; e += 256) {
+    const int i = e >> 6, j = e & 63;
+    Linv[e] = (i < m && j < m) ? (j <= i ? Ls[j][i + 1] : cmk(0, 0)) : cmk(i == j ? 1.0 : 0.0, 0.0);
+  }
   __syncthreads();
   if (t == 0 && bad) fail[b] = 1;
 }
