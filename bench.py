@@ -49,7 +49,14 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-q", type=int, default=4, help="q-points fitted in the CPU sample")
+    p.add_argument("--no-isolated", action="store_true",
+                   help="skip the untimed single-lane step (profiling runs: only warmup + timed "
+                        "steps reach the profiler)")
+    p.add_argument("--cpu-q", type=int, default=8, help="q-points fitted in the CPU sample")
+    p.add_argument("--emulate-ranks", type=int, default=0, metavar="N",
+                   help="time, on this one GPU, each rank's share of an N-rank k-sharded build "
+                        "(its compute; collectives replaced by their local effect, kshard."
+                        "EmulatedGroup) and print one JSON line with the per-rank step times")
     return p.parse_args()
 
 
@@ -86,12 +93,18 @@ def cpu_baseline(cell, kmesh, m0, c0, x0, chi, dm, nq):
     t0 = time.perf_counter()
     x4 = R.build_x4(xip, phase)
     t["x4"] = time.perf_counter() - t0
-    # sampled q: Gamma plus complex q (2 k_q not a reciprocal vector) spread over the mesh
+    # sampled q: Gamma, self-conjugate q (2 k_q a reciprocal vector) and complex q spread over
+    # the mesh, in the proportion the mesh has them (the reference treats every q alike)
     ks = np.stack(np.unravel_index(np.arange(nk), tuple(kmesh)), 1)
-    cplx = [q for q in range(nk) if ((2 * ks[q]) % np.asarray(kmesh)).any()] or list(range(1, nk))
-    qs = [0] + [cplx[i] for i in np.linspace(0, len(cplx) - 1, max(nq - 1, 0)).astype(int)
-                if cplx][:max(nq - 1, 0)]
-    qs = sorted(set(qs))[:nk]
+    selfc = [q for q in range(1, nk) if not ((2 * ks[q]) % np.asarray(kmesh)).any()]
+    cplx = [q for q in range(nk) if ((2 * ks[q]) % np.asarray(kmesh)).any()]
+    nq = min(nq, nk)
+    n_self = min(len(selfc), max(1 if selfc else 0, round((nq - 1) * len(selfc) / max(nk - 1, 1))))
+    n_cplx = min(len(cplx), nq - 1 - n_self)
+
+    def spread(v, n):
+        return [v[i] for i in np.linspace(0, len(v) - 1, n).astype(int)] if n > 0 else []
+    qs = sorted(set([0] + spread(selfc, n_self) + spread(cplx, n_cplx)))
     # the y build of fftisdf.py:67-87 over the whole grid in its 8000-point blocks; the
     # 28.7 GB y (C3) is not kept, only the sampled q columns
     yq = np.empty((len(qs), ngrid, nip), complex)
@@ -124,17 +137,108 @@ def cpu_baseline(cell, kmesh, m0, c0, x0, chi, dm, nq):
         affinity = len(os.sched_getaffinity(0))
     except Exception:
         affinity = None
+    share = os.environ.get("OMP_NUM_THREADS")
     return dict(value=nk / total, unit="k-points/s", cores=int(cores), kind="port",
                 sample=(f"oracle (NumPy/SciPy gelsy restatement of fftisdf.py) timed on "
                         f"selection + x4 + the full-grid y build ({ngrid} points) + gelsy fit/"
                         f"FFT/W for q {qs} of {nk} (x{nk / len(qs):.0f}) + get_jk "
-                        f"(est. {total:.1f} s/job)"),
-                affinity_cpus=affinity, host_cpus=os.cpu_count(),
+                        f"(est. {total:.1f} s/job); BLAS threads = FFT workers = the box's CPU "
+                        f"share"),
+                cpu_share=int(share) if share and share.isdigit() else None,
+                fft_workers=R._fft_workers(), affinity_cpus=affinity, host_cpus=os.cpu_count(),
                 stages_s={k: round(v, 3) for k, v in t.items()})
+
+
+def emulate_ranks(args):
+    """Per-rank compute of an N-way k-sharded C3 build, one rank at a time on this
+    GPU: replicated selection + x4, the y build on the rank's grid slice for every fitted q, the
+    unpack of its all-to-all pieces (handed over pre-filled from a full 1-GPU y, so the fit sees
+    real data), its q-chunk's factor + fit, its W_s row-block partials + the local part of the
+    reduce-scatter, its get_jk rows.  The max over ranks is the compute critical path of the
+    N-GPU step; the collectives' transfer time is reported as a bytes budget beside it."""
+    import torch
+    from fisdf import ISDF, kshard
+    torch.cuda.set_device(0)
+    cell, kmesh, m0, c0, x0, chi, dm = setup(args.config)
+    nk = int(np.prod(kmesh))
+    N = args.emulate_ranks
+    # the interpolation points and the full y of every fitted q (untimed, once)
+    ref = ISDF(cell, cell.get_kpts(kmesh), m0=list(m0), c0=c0)
+    d = ref.device
+    ref._kmesh()
+    ref._ao_parent = d.to_dev(x0)
+    ref._ao_grid = d.to_dev(chi)
+    ref._select()
+    X = ref._dev_state["X"]
+    nip, nao = X.shape[1], cell.nao_nr()
+    from fisdf import _lib
+    from fisdf.isdf import _fit_qset
+    fit_qs, partner, weight = _fit_qset(ref, np.asarray(kmesh))
+    ngrid = int(np.prod(cell.mesh))
+    yall = d.empty((len(fit_qs), nip, ngrid))
+    km_c, km_p = _lib.iarr(kmesh)
+    a_c, a_p = _lib.darr(np.asarray(cell.lattice_vectors(), float).ravel())
+    qs = np.ascontiguousarray(fit_qs, dtype=np.int32)
+    d.ctx.call("fisdf_set_time_reversal", 1)
+    d.ctx.call("fisdf_build_y_qs", _lib.ptr(ref._ao_grid), ngrid * nao, 0, ngrid, ngrid,
+               _lib.ptr(X), nip, nao, km_p, a_p, qs.ctypes.data_as(_lib._ip), len(qs),
+               _lib.ptr(yall))
+    real_q = np.array([partner[q] == q for q in fit_qs])
+    chunks = kshard.balanced_chunks(np.where(real_q, 0.6, 1.0), N)
+    slices = kshard.grid_slices(cell.mesh, N)
+    per_rank = []
+    for R in range(N):
+        pieces = kshard.emulated_pieces(yall, chunks, slices, R)
+        df = ISDF(cell, cell.get_kpts(kmesh), m0=list(m0), c0=c0,
+                  comm=kshard.EmulatedGroup(R, N, pieces))
+        df._kmesh()
+        df._ao_parent, df._ao_grid = ref._ao_parent, ref._ao_grid
+
+        def step():
+            df._dev_state = None
+            df.build()
+            df.get_jk(dm)
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        df.device.ctx.call("fisdf_set_timing", 1)
+        df.device.ctx.timings()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / args.steps
+        st = df.device.ctx.timings()
+        df.device.ctx.call("fisdf_set_timing", 0)
+        assert np.array_equal(df.perm, ref.perm)
+        per_rank.append({"rank": R, "q": [int(q) for q in df.my_qs], "ms_per_step": round(dt * 1e3, 3),
+                         "stages_ms": {k: round(v[0] / args.steps, 3) for k, v in st.items()
+                                       if v[0] > 0}})
+        del df, pieces
+        torch.cuda.empty_cache()
+    worst = max(per_rank, key=lambda r: r["ms_per_step"])
+    # collective bytes of the worst rank (fp64): the chunked all-to-all of y (its q on the other
+    # ranks' slices in, its slice of the others' q out) and the W_s reduce-scatter (real parts)
+    R = worst["rank"]
+    a0, a1 = chunks[R]
+    ng_self = slices[R][1]
+    a2a_in = (a1 - a0) * nip * (ngrid - ng_self) * 16
+    a2a_out = (len(fit_qs) - (a1 - a0)) * nip * ng_self * 16
+    ws_rs = (N - 1) / N * nk * nip * nip * 8
+    out = {"metric": "per-rank compute time of an emulated k-sharded step", "config": args.config,
+           "n_ranks": N, "steps": args.steps, "warmup": args.warmup,
+           "one_gpu_reference": "bench.py default line (same config)",
+           "max_rank_ms": worst["ms_per_step"], "worst_rank": R,
+           "comm_bytes_worst_rank": {"all_to_all_in": a2a_in, "all_to_all_out": a2a_out,
+                                     "ws_reduce_scatter": ws_rs},
+           "ranks": per_rank}
+    print(json.dumps(out))
 
 
 def main():
     args = parse()
+    if args.emulate_ranks > 0:
+        return emulate_ranks(args)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -205,8 +309,8 @@ def main():
         if not re or not half:
             ncols.append(ngrid)
             continue
-        m0 = 2 * int(np.unravel_index(int(q), tuple(km))[0]) // int(km[0])
-        nh = max(i0 + 1 for i0 in range(n0) if i0 <= (-i0 - m0) % n0)
+        mq = 2 * int(np.unravel_index(int(q), tuple(km))[0]) // int(km[0])
+        nh = max(i0 + 1 for i0 in range(n0) if i0 <= (-i0 - mq) % n0)
         ncols.append(nh * n1 * n2)
     flop_step = float(np.sum(np.where(real, 2.0, 4.0) * ranks ** 2 * np.asarray(ncols, float)))
     KERNELS = {
@@ -227,17 +331,30 @@ def main():
                        "flop_per_launch": flop_step / max(len(ranks), 1),
                        "avg_launch_ms": ms / max(calls, 1), "launches": int(calls),
                        "ms_per_step": round(ms / args.steps, 3)}
+    # step-level MFMA work of the algorithm actually run: the fit's two GEMMs above
+    # plus the y build's fx GEMM (time-reversal representatives), the x4 GEMMs and the selection
+    # Gram (real part, K = nk nao) — every other stage is HBM- or latency-bound
+    nao, nip = cell.nao_nr(), int(df.nip)
+    ng0 = int(np.prod(m0))
+    nk_half = len(set(min(q, int(p)) for q, p in enumerate(df.q_partner)))
+    flop_other = (8.0 * nk_half * ngrid * nao * nip          # y: fx_k = X_k f_k^H
+                  + 8.0 * nk * nip * nip * nao               # x4: x2_k = X_k^* X_k^T
+                  + 2.0 * ng0 * ng0 * nk * nao)              # selection: Re(P P^H), lower half
+    step_flop = 2 * flop_step + flop_other                   # trsm + herk, same count
+
     # in the timed region the fit lanes share the CUs, so the per-launch durations above
     # include contention with the other lane's kernels; one extra untimed step with a single
     # lane gives each kernel's own rate
-    d.ctx.call("fisdf_set_fit_lanes", 1)
-    d.ctx.call("fisdf_set_timing", 1)
-    d.ctx.timings()
-    step()
-    torch.cuda.synchronize()
-    iso_st = d.ctx.timings()
-    d.ctx.call("fisdf_set_timing", 0)
-    d.ctx.call("fisdf_set_fit_lanes", 0)
+    iso_st = {k: (0.0, 0) for k in stages}
+    if not args.no_isolated:
+        d.ctx.call("fisdf_set_fit_lanes", 1)
+        d.ctx.call("fisdf_set_timing", 1)
+        d.ctx.timings()
+        step()
+        torch.cuda.synchronize()
+        iso_st = d.ctx.timings()
+        d.ctx.call("fisdf_set_timing", 0)
+        d.ctx.call("fisdf_set_fit_lanes", 0)
     tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     traffic = json.load(open(tfile)) if os.path.exists(tfile) else {}
     for name, (label, tkey) in KERNELS.items():
@@ -291,6 +408,15 @@ def main():
                        "parallelism": f"k-shard x{world}"},
             "roofline": roof,
             "roofline_secondary": roof2,
+            "step_mfma": {"flop_per_step": step_flop, "fit_flop_per_step": 2 * flop_step,
+                          "achieved": round(step_flop / (ms_per_step * 1e-3) / 1e12, 3),
+                          "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                          "frac": round(step_flop / (ms_per_step * 1e-3) / 1e12
+                                        / PEAK_FP64_TFLOPS, 4),
+                          "note": "algorithmic MFMA work of the algorithm run (fit TRSM + HERK "
+                                  "at 4 r^2 N each per complex q, 2 r^2 N_half per self-"
+                                  "conjugate q; y fx GEMM; x4; selection Gram) over the whole "
+                                  "step time"},
             "cpu_baseline": cpu,
             "ao_eval": ao,
             "stages_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()},
@@ -304,6 +430,10 @@ def main():
     d.ctx.close()
     if comm is not None:
         torch.distributed.destroy_process_group()
+    maps = os.environ.get("FISDF_MAPS_OUT")
+    if maps:  # the address map, to symbolize a crash in the exit handlers after this point
+        with open("/proc/self/maps") as src, open(maps, "w") as dst:
+            dst.write(src.read())
 
 
 if __name__ == "__main__":

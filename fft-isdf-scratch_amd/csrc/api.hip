@@ -19,6 +19,11 @@ namespace fisdf {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
+LaunchEvents& launch_events() {
+  static thread_local LaunchEvents ev;
+  return ev;
+}
+
 }  // namespace fisdf
 
 using namespace fisdf;
@@ -48,9 +53,10 @@ struct fisdf_ctx {
   cplx* f_L = nullptr;      // (nk, nip, nip) raw left-looking factor (row order)
   cplx* f_Lp = nullptr;     // (nk, nip*nip) pivot-order factor, ld = rank_q
   cplx* f_Linv = nullptr;   // (nk, nblk*nb*nb)
-  cplx* f_Q = nullptr;      // (nk, nip, nip) block-row operator of trsm_merged (build_trsm_q)
-  cplx* f_Li = nullptr;     // (nk, nip, nip) L^{-1} (pivot order) = trsm_merged on the identity
-  cplx* f_ksw = nullptr;    // split-K partials of that substitution (kFacSplitElems)
+  cplx* f_Q = nullptr;      // (nk, nip, nip) block-row operator of trsm_merged_batched (build_trsm_q)
+  cplx* f_Li = nullptr;     // (nk, nip, nip) L^{-1} (pivot order) = trsm_merged_batched on the identity
+  cplx* f_ksw = nullptr;    // split-K partials of that substitution (trsm_split_work_elems)
+  long f_ksw_elems = 0;
   cplx* f_x4s = nullptr;    // (nk, nip, nip) staged x4_q of the factored slots
   int* f_fail_pinned = nullptr;  // unpivoted path: per-slot failure flags (host, pinned)
   int* f_qr_pinned = nullptr;    // factored q-list + real flags (2 nk ints, pinned) and device copy
@@ -76,7 +82,7 @@ struct fisdf_ctx {
   std::vector<hipEvent_t> ev_q;  // FISDF_FIT_PIPE: Yhat of fitted q ready (FFT stream)
   std::vector<hipEvent_t> ev_free;  // FISDF_FIT_PIPE: Yhat ring slot read by its lane
   int pipe_mode = -1;   // fisdf_set_fit_pipe; -1: environment FISDF_FIT_PIPE (default on)
-  int pipe_depth = 0;   // ring slots; 0: FISDF_PIPE_DEPTH or lanes + 2
+  int pipe_depth = 0;   // ring slots; 0: lanes + 2
   int last_fit_lanes = 0, last_fit_pipe = 0;  // what the last fisdf_fit_coulomb_qs ran with
   std::vector<hipEvent_t> ev_ready;  // fisdf_mark_y_ready: y of local q j landed (sharded fit)
   std::vector<char> ready_marked;
@@ -161,22 +167,38 @@ int upload_ints(fisdf_ctx* c, const int* h, int n, int* d) {
   return n <= 0 ? 0 : upload_bytes(c, h, sizeof(int) * (size_t)n, d);
 }
 
+// Stage timer on stream `st`.  Default: events recorded on the stream around the stage.
+// kernel_exact: the stage is ONE zgemm()/herk() call, whose first kernel takes `a` and whose last
+// kernel takes `b` at launch (launch_events, hipExtLaunchKernelGGL) — the kernels' own begin /
+// end, as rocprofv3's kernel trace reports them, without the time the stream waits for CUs the
+// other fit lanes hold between the two stream positions.
 struct StageTimer {
   fisdf_ctx* c;
   int stage;
   hipStream_t st;
+  bool exact;
   hipEvent_t a = nullptr, b = nullptr;
-  StageTimer(fisdf_ctx* c_, int stg, hipStream_t on = nullptr)
-      : c(c_), stage(stg), st(on ? on : c_->stream) {
+  StageTimer(fisdf_ctx* c_, int stg, hipStream_t on = nullptr, bool kernel_exact = false)
+      : c(c_), stage(stg), st(on ? on : c_->stream), exact(kernel_exact) {
     if (c->timing) {
       (void)hipEventCreate(&a);
       (void)hipEventCreate(&b);
-      (void)hipEventRecord(a, st);
+      if (exact)
+        launch_events() = LaunchEvents{a, b};
+      else
+        (void)hipEventRecord(a, st);
     }
   }
   ~StageTimer() {
     if (c->timing) {
-      (void)hipEventRecord(b, st);
+      if (exact) {
+        LaunchEvents& le = launch_events();
+        if (le.start == a) (void)hipEventRecord(a, st);  // no kernel ran: an empty interval
+        if (le.stop == b || le.start == a) (void)hipEventRecord(b, st);
+        le = LaunchEvents();
+      } else {
+        (void)hipEventRecord(b, st);
+      }
       c->events.push_back({stage, a, b});
     }
   }
@@ -264,6 +286,7 @@ int free_factors(fisdf_ctx* c) {
   c->f_Li = nullptr;
   if (c->f_ksw) FISDF_HIP(hipFree(c->f_ksw));
   c->f_ksw = nullptr;
+  c->f_ksw_elems = 0;
   if (c->f_x4s) FISDF_HIP(hipFree(c->f_x4s));
   c->f_x4s = nullptr;
   if (c->f_M) FISDF_HIP(hipFree(c->f_M));
@@ -437,13 +460,7 @@ int env_fit_pipe() {
   return v;
 }
 
-int env_pipe_depth(int lanes) {
-  static const int v = [] {
-    const char* e = getenv("FISDF_PIPE_DEPTH");
-    return e ? atoi(e) : 0;
-  }();
-  return v > 0 ? v : lanes + 2;
-}
+int default_pipe_depth(int lanes) { return lanes + 2; }
 
 int num_cus(int device) {
   int n = 0;
@@ -748,6 +765,43 @@ int fisdf_pivoted_cholesky(fisdf_ctx* c, const void* A, int n, int batch, int rm
   return 0;
 }
 
+int fisdf_cholesky(fisdf_ctx* c, void* A, int n, int batch, double tol_rel, int* h_fail) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(n >= 1 && batch >= 1, "cholesky: bad sizes");
+  Carver cv;
+  size_t oW = cv.take(sizeof(cplx) * (size_t)batch * 4096 + sizeof(double) * batch);
+  size_t oP = cv.take(sizeof(int) * (size_t)batch * n);
+  size_t oR = cv.take(sizeof(int) * batch);
+  size_t oF = cv.take(sizeof(int) * batch);
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  char* b = (char*)base;
+  FISDF_TRY(chol_unpivoted(c->stream, (cplx*)A, n, batch, tol_rel, (int*)(b + oP), (int*)(b + oR),
+                           (int*)(b + oF), (cplx*)(b + oW)));
+  FISDF_HIP(hipMemcpyAsync(h_fail, b + oF, sizeof(int) * batch, hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int fisdf_tri_inverse(fisdf_ctx* c, const void* L, int n, int batch, void* Linv) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(n >= 1 && batch >= 1, "tri_inverse: bad sizes");
+  const long nn = (long)n * n, we = std::max(1L, trsm_split_work_elems(n, batch));
+  Carver cv;
+  size_t oQ = cv.take(sizeof(cplx) * (size_t)batch * nn);
+  size_t oK = cv.take(sizeof(cplx) * (size_t)we);
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  cplx* Q = (cplx*)((char*)base + oQ);
+  // the factor stage's own sequence (factor_finish): block-row operator, then the merged
+  // substitution applied to the identity
+  FISDF_TRY(build_trsm_q(c->stream, (const cplx*)L, n, nn, Q, batch, GEMM_FULL));
+  FISDF_TRY(set_identity(c->stream, (cplx*)Linv, n, batch));
+  FISDF_TRY(trsm_merged_batched(c->stream, Q, nn, n, (cplx*)Linv, n, nn, n, batch, true,
+                                (cplx*)((char*)base + oK), we));
+  return 0;
+}
+
 // ---- A1 ---------------------------------------------------------------------
 int fisdf_select_points(fisdf_ctx* c, const void* x0v, int nk, int ng0, int nao, int nip_max,
                         double tol, int* h_perm, int* h_npiv, int* h_full_rank) {
@@ -981,15 +1035,12 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
   // short-K changes: y 28.1 / 22.7 / 20.9 / 18.4 / 16.7 ms for 128 MB / 256 MB / 512 MB /
   // 1 GB / 2 GB — cache-sized blocks lose more to the smaller GEMM/DFT launches than they
   // gain from Infinity-Cache residency; bigger blocks slow the side-stream factorisation)
-  static const long yblk_bytes = [] {
-    const char* e = getenv("FISDF_YBLK_MB");
-    return (e ? atol(e) : 2048L) << 20;
-  }();
+  constexpr long yblk_bytes = 2048L << 20;
   // time reversal (fisdf_set_time_reversal): fx_k only for the representatives k <= -k, the
   // others are conj(fx_{-k}) inside kmesh_y — 36 of 64 k at 4x4x4
   const bool half = c->time_reversal;
   if (half && nblk > 0) {
-    // fused fx + k-mesh DFT (FISDF_Y_FUSED, default on): no fx round trip through HBM
+    // fused fx + k-mesh DFT where the k-mesh allows it: no fx round trip through HBM
     bool done = false;
     const size_t yw = y_fused_workspace(kmesh, nip, nao, nblk);
     if (yw) {
@@ -1006,14 +1057,10 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
   const long per_g = (long)nks * nip * sizeof(cplx);
   int gb = (int)std::max(64L, std::min<long>(nblk, yblk_bytes / std::max(per_g, 1L)));
   gb = std::min(gb, std::max(nblk, 1));
-  // pipelined (FISDF_Y_PIPE, default on): the fx GEMM of block i+1 (main stream) runs beside
-  // the k-mesh DFT of block i (aux stream) on two fx buffers — the GEMM is write/compute
-  // bound, the DFT read/write bound, and neither alone saturates HBM
-  static const bool pipe_env = [] {
-    const char* e = getenv("FISDF_Y_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  const int nbuf = pipe_env && gb < nblk ? 2 : 1;
+  // pipelined: the fx GEMM of block i+1 (main stream) runs beside the k-mesh DFT of block i
+  // (aux stream) on two fx buffers — the GEMM is write/compute bound, the DFT read/write bound,
+  // and neither alone saturates HBM
+  const int nbuf = gb < nblk ? 2 : 1;
   Carver cv;
   size_t o1[2];
   for (int i = 0; i < nbuf; ++i) o1[i] = cv.take((size_t)per_g * gb);
@@ -1029,8 +1076,7 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
     FISDF_HIP(hipEventRecord(c->ev_fork, c->stream));
     FISDF_HIP(hipStreamWaitEvent(sk, c->ev_fork, 0));
   }
-  static const int fx_epi = getenv("FISDF_FX_NT") && getenv("FISDF_FX_NT")[0] == '0'
-                                ? EPI_NONE : EPI_STREAM;
+  const int fx_epi = EPI_STREAM;  // fx is read back by the DFT only a block later
   int blk = 0;
   for (int s0 = 0; s0 < nblk; s0 += gb, ++blk) {
     const int m = std::min(gb, nblk - s0);
@@ -1081,9 +1127,6 @@ int fisdf_build_y(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int nblk
 // need_linv: the diagonal-block inverses of Lp (trsm_blocked, used only when some rank < nip;
 // the unpivoted path is full-rank by construction — a failing slot is refactored, and this
 // rerun, by factor_pivoted_slots)
-// split-K workspace of the L^{-1} substitution: <= 256 tiles of 64 x 64 partials
-constexpr long kFacSplitElems = 256L * 64 * 64;
-
 int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src, bool need_linv) {
   const int nk = c->f_nk, nip = c->f_nip, nb = c->f_nb, nblk = (nip + nb - 1) / nb;
   const long nn = (long)nip * nip;
@@ -1102,7 +1145,7 @@ int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src, bool nee
   // tests/experiments/explicit_tri_inverse.py)
   FISDF_TRY(set_identity(s, c->f_Li, nip, nk));
   FISDF_TRY(trsm_merged_batched(s, c->f_Q, nn, nip, c->f_Li, nip, nn, nip, nk, true, c->f_ksw,
-                                 kFacSplitElems));
+                                 c->f_ksw_elems));
   return 0;
 }
 
@@ -1170,13 +1213,12 @@ int factor_pivoted_slots(fisdf_ctx* c, hipStream_t s, const std::vector<int>& sl
 
 static int ensure_side(fisdf_ctx* c) {
   if (!c->side) {
-    // FISDF_SIDE_PRIO=1: the factorisation (a chain of small kernels beside the y build's
-    // large ones) on a high-priority stream
-    const char* pe = getenv("FISDF_SIDE_PRIO");
-    int lo = 0, hi = 0;
-    FISDF_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    FISDF_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking,
-                                          (pe && pe[0] == '1') ? hi : lo));
+    // the factor chain (small latency-bound kernels) on the device's LEAST priority: the y
+    // build and the fit go first, the chain fills the gaps (at normal priority the factor ends
+    // 2 ms sooner but the C3 step is 5 ms slower: r03 A/B)
+    int least = 0, greatest = 0;
+    FISDF_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    FISDF_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, least));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_x4, hipEventDisableTiming));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_fac, hipEventDisableTiming));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_chol, hipEventDisableTiming));
@@ -1220,7 +1262,9 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   FISDF_HIP(hipMalloc(&c->f_Linv, sizeof(cplx) * (size_t)nk * nblk * nb * nb));
   FISDF_HIP(hipMalloc(&c->f_Q, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_Li, sizeof(cplx) * nk * nn));
-  FISDF_HIP(hipMalloc(&c->f_ksw, sizeof(cplx) * kFacSplitElems));
+  // split-K partials of the L^{-1} substitution for the whole batch (one launch per block row)
+  c->f_ksw_elems = std::max(1L, trsm_split_work_elems(nip, nk));
+  FISDF_HIP(hipMalloc(&c->f_ksw, sizeof(cplx) * c->f_ksw_elems));
   FISDF_HIP(hipMalloc(&c->f_piv, sizeof(int) * (size_t)nk * nip));
   FISDF_HIP(hipMalloc(&c->f_rank_dev, sizeof(int) * nk));
   FISDF_HIP(hipHostMalloc((void**)&c->f_rank_pinned, sizeof(int) * nk, hipHostMallocDefault));
@@ -1285,9 +1329,6 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   }
   FISDF_HIP(hipEventRecord(c->ev_fac, s));
   c->f_pending = true;
-  // experiment: FISDF_FACTOR_SERIAL=1 makes later work on the main stream wait for the chain
-  static const bool serial = getenv("FISDF_FACTOR_SERIAL") && getenv("FISDF_FACTOR_SERIAL")[0] == '1';
-  if (serial) FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_fac, 0));
   return 0;
 }
 
@@ -1478,6 +1519,12 @@ int fisdf_factor_x4(fisdf_ctx* c, const void* x4v, int q0, int q1, int nip, doub
 int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv, int nip,
                          const int mesh[3], const int kmesh[3], const double a[9], void* Wqv) {
   FISDF_TRY(device_guard(c));
+  // the marks belong to this call: cleared on every return, error returns included, so a failed
+  // call cannot leave the next one running in 'ready' mode against stale events
+  struct ClearMarks {
+    fisdf_ctx* c;
+    ~ClearMarks() { c->ready_marked.assign(c->ready_marked.size(), 0); }
+  } clear_marks{c};
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
   FISDF_TRY(check_qlist(h_qs, nq, nk, "fit_coulomb"));
   // the listed q must be a contiguous run of the factored q-list (slots s0 .. s0+nq-1): the
@@ -1508,14 +1555,10 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       rfmax = nip;
       ++ncod;
     }
-  static const int ks_env = [] {
-    const char* e = getenv("FISDF_HERK_KS");
-    return e ? atoi(e) : 0;
-  }();
   // split-K of each q's HERK from its own rank (not the call's largest), so a q's arithmetic
   // does not depend on which other q share the call (1-GPU vs sharded builds agree bitwise)
   const int ncu = num_cus(c->device);
-  auto ks_of = [&](int r, long K) { return ks_env > 0 ? ks_env : pick_ksplit_herk(r, (int)K, ncu); };
+  auto ks_of = [&](int r, long K) { return pick_ksplit_herk(r, (int)K, ncu); };
   int ks = 1;
   for (int lq = 0; lq < nq; ++lq) ks = std::max(ks, ks_of(c->f_rank[s0 + lq], ngrid));
   // a self-conjugate q is fitted on the prefix planes of its Hermitian G pairs (about half the
@@ -1557,7 +1600,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   const bool ready = nready > 0;
   if (pipe) NL = std::min(NL, ready ? 2 : 3);  // aux[2] is the FFT stream
   if (ready) NL = std::min(NL, 3);
-  int D = pipe ? std::min(nq, c->pipe_depth > 0 ? c->pipe_depth : env_pipe_depth(NL)) : 0;
+  int D = pipe ? std::min(nq, c->pipe_depth > 0 ? c->pipe_depth : default_pipe_depth(NL)) : 0;
   Carver cv;
   size_t oY[4], oU[4], oK[4], oTc[4];
   size_t oYall = 0;
@@ -1612,7 +1655,6 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   cplx* S = (cplx*)(b + oS);
   if (rmax == 0) {
     FISDF_TRY(join_factors(c));
-    c->ready_marked.assign(c->ready_marked.size(), 0);
     FISDF_HIP(hipMemsetAsync(Wq, 0, sizeof(cplx) * nq * nn, c->stream));
     return 0;
   }
@@ -1714,26 +1756,21 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     const long ncol = ncols_of(lq);  // grid columns fitted (half for a self-conjugate q)
     if (c->f_fac_unjoined) FISDF_HIP(hipStreamWaitEvent(st, c->ev_fac, 0));  // L^-1, Q, ...
     {
-      StageTimer tm(c, FISDF_ST_TRSM, st);
-      // U = L^{-1} Yh   (fit, factored order; (x4_q)_PP = L L^H)
-      static const bool tri_gemm = [] {
-        const char* e = getenv("FISDF_TRSM");
-        return !(e && std::string(e) == "merged");
-      }();
+      // U = L^{-1} Yh   (fit, factored order; (x4_q)_PP = L L^H): one GEMM (timed kernel-exact)
+      // on a full-rank q and on a minimum-norm q; the basic solution of a rank-deficient q
+      // (FISDF_FIT_BASIC) substitutes block by block
+      const bool one_gemm = cod_of(sl) || r == nip;
+      StageTimer tm(c, FISDF_ST_TRSM, st, one_gemm);
       if (cod_of(sl)) {  // U = A^+ Yh[P]: the minimum-norm operator over all nip rows
         FISDF_TRY(zgemm(st, OP_N, OP_N, r, (int)ncol, nip, ONE, c->f_M + (long)sl * nn, nip, 0, Yh,
                         ngrid, 0, ZERO, U, ngrid, 0, 1, 1, nullptr, EPI_NONE, nullptr,
                         real_q ? GEMM_A_REAL : GEMM_FULL));
         Uq = U;
-      } else if (r == nip && tri_gemm) {  // one lower-triangular GEMM with L^{-1}
+      } else if (r == nip) {  // one lower-triangular GEMM with L^{-1}
         FISDF_TRY(zgemm(st, OP_N, OP_N, nip, (int)ncol, nip, ONE, c->f_Li + (long)sl * nn, nip, 0,
                         Yh, ngrid, 0, ZERO, U, ngrid, 0, 1, 1, nullptr, EPI_NONE, nullptr,
                         GEMM_A_LOWER | (real_q ? GEMM_A_REAL : GEMM_FULL)));
         Uq = U;
-      } else if (r == nip) {  // merged block-row substitution, in place
-        FISDF_TRY(trsm_merged(st, c->f_Q + (long)sl * nn, nip, Yh, ngrid, (int)ncol,
-                              real_q ? GEMM_A_REAL : GEMM_FULL));
-        Uq = Yh;
       } else {
         FISDF_TRY(trsm_blocked(st, 1, Lp, nip, 0, r, Linv, 0, nb, Yh, ngrid, 0, U, ngrid,
                                0, (int)ncol, 1, real_q ? 1 : 0));
@@ -1741,7 +1778,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     }
     cplx* scratch = Uq == U ? Yh : U;
     {
-      StageTimer tm(c, FISDF_ST_HERK, st);
+      StageTimer tm(c, FISDF_ST_HERK, st, true);
       // G = U U^H  (:121 by Parseval)
       FISDF_TRY(herk(st, r, (int)ncol, 1.0, Uq, ngrid, G + lq * rr, rmax, ks_of(r, ncol), kw,
                      real_q ? GEMM_RE_ONLY : GEMM_FULL));
@@ -1788,7 +1825,6 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     FISDF_HIP(hipEventRecord(c->ev_join[i], c->aux[i]));
     FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_join[i], 0));
   }
-  c->ready_marked.assign(c->ready_marked.size(), 0);
   FISDF_TRY(join_factors(c));
   {
     StageTimer tm(c, FISDF_ST_SMALL);
@@ -1889,6 +1925,49 @@ int fisdf_build_ws_qs(fisdf_ctx* c, const void* Wqv, const int* h_qs, const doub
   FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nn, nq, cmk(std::sqrt((double)nk), 0), dph, nq, 0,
                   (const cplx*)Wqv, nn, 0, ZERO, (cplx*)Wsv, nn, 0, 1, 1, nullptr, EPI_REAL,
                   nullptr));
+  return 0;
+}
+
+int fisdf_build_ws_rows(fisdf_ctx* c, const void* Wqv, const int* h_qs, const double* h_wt, int nq,
+                        int nip, const int kmesh[3], const double a[9], int i0, int i1,
+                        void* Wsv) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(0 <= i0 && i0 <= i1 && i1 <= nip, "build_ws_rows: bad row range");
+  StageTimer tm(c, FISDF_ST_WS);
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  FISDF_TRY(check_qlist(h_qs, nq, nk, "build_ws_rows"));
+  const long nb = i1 - i0, nn = (long)nip * nip;
+  if (nb == 0) return 0;
+  if (nq == 0) {
+    FISDF_HIP(hipMemsetAsync(Wsv, 0, sizeof(cplx) * nk * nb * nip, c->stream));
+    return 0;
+  }
+  CellGeom g;
+  lattice(a, g);
+  std::vector<cplx> ph((size_t)nk * nq);
+  for (int R = 0; R < nk; ++R) {
+    int r2 = R % kmesh[2], r1 = (R / kmesh[2]) % kmesh[1], r0 = R / (kmesh[1] * kmesh[2]);
+    double T[3];
+    for (int cc = 0; cc < 3; ++cc) T[cc] = r0 * g.a[0][cc] + r1 * g.a[1][cc] + r2 * g.a[2][cc];
+    for (int i = 0; i < nq; ++i) {
+      double k[3];
+      kpoint(kmesh, g, h_qs[i], k);
+      const double th = T[0] * k[0] + T[1] * k[1] + T[2] * k[2];
+      const double w = (h_wt ? h_wt[i] : 1.0) / std::sqrt((double)nk);
+      ph[(size_t)R * nq + i] = cmk(w * std::cos(th), w * std::sin(th));
+    }
+  }
+  Carver cv;
+  size_t oP = cv.take(sizeof(cplx) * ph.size());
+  void* base;
+  FISDF_TRY(arena_get(c, cv.off, &base));
+  cplx* dph = (cplx*)((char*)base + oP);
+  FISDF_TRY(upload_bytes(c, ph.data(), sizeof(cplx) * ph.size(), dph));
+  // W_s[R][i0:i1] = sqrt(nk) Re(sum_i Phi_sel[R,i] W_{q_i}[i0:i1]) (fftisdf.py:205-207): the same
+  // GEMM as fisdf_build_ws_qs on the row block (B = W_q rows i0..i1, ld nip^2), written (nk, nb, nip)
+  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, (int)(nb * nip), nq, cmk(std::sqrt((double)nk), 0), dph,
+                  nq, 0, (const cplx*)Wqv + (long)i0 * nip, nn, 0, ZERO, (cplx*)Wsv, nb * nip, 0, 1,
+                  1, nullptr, EPI_REAL, nullptr));
   return 0;
 }
 
@@ -2033,17 +2112,38 @@ int fisdf_get_j(fisdf_ctx* c, const void* Xv, const void* W0, const void* dmsv, 
 }
 
 // ---- A8 -----------------------------------------------------------------------
+static int get_k_block(fisdf_ctx* c, const void* Xv, const cplx* Ws_rows, long ws_Rstride,
+                       const void* dmsv, int nset, int nip, int nao, const int kmesh[3],
+                       const double a[9], int i0, int i1, void* vkv);
+
 int fisdf_get_k_rows(fisdf_ctx* c, const void* Xv, const void* Wsv, const void* dmsv, int nset,
                      int nip, int nao, const int kmesh[3], const double a[9], int i0, int i1,
                      void* vkv) {
   FISDF_TRY(device_guard(c));
   FISDF_CHECK(0 <= i0 && i0 <= i1 && i1 <= nip, "get_k: bad row range");
+  // rows i0.. of W_s[R] inside the full (nk, nip, nip) array
+  return get_k_block(c, Xv, (const cplx*)Wsv + (long)i0 * nip, (long)nip * nip, dmsv, nset, nip,
+                     nao, kmesh, a, i0, i1, vkv);
+}
+
+int fisdf_get_k_rows_local(fisdf_ctx* c, const void* Xv, const void* Ws_rows, const void* dmsv,
+                           int nset, int nip, int nao, const int kmesh[3], const double a[9],
+                           int i0, int i1, void* vkv) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(0 <= i0 && i0 <= i1 && i1 <= nip, "get_k: bad row range");
+  // this rank's rows only: (nk, i1 - i0, nip) from fisdf_build_ws_rows + a reduce-scatter
+  return get_k_block(c, Xv, (const cplx*)Ws_rows, (long)(i1 - i0) * nip, dmsv, nset, nip, nao,
+                     kmesh, a, i0, i1, vkv);
+}
+
+static int get_k_block(fisdf_ctx* c, const void* Xv, const cplx* Ws_rows, long ws_Rstride,
+                       const void* dmsv, int nset, int nip, int nao, const int kmesh[3],
+                       const double a[9], int i0, int i1, void* vkv) {
   StageTimer tm(c, FISDF_ST_K);
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
   const cplx* phase;
   FISDF_TRY(get_phase(c, kmesh, a, &phase));
   const cplx* X = (const cplx*)Xv;
-  const cplx* Ws = (const cplx*)Wsv;
   const cplx* dms = (const cplx*)dmsv;
   cplx* vk = (cplx*)vkv;
   const int nb = i1 - i0;
@@ -2072,16 +2172,16 @@ int fisdf_get_k_rows(fisdf_ctx* c, const void* Xv, const void* Wsv, const void* 
       // Gamma only (Phi = 1): rho_s = Re(rho_k) (:215-216) and V = W_s * rho_s^T (:219) in this
       // GEMM's epilogue; V_k = V_s (:222)
       FISDF_TRY(zgemm(c->stream, OP_N, OP_T, nb, nip, nao, ONE, T, nao, ba, X, nao, xs, ZERO, B1,
-                      nip, bn, 1, 1, (cplx*)(Ws + (long)i0 * nip), EPI_WSRHO, c->maximag + 2,
-                      GEMM_FULL, (long)nip));
+                      nip, bn, 1, 1, (cplx*)Ws_rows, EPI_WSRHO, c->maximag + 2, GEMM_FULL,
+                      (long)nip));
     } else {
       FISDF_TRY(zgemm(c->stream, OP_N, OP_T, nb, nip, nao, ONE, T, nao, ba, X, nao, xs, ZERO, B1,
                       nip, bn, nk));
       // rho_s = Phi rho_k (:215), real (:216), and V_s = W_s * rho_s^T (:219) for the block
       // rows, both in the GEMM's epilogue (EPI_WSRHO: Re(W_s) Re(.), max |Im rho_s| recorded)
       FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, bn, nk, ONE, phase, nk, 0, B1, bn, 0, ZERO, B2,
-                      bn, 0, 1, 1, (cplx*)(Ws + (long)i0 * nip), EPI_WSRHO, c->maximag + 2,
-                      GEMM_FULL, (long)nip * nip));
+                      bn, 0, 1, 1, (cplx*)Ws_rows, EPI_WSRHO, c->maximag + 2, GEMM_FULL,
+                      ws_Rstride));
       // V_k = Phi^T V_s (:222)
       FISDF_TRY(zgemm(c->stream, OP_T, OP_N, nk, bn, nk, ONE, phase, nk, 0, B2, bn, 0, ZERO, B1,
                       bn, 0, 1));

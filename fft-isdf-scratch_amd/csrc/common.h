@@ -1,6 +1,7 @@
 // fisdf — MI355X-native FFT-ISDF kernels: shared device/host helpers.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -38,6 +39,16 @@ void set_error(const std::string& msg);
     int _r = (call);           \
     if (_r != 0) return _r;    \
   } while (0)
+
+// ---- kernel-exact stage timing: when set, the next zgemm()/herk() call launches its first
+// kernel with `start` and its last kernel with `stop` through hipExtLaunchKernelGGL, so the two
+// events carry that call's kernel begin / end timestamps (the dispatch packet's, as rocprofv3's
+// kernel trace sees them) instead of the stream positions around it; the call clears both.
+// Host-thread local (one context per thread).
+struct LaunchEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchEvents& launch_events();
 
 // ---- complex helpers (device + host)
 __host__ __device__ inline cplx cmk(double r, double i) { cplx c; c.x = r; c.y = i; return c; }

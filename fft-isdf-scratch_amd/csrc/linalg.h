@@ -15,10 +15,13 @@ int gather_lp(hipStream_t s, const cplx* L, int n, int rmax, const int* piv, con
 int trinv_blocks(hipStream_t s, const cplx* Lp, int r, int ldl, long sL, int nb, long sLi,
                  cplx* Linv, int batch);
 int build_trsm_q(hipStream_t s, const cplx* Lp, int r, long sL, cplx* Q, int batch, int mode);
-int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol, int mode);
 int trsm_merged_batched(hipStream_t s, const cplx* Q, long sQ, int r, cplx* X, long ld, long sX,
                         int ncol, int batch, bool lower_rhs = false, cplx* work = nullptr,
                         long work_elems = 0);
+// split-K of one block row of trsm_merged_batched (from its shape only) and the workspace
+// (complex elements) that lets a batch of `batch` r x r matrices run in one launch per row
+int trsm_split_k(int nc, int b1);
+long trsm_split_work_elems(int r, int batch);
 int set_identity(hipStream_t s, cplx* X, int n, int batch);
 int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, long ldl, long sL, int r,
                  const cplx* Linv, long sLi, int nb, cplx* B, long ldb, long sB, cplx* X, long ldx,
@@ -77,8 +80,8 @@ int kmesh_half_count(const int kmesh[3]);
 // Fused y build (time reversal, register k-meshes): fx_k = X_k f_k^H on MFMA for the
 // representative k, staged per 16 x 16 (I, g) tile in LDS, then the kmesh_y DFTs — no fx in
 // HBM.  X (nk, nip, nao); F = f + g0*nao with k stride fks (g rows of nao); writes
-// yT[slot][I][goff + g] for g < m.  *handled = false (nothing enqueued) for other k-meshes,
-// nk > 64, or FISDF_Y_FUSED=0.
+// yT[slot][I][goff + g] for g < m.  *handled = false (nothing enqueued) for other k-meshes
+// or nk > 64 (the two-kernel path then runs).
 // workspace bytes of y_fused for this shape (0: the fused kernel does not apply)
 size_t y_fused_workspace(const int kmesh[3], int nip, int nao, int m);
 int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long fks, int m,

@@ -64,7 +64,7 @@ __global__ __launch_bounds__(64) void trinv_blocks_kernel(const cplx* __restrict
 }
 
 // Same inverses for the partition [0, s0), [s0, s0+64), ... written straight into the
-// diagonal blocks of Q (ld = ldq) — the block-row operator of trsm_merged.  Register-blocked
+// diagonal blocks of Q (ld = ldq) — the block-row operator of trsm_merged_batched.  Register-blocked
 // like chol_diag_kernel's inverse phase: 256 threads, thread t owns the 4 x 4 block (rows
 // 4 (t >> 4), cols 4 (t & 15)) of X = L_bb^{-1}, built by right-looking forward substitution
 // on the identity (row k final once rows < k are subtracted, then scaled by 1 / L_kk) with one
@@ -845,7 +845,7 @@ int gather_lp(hipStream_t s, const cplx* L, int n, int rmax, const int* piv, con
 // Q (r x r, ld = r per batch entry): block rows of the merged forward substitution,
 //   Q[b, b] = L_bb^{-1},  Q[b, :b0] = -L_bb^{-1} L[b, :b0]
 // over the partition [0, s0), [s0, s0+64), ..., s0 = r - 64 (nblk - 1) (the partial block
-// first, so every large-K step of trsm_merged has a full 64-row tile).
+// first, so every large-K step of trsm_merged_batched has a full 64-row tile).
 int build_trsm_q(hipStream_t s, const cplx* Lp, int r, long sL, cplx* Q, int batch, int mode) {
   const int nblk = (r + 63) / 64;
   if (nblk == 0 || batch == 0) return 0;
@@ -864,29 +864,38 @@ int build_trsm_q(hipStream_t s, const cplx* Lp, int r, long sL, cplx* Q, int bat
   return 0;
 }
 
-// X = L^{-1} X in place for X (r x ncol, ld): one GEMM per block row with the Q of
-// build_trsm_q, X[b] = Q[b, :b1] X[:b1] — each workgroup owns whole columns (M <= 64), so
-// it reads all of X[:b1] for its columns before its epilogue overwrites X[b].
-int trsm_merged(hipStream_t s, const cplx* Q, int r, cplx* X, long ld, int ncol, int mode) {
-  const int nblk = (r + 63) / 64;
-  if (nblk == 0) return 0;
-  const int s0 = r - 64 * (nblk - 1);
-  const cplx one = cmk(1, 0), zero = cmk(0, 0);
-  for (int b = 0; b < nblk; ++b) {
-    const int b0 = b == 0 ? 0 : s0 + (b - 1) * 64;
-    const int m = std::min(b == 0 ? s0 : 64, r - b0), b1 = b0 + m;
-    FISDF_TRY(zgemm(s, OP_N, OP_N, m, ncol, b1, one, Q + (long)b0 * r, r, 0, X, ld, 0, zero,
-                    X + (long)b0 * ld, ld, 0, 1, 1, nullptr, EPI_NONE, nullptr, mode));
-  }
-  return 0;
-}
-
-// trsm_merged over a batch (Q and X with batch strides sQ, sX): one launch per block row.
+// X = L^{-1} X in place for a batch of X (r x ncol, ld; batch strides sQ, sX): one GEMM launch
+// per block row with the Q of build_trsm_q, X[b] = Q[b, :b1] X[:b1] — each workgroup owns whole
+// columns (M <= 64), so it reads all of X[:b1] for its columns before its epilogue overwrites
+// X[b].
 // lower_rhs: X is lower-triangular (the identity, for L^{-1}), so block row b only has
 // columns < b1 to compute (the rest stay zero)
-// work (work_elems cplx, may be null): split-K partials for block rows whose grid would leave
-// most CUs idle (a small batch: each 64 x 64 tile otherwise runs its whole K = b1 alone); the
-// partials are reduced by a later kernel, so the in-place update stays safe
+// work (work_elems cplx, may be null): split-K partials for long block rows (each 64 x 64 tile
+// otherwise runs its whole K = b1 alone, which leaves most CUs idle for a small batch); the
+// partials are reduced by a later kernel, so the in-place update stays safe.  The split of a
+// block row depends on that row's shape only (trsm_split_k), never on the batch size, so a
+// matrix gets the same summation order whichever other matrices share its batch (the 1-GPU and
+// the k-sharded builds factor different batches and must agree bitwise); a batch whose partials
+// exceed the workspace is processed in sub-batches.
+int trsm_split_k(int nc, int b1) {
+  if (b1 < 256) return 1;
+  const int tiles = (nc + 63) / 64;
+  return std::max(1, std::min({256 / std::max(tiles, 1), b1 / 128, 16}));
+}
+
+long trsm_split_work_elems(int r, int batch) {
+  long mx = 0;
+  const int nblk = (r + 63) / 64, s0 = r - 64 * (nblk - 1);
+  for (int b = 0; b < nblk; ++b) {
+    const int b0 = b == 0 ? 0 : s0 + (b - 1) * 64, m = std::min(b == 0 ? s0 : 64, r - b0);
+    for (int nc : {r, b0 + m}) {  // a full right-hand side, or the lower-triangular identity
+      const int ks = trsm_split_k(nc, b0 + m);
+      if (ks > 1) mx = std::max(mx, (long)ks * m * nc);
+    }
+  }
+  return mx * batch;
+}
+
 int trsm_merged_batched(hipStream_t s, const cplx* Q, long sQ, int r, cplx* X, long ld, long sX,
                         int ncol, int batch, bool lower_rhs, cplx* work, long work_elems) {
   const int nblk = (r + 63) / 64;
@@ -897,14 +906,16 @@ int trsm_merged_batched(hipStream_t s, const cplx* Q, long sQ, int r, cplx* X, l
     const int b0 = b == 0 ? 0 : s0 + (b - 1) * 64;
     const int m = std::min(b == 0 ? s0 : 64, r - b0), b1 = b0 + m;
     const int nc = lower_rhs ? std::min(ncol, b1) : ncol;
-    const long tiles = (long)((nc + 63) / 64) * batch;
-    int ks = 1;
-    if (work && tiles < 128 && b1 >= 256) {
-      ks = (int)std::min<long>({256 / tiles, b1 / 128, 16});
-      while (ks > 1 && (long)ks * batch * m * nc > work_elems) --ks;
+    const int ks = work ? trsm_split_k(nc, b1) : 1;
+    const long per = (long)ks * m * nc;  // partials of one matrix
+    const int sub = ks > 1 ? (int)std::max(1L, std::min<long>(batch, work_elems / per)) : batch;
+    FISDF_CHECK(ks == 1 || per <= work_elems, "trsm_merged_batched: split-K workspace too small");
+    for (int z0 = 0; z0 < batch; z0 += sub) {
+      const int nb = std::min(sub, batch - z0);
+      FISDF_TRY(zgemm(s, OP_N, OP_N, m, nc, b1, one, Q + z0 * sQ + (long)b0 * r, r, sQ,
+                      X + z0 * sX, ld, sX, zero, X + z0 * sX + (long)b0 * ld, ld, sX, nb, ks,
+                      ks > 1 ? work : nullptr));
     }
-    FISDF_TRY(zgemm(s, OP_N, OP_N, m, nc, b1, one, Q + (long)b0 * r, r, sQ, X, ld, sX, zero,
-                    X + (long)b0 * ld, ld, sX, batch, std::max(ks, 1), ks > 1 ? work : nullptr));
   }
   return 0;
 }
@@ -1449,17 +1460,9 @@ int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const 
   return 0;
 }
 
-bool y_fused_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("FISDF_Y_FUSED");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 size_t y_fused_workspace(const int kmesh[3], int nip, int nao, int m) {
   const int n0 = kmesh[0], P = kmesh[1] * kmesh[2];
-  if (!y_fused_enabled() || n0 * P > 64 || n0 > 4 || P > 16 || m <= 0 || nip <= 0 || nao > 128)
+  if (n0 * P > 64 || n0 > 4 || P > 16 || m <= 0 || nip <= 0 || nao > 128)
     return 0;
   const int nr = (n0 % 2 == 0 && n0 > 1) ? 2 : 1;
   int nslot = n0 >= 3 ? P : 0;  // chunk A + chunk B (in-plane representatives), upper bound
@@ -1474,7 +1477,7 @@ int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long 
   *handled = false;
   const int n0 = kmesh[0], n1 = kmesh[1], n2 = kmesh[2];
   const int nk = n0 * n1 * n2, P = n1 * n2;
-  if (!y_fused_enabled() || nk > 64 || n0 > 4 || P > 16 || m <= 0 || nip <= 0) return 0;
+  if (nk > 64 || n0 > 4 || P > 16 || m <= 0 || nip <= 0) return 0;
   for (int i = 0; i < nq; ++i)
     FISDF_CHECK(h_qs[i] >= 0 && h_qs[i] < nk && (i == 0 || h_qs[i] > h_qs[i - 1]),
                 "y_fused: q-list must be ascending and inside the k-mesh");
@@ -1515,7 +1518,7 @@ int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long 
                      nao, plan, FT);
   FISDF_HIP(hipGetLastError());
   const int nIt = (nip + 15) / 16, nGt = (m + 15) / 16;
-  static const int gpair = std::max(1, getenv("FISDF_YF_GPAIR") ? atoi(getenv("FISDF_YF_GPAIR")) : 4);
+  constexpr int gpair = 4;  // g-tiles per group of the XCD walk (2 / 8 measured no better)
   const long grid = (long)nIt * ((nGt + 8 * gpair - 1) / (8 * gpair)) * gpair * 8;
   FISDF_CHECK(grid < (1L << 31), "y_fused: grid too large");
   static const int mode = getenv("FISDF_YF_MODE") ? atoi(getenv("FISDF_YF_MODE")) : 0;

@@ -952,25 +952,19 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
       return 0;
     return v;
   }();
-  static const int wgs_env = [] {
-    const char* e = getenv("FISDF_SEL_WGS");
-    return e ? atoi(e) : 0;
-  }();
-  // read per call (tests switch them): FISDF_SEL_HYBRID=0 disables the LDS + global split,
-  // FISDF_SEL_LDS_COLS=k forces it with at most k LDS columns
-  const char* eh = getenv("FISDF_SEL_HYBRID");
-  const bool hybrid = !(eh && eh[0] == '0');
+  // read per call (the GPU tests force the split path on small cases): FISDF_SEL_LDS_COLS=k
+  // keeps at most k columns of the owned L rows in LDS
   const char* ek = getenv("FISDF_SEL_LDS_COLS");
   const int kcap = ek ? atoi(ek) : 0;
   constexpr size_t kLds = 150 * 1024;
-  int G = wgs_env > 0 ? wgs_env : 128;
-  G = std::min({G, ncu, (n + 7) / 8});
+  // 128 workgroups: the per-pivot time is flat from 128 to 256 (cross-XCD round trips)
+  int G = std::min({128, ncu, (n + 7) / 8});
   if (G < 1) return 0;
   int RW = (n + G - 1) / G;
   G = (n + RW - 1) / RW;
   int K = rmax, tpr = 8;
   size_t lds = sizeof(double) * ((size_t)RW * rmax + rmax + 2 * (size_t)RW);
-  if ((lds > kLds || kcap > 0) && hybrid && wgs_env <= 0) {
+  if (lds > kLds || kcap > 0) {
     // the owned L rows do not fit: one workgroup per CU, the first K columns in LDS and the
     // rest read back (agent-coherent) from the global L; 16 threads per row when RW <= 16
     G = std::min(ncu, (n + 7) / 8);
@@ -1002,17 +996,13 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
                   (void*)&K,   (void*)&tpr,   (void*)&piv, (void*)&rank, (void*)&rec, (void*)&Lg,   (void*)&err};
   const hipError_t e = hipLaunchCooperativeKernel((const void*)pchol_select_coop, dim3(G),
                                                   dim3(SC_THREADS), args, (unsigned)lds, s);
-  static const bool dbg = getenv("FISDF_SEL_DEBUG") != nullptr;
-  if (e != hipSuccess) {
-    if (dbg) fprintf(stderr, "[fisdf] cooperative selection refused: %s (G=%d RW=%d lds=%zu)\n",
-                     hipGetErrorString(e), G, RW, lds);
+  if (e != hipSuccess) {  // refused (e.g. not co-resident): the caller's blocked path runs
     (void)hipGetLastError();
     return 0;
   }
   int h_err = 0;
   FISDF_HIP(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, s));
   FISDF_HIP(hipStreamSynchronize(s));
-  if (dbg) fprintf(stderr, "[fisdf] cooperative selection G=%d RW=%d K=%d tpr=%d lds=%zu err=%d\n", G, RW, K, tpr, lds, h_err);
   *handled = h_err == 0;
   return 0;
 }

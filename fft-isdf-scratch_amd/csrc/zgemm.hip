@@ -5,54 +5,35 @@
 // HERK that W_q = zeta_q z_q^H (fftisdf.py:121) becomes after the Parseval rewrite.
 //
 // Tile: 64x64 complex per 256-thread workgroup (4 waves, each 32x32 = 2x2 MFMA blocks of
-// 16x16).  K advances BK complex per step through a DOUBLE-BUFFERED LDS ring (one barrier
-// per step): the registers loaded during step k are written to the other buffer at the
-// top of step k+1, the loads of step k+2 are issued, then the MFMAs of step k+1 run.
-// LDS holds interleaved complex (16 B), so each MFMA operand pair (re, im) is one
-// ds_read_b128.  Layout per operand follows its global order so stores stay coalesced
-// and conflict-free:
+// 16x16).  K advances BK complex per step; the operand tiles go global -> LDS by LDS-DMA
+// through an NS-deep ring (zgemm_glds_kernel below).  LDS holds interleaved complex (16 B), so
+// each MFMA operand pair (re, im) is one ds_read_b128.  Layout per operand:
 //   * M/N-contiguous operand: LDS [k][m] plain (64 complex rows = 256 dwords: the
 //     ds_read_b128 lane groups hit disjoint banks);
-//   * K-contiguous operand:   LDS [m][k ^ (m & 15)] (XOR swizzle on the 16-complex row:
-//     fragment reads and 8-lane row stores both conflict-free).
-// Complex product = 4 real MFMAs per 16x16x4 block, issued term-major so an accumulator
-// is reused only every 4th MFMA:   Cr += Ar Br - Ai Bi ;  Ci += Ar Bi + Ai Br.
+//   * K-contiguous operand:   LDS [m][k ^ (m & 15)] (XOR swizzle on the 16-complex row).
 // f64 MFMA fragment maps (cdna_hip_programming.md §3):
 //   A: lane l holds A[i=l&15][k=l>>4];  B: B[k=l>>4][j=l&15];
 //   C/D: 4 f64 per lane, col = l&15, row = (l>>4) + 4*r.
+//
+// HERK=true: C = alpha A A^H (OPA = N, OPB = C, B == A, M == N); only lower-triangle tiles
+// (ti >= tj) are launched and the epilogue mirrors the conjugate into the upper triangle —
+// half the MFMA work of the GEMM.
+//
+// XCD-aware tile order.  The grid is 1-D, padded to a multiple of 8: workgroup b runs on
+// XCD b % 8 (the dispatcher's round-robin; used for speed only, never for correctness) and
+// XCD x owns the contiguous chunk [x*per, (x+1)*per) of the tile order (z-slice major, then
+// M-tile fastest).  The workgroups resident on one XCD at a time are therefore neighbours
+// in that order: the M-tiles of one N-panel (GEMM), or all tiles of one K-split (HERK),
+// which read the same operand panels — served by that XCD's own 4 MB L2 instead of
+// each XCD re-fetching them from HBM / Infinity Cache.
 #include "common.h"
 
 namespace fisdf {
 
 namespace {
 
-#ifndef FISDF_BK
-#define FISDF_BK 8  // A/B on MI355X (C3 bench): BK=8 (32 KB LDS, 3 WGs/CU) 333 ms vs BK=16 348 ms
-#endif
-constexpr int BM = 64, BN = 64, BK = FISDF_BK;
+constexpr int BM = 64, BN = 64, BK = 8;  // BK = 8: 16 KB per ring slot (BK = 16 measured slower)
 constexpr int TILE = 64 * BK;   // complex elements per operand tile
-constexpr int LPT = TILE / 256;  // loads per thread per operand per step
-
-// element (r, c) of op(P) where op(P) is R x Ccols.  Branch-free: the load is issued
-// unconditionally (out-of-range lanes read element 0) and the in-range bit is returned; the
-// zero-masking and conjugation happen at LDS-store time one step later, so the loads of a
-// step stay in flight across the MFMAs instead of being drained right after issue
-// (cdna_hip_programming.md §5, trap (c)).
-template <int OP>
-__device__ __forceinline__ cplx load_raw(const cplx* __restrict__ P, long ld, int r, int c, int R,
-                                         int Ccols, bool& ok) {
-  ok = (r < R) & (c < Ccols);
-  long off = (OP & 1) ? (long)c * ld + r : (long)r * ld + c;
-  return P[ok ? off : 0];
-}
-
-template <int OP>
-__device__ __forceinline__ cplx finish(cplx v, bool ok) {
-  cplx o;
-  o.x = ok ? v.x : 0.0;
-  o.y = ok ? ((OP & 2) ? -v.y : v.y) : 0.0;
-  return o;
-}
 
 // Operand staging. ROW_IS_K: the tile's "outer" index is the M (or N) index and k is
 // contiguous in global memory (A op N/conj, B op T/conj-T).
@@ -180,154 +161,8 @@ __device__ __forceinline__ void zgemm_epilogue(int M, int N, cplx alpha, cplx be
       }
 }
 
-// HERK=true: C = alpha A A^H (OPA = N, OPB = C, B == A, M == N); only lower-triangle tiles
-// (ti >= tj) are launched and the epilogue mirrors the conjugate into the upper triangle —
-// half the MFMA work of the GEMM.
-//
-// XCD-aware tile order.  The grid is 1-D, padded to a multiple of 8: workgroup b runs on
-// XCD b % 8 (the dispatcher's round-robin; used for speed only, never for correctness) and
-// XCD x owns the contiguous chunk [x*per, (x+1)*per) of the tile order (z-slice major, then
-// M-tile fastest).  The workgroups resident on one XCD at a time are therefore neighbours
-// in that order: the M-tiles of one N-panel (GEMM), or all tiles of one K-split (HERK),
-// which read the same operand panels — served by that XCD's own 4 MB L2 instead of
-// each XCD re-fetching them from HBM / Infinity Cache.
-template <int OPA, int OPB, bool HERK>
-__global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx alpha,
-                                                    const cplx* __restrict__ A, long lda, long sA,
-                                                    const cplx* __restrict__ B, long ldb, long sB,
-                                                    cplx beta, cplx* __restrict__ C, long ldc, long sC,
-                                                    int ksplit, int kchunk, cplx* __restrict__ work,
-                                                    int epi, unsigned long long* __restrict__ mon, long ldaux,
-                                                    int nMt, int ntile, int ntot) {
-  constexpr bool AK = !(OPA & 1);  // A stored [m][k]
-  constexpr bool BKc = (OPB & 1);  // B stored [n][k]
-  typedef Stage<AK> SA;
-  typedef Stage<BKc> SB;
-  __shared__ cplx As[2][TILE];
-  __shared__ cplx Bs[2][TILE];
-
-  const int per = (int)(gridDim.x >> 3);
-  const int order = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-  if (order >= ntot) return;  // padding of the 1-D grid (uniform per workgroup)
-  const int zz = order / ntile, t = order - zz * ntile;
-  const int split = zz % ksplit;
-  const int bz = zz / ksplit;
-  A += (long)bz * sA;
-  B += (long)bz * sB;
-  int ti = t % nMt, tj = t / nMt;
-  if (HERK) {  // t = ti*(ti+1)/2 + tj, tj <= ti
-    ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-    while (ti * (ti + 1) / 2 > t) --ti;
-    tj = t - ti * (ti + 1) / 2;
-  }
-  const int m0 = ti * BM, n0 = tj * BN;
-  const int kbeg = split * kchunk;
-  const int kend = min(K, kbeg + kchunk);
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
-
-  f64x4 accR[2][2], accI[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      accR[i][j] = f64x4{0, 0, 0, 0};
-      accI[i][j] = f64x4{0, 0, 0, 0};
-    }
-
-  cplx ra[LPT], rb[LPT];
-  bool oka[LPT], okb[LPT];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < LPT; ++j) {
-      int x, k;
-      SA::coord(tid + 256 * j, x, k);
-      const int gk = k0 + k;
-      ra[j] = load_raw<OPA>(A, lda, m0 + x, gk, M, gk < kend ? K : 0, oka[j]);
-      SB::coord(tid + 256 * j, x, k);
-      const int gk2 = k0 + k;
-      rb[j] = load_raw<OPB>(B, ldb, gk2, n0 + x, gk2 < kend ? K : 0, N, okb[j]);
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < LPT; ++j) {
-      int x, k;
-      SA::coord(tid + 256 * j, x, k);
-      As[buf][SA::slot(x, k)] = finish<OPA>(ra[j], oka[j]);
-      SB::coord(tid + 256 * j, x, k);
-      Bs[buf][SB::slot(x, k)] = finish<OPB>(rb[j], okb[j]);
-    }
-  };
-
-  // Branch-free ring: every step stores the prefetched tile into the idle buffer and issues
-  // the loads two steps ahead (past kend they are masked to zero and never consumed).
-  const int nsteps = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  if (nsteps > 0) {
-    gload(kbeg);
-    lstore(0);
-    gload(kbeg + BK);
-  }
-  const int i16 = lane & 15, kq = lane >> 4;
-  for (int s = 0; s < nsteps; ++s) {
-    const int cur = s & 1;
-    __syncthreads();  // buffer `cur` complete; buffer `cur^1` no longer read
-    lstore(cur ^ 1);
-    gload(kbeg + (s + 2) * BK);
-    const cplx* as = As[cur];
-    const cplx* bs = Bs[cur];
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 4) {
-      const int k = kk + kq;
-      cplx a[2], b[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        a[t] = as[SA::slot(wm + t * 16 + i16, k)];
-        b[t] = bs[SB::slot(wn + t * 16 + i16, k)];
-      }
-      const double nai0 = -a[0].y, nai1 = -a[1].y;
-      const double nai[2] = {nai0, nai1};
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-          accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].x, b[ni].x, accR[mi][ni], 0, 0, 0);
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-          accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].x, b[ni].y, accI[mi][ni], 0, 0, 0);
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-          accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[mi], b[ni].y, accR[mi][ni], 0, 0, 0);
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-          accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].y, b[ni].x, accI[mi][ni], 0, 0, 0);
-    }
-  }
-
-  // every block was computed; strictly-upper HERK blocks are written as mirrors instead
-  int mask = 0;
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      const int r0 = m0 + wm + mi * 16, c0 = n0 + wn + ni * 16;
-      mask |= (r0 < M && c0 < N && !(HERK && c0 > r0) ? 1 : 0) << (mi * 2 + ni);
-    }
-  zgemm_epilogue<HERK>(M, N, alpha, beta, C, ldc, sC, ksplit, split, bz, work, epi, mon, ldaux, m0, n0, wm,
-                       wn, lane, mask, accR, accI);
-}
-
-// ---- LDS-DMA variant -------------------------------------------------------------------
-// Same tile, tile order, masks and epilogue as zgemm_kernel, but the operand tiles go
-// global -> LDS directly (global_load_lds_dwordx4, no staging registers) through a THREE-deep
+// ---- the GEMM kernel -------------------------------------------------------------------
+// The operand tiles go global -> LDS directly (global_load_lds_dwordx4, no staging registers) through a THREE-deep
 // LDS ring: the loads of K-step s+2 are issued at step s, so each has two full steps to land
 // (the register-staged kernel waited on its loads one step after issue: at 3 workgroups/CU
 // its per-step time was set by L2/HBM latency, not by the MFMA pipe).  The LDS image is
@@ -339,9 +174,6 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int N, int K, cplx al
 #endif
 #ifndef FISDF_NST
 #define FISDF_NST 3
-#endif
-#ifndef FISDF_PREREAD
-#define FISDF_PREREAD 0
 #endif
 constexpr int NST = FISDF_NST;  // LDS ring depth; loads run NST-1 K-steps ahead
 constexpr int LPW = TILE / (64 * 4);  // glds wave-instructions per operand per step per wave
@@ -444,9 +276,6 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
                  : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
   };
   auto issue = [&](int st) {  // K-step st -> ring slot st % NS
-#ifdef FISDF_NOLOAD
-    if (st >= NS - 1) return;  // experiment: MFMA/LDS ceiling without global traffic
-#endif
     const int buf = st % NS;
     const int k0 = kbeg + st * BK;
     const unsigned la = lds0 + (unsigned)((buf * 2 + 0) * TILE) * 16u;
@@ -502,37 +331,17 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
       const cplx* as = sm + (long)(cur * 2 + 0) * TILE;
       const cplx* bs = sm + (long)(cur * 2 + 1) * TILE;
       const int kleft = kend - kbeg - s * BK;  // K-substeps past the end hold only zeros
-#if FISDF_PREREAD
-      // every K-substep's fragments are read from the ring slot before the next step's loads
-      // are issued, so their LDS latency overlaps the glds issue and the first MFMAs
-      cplx fa[BK / 4][2], fb[BK / 4][2];
-#pragma unroll
-      for (int kk = 0; kk < BK; kk += 4)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          fa[kk / 4][u] = as[SA::slot((wm + u * 16 + i16) & 63, kk + kq)];
-          fb[kk / 4][u] = bs[SB::slot((wn + u * 16 + i16) & 63, kk + kq)];
-        }
-#endif
       issue(s + NS - 1);
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 4) {
         if (kk > 0 && kk >= kleft) break;
         cplx a[2], b[2];
-#if FISDF_PREREAD
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          a[u] = fa[kk / 4][u];
-          b[u] = fb[kk / 4][u];
-        }
-#else
         const int k = kk + kq;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {  // & 63: a masked block past the tile reads in-tile rows
           a[u] = as[SA::slot((wm + u * 16 + i16) & 63, k)];
           b[u] = bs[SB::slot((wn + u * 16 + i16) & 63, k)];
         }
-#endif
         // op(A) = a (or conj a), op(B) = b (or conj b):
         //   Re += ar br - ai' bi' ;  Im += ar bi' + ai' br   (ai' = +-ai, bi' = +-bi)
         double ar[2], ai[2], nai[2], br[2], bi[2];
@@ -680,19 +489,23 @@ __global__ __launch_bounds__(256) void herk_reduce_kernel(int n, int ksplit,
   }
 }
 
-// 0 = register-staged kernel, 1 = LDS-DMA kernel (default; FISDF_GEMM=reg selects 0)
-int gemm_variant() {
-  static int v = [] {
-    const char* e = getenv("FISDF_GEMM");
-    return (e && std::string(e) == "reg") ? 0 : 1;
-  }();
-  return v;
-}
+// the kernel-exact timing events of the current zgemm()/herk() call (taken from launch_events()
+// at its entry): the main kernel records `start`, the call's last kernel `stop`
+struct CallEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+  CallEvents() {
+    LaunchEvents& le = launch_events();
+    start = le.start;
+    stop = le.stop;
+    le = LaunchEvents();
+  }
+};
 
 template <int OPA, int OPB, bool HERK = false, int MODE = GEMM_FULL>
 void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cplx* A, long lda,
             long sA, const cplx* B, long ldb, long sB, cplx beta, cplx* C, long ldc, long sC,
-            int ksplit, int kchunk, cplx* work, int epi, unsigned long long* mon, long ldaux) {
+            int ksplit, int kchunk, cplx* work, int epi, unsigned long long* mon, long ldaux,
+            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
   // grid = (N-tiles or triangle tiles, M-tiles, z-slices) -> padded 1-D XCD-aware order
   const int nMt = HERK ? 1 : (int)grid.y;
   const int ntile = (int)(grid.x * (HERK ? 1 : grid.y));
@@ -700,18 +513,27 @@ void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cpl
   const long per = (ntot + 7) / 8;
   // short K loops (<= 4 steps per workgroup, e.g. the y build's K = nao): a 2-deep ring
   // (32 KB of LDS) lets more workgroups share a CU, overlapping their load and store phases
-  if ((gemm_variant() == 1 || MODE != GEMM_FULL) && kchunk <= 4 * BK)
-    hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, 2>), dim3((unsigned)(8 * per)),
-                       dim3(256), 0, s, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
-                       ksplit, kchunk, work, epi, mon, ldaux, nMt, ntile, (int)ntot);
-  else if (gemm_variant() == 1 || MODE != GEMM_FULL)
-    hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, NST>), dim3((unsigned)(8 * per)), dim3(256), 0,
-                       s, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk,
-                       work, epi, mon, ldaux, nMt, ntile, (int)ntot);
-  else
-    hipLaunchKernelGGL((zgemm_kernel<OPA, OPB, HERK>), dim3((unsigned)(8 * per)), dim3(256), 0, s, M,
-                       N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work,
-                       epi, mon, ldaux, nMt, ntile, (int)ntot);
+  const dim3 g((unsigned)(8 * per));
+  // the extension launch only when timing asks for the kernel's own timestamps
+  if (kchunk <= 4 * BK) {
+    if (ev0 || ev1)
+      hipExtLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, 2>), g, dim3(256), 0, s, ev0,
+                            ev1, 0, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
+                            ksplit, kchunk, work, epi, mon, ldaux, nMt, ntile, (int)ntot);
+    else
+      hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, 2>), g, dim3(256), 0, s, M, N, K,
+                         alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work,
+                         epi, mon, ldaux, nMt, ntile, (int)ntot);
+  } else {
+    if (ev0 || ev1)
+      hipExtLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, NST>), g, dim3(256), 0, s,
+                            ev0, ev1, 0, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
+                            ksplit, kchunk, work, epi, mon, ldaux, nMt, ntile, (int)ntot);
+    else
+      hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, NST>), g, dim3(256), 0, s, M, N,
+                         K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work,
+                         epi, mon, ldaux, nMt, ntile, (int)ntot);
+  }
 }
 
 }  // namespace
@@ -741,15 +563,17 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
   FISDF_CHECK((long)((N + BN - 1) / BN) * ((M + BM - 1) / BM) * batch * ksplit < (1L << 31),
               "zgemm: too many tiles");
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch * ksplit);
+  const CallEvents ev;
+  hipEvent_t ev_last = ksplit > 1 ? nullptr : ev.stop;  // the reduce ends the call when split
 #define FISDF_CASE(a, b)                                                                      \
   case a * 4 + b:                                                                             \
     launch<a, b>(s, grid, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit,   \
-                 kchunk, work, epi, mon, ldaux);                                              \
+                 kchunk, work, epi, mon, ldaux, ev.start, ev_last);                           \
     break;
 #define FISDF_MCASE(a, b, m)                                                                  \
   if (opA == a && opB == b && mode == m) {                                                    \
     launch<a, b, false, m>(s, grid, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, \
-                           ksplit, kchunk, work, epi, mon, ldaux);                            \
+                           ksplit, kchunk, work, epi, mon, ldaux, ev.start, ev_last);         \
   }
   FISDF_MCASE(0, 0, 1) FISDF_MCASE(0, 0, 2) FISDF_MCASE(0, 0, 3)
   FISDF_MCASE(0, 0, 4) FISDF_MCASE(0, 0, 5)
@@ -767,8 +591,12 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
   if (ksplit > 1) {
     long MN = (long)M * N;
     int blocks = (int)std::min<long>((MN + 255) / 256, 4096);
-    hipLaunchKernelGGL(ksplit_reduce, dim3(blocks, batch), dim3(256), 0, s, M, N, ksplit, work,
-                       alpha, beta, C, ldc, sC);
+    if (ev.stop)
+      hipExtLaunchKernelGGL(ksplit_reduce, dim3(blocks, batch), dim3(256), 0, s, nullptr, ev.stop,
+                            0, M, N, ksplit, (const cplx*)work, alpha, beta, C, ldc, sC);
+    else
+      hipLaunchKernelGGL(ksplit_reduce, dim3(blocks, batch), dim3(256), 0, s, M, N, ksplit,
+                         (const cplx*)work, alpha, beta, C, ldc, sC);
     FISDF_HIP(hipGetLastError());
   }
   return 0;
@@ -787,18 +615,24 @@ int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cpl
   ksplit = std::max(1, (K + kchunk - 1) / kchunk);
   const int nt = (n + BM - 1) / BM;
   dim3 grid(nt * (nt + 1) / 2, 1, ksplit);
+  const CallEvents ev;
+  hipEvent_t ev_last = ksplit > 1 ? nullptr : ev.stop;
   if (mode == GEMM_RE_ONLY)  // C = Re(A A^H): 2 of the 4 MFMAs per complex block
     launch<OP_N, OP_C, true, GEMM_RE_ONLY>(s, grid, n, n, K, cmk(alpha, 0), A, lda, 0, A, lda, 0,
                                            cmk(0, 0), C, ldc, 0, ksplit, kchunk, work, EPI_NONE,
-                                           nullptr, 0);
+                                           nullptr, 0, ev.start, ev_last);
   else
     launch<OP_N, OP_C, true>(s, grid, n, n, K, cmk(alpha, 0), A, lda, 0, A, lda, 0, cmk(0, 0), C,
-                             ldc, 0, ksplit, kchunk, work, EPI_NONE, nullptr, 0);
+                             ldc, 0, ksplit, kchunk, work, EPI_NONE, nullptr, 0, ev.start, ev_last);
   FISDF_HIP(hipGetLastError());
   if (ksplit > 1) {
     const int t32 = (n + 31) / 32;
-    hipLaunchKernelGGL(herk_reduce_kernel, dim3(t32 * (t32 + 1) / 2), dim3(256), 0, s, n, ksplit,
-                       work, alpha, C, ldc);
+    if (ev.stop)
+      hipExtLaunchKernelGGL(herk_reduce_kernel, dim3(t32 * (t32 + 1) / 2), dim3(256), 0, s,
+                            nullptr, ev.stop, 0, n, ksplit, (const cplx*)work, alpha, C, ldc);
+    else
+      hipLaunchKernelGGL(herk_reduce_kernel, dim3(t32 * (t32 + 1) / 2), dim3(256), 0, s, n, ksplit,
+                         (const cplx*)work, alpha, C, ldc);
     FISDF_HIP(hipGetLastError());
   }
   return 0;

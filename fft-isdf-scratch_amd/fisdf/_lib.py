@@ -80,6 +80,8 @@ _SIGS = {
     "fisdf_get_k": ([_vp, _vp, _vp, _vp, _i, _i, _i, _ip, _dp, _vp], _i),
     "fisdf_get_j_rows": ([_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp], _i),
     "fisdf_get_k_rows": ([_vp, _vp, _vp, _vp, _i, _i, _i, _ip, _dp, _i, _i, _vp], _i),
+    "fisdf_get_k_rows_local": ([_vp, _vp, _vp, _vp, _i, _i, _i, _ip, _dp, _i, _i, _vp], _i),
+    "fisdf_build_ws_rows": ([_vp, _vp, _ip, _dp, _i, _i, _ip, _dp, _i, _i, _vp], _i),
     "fisdf_get_eri": ([_vp, _vp, _i, _i, _ip, _vp, C.POINTER(_vp), _ip, _vp], _i),
     "fisdf_zgemm": ([_vp, _i, _i, _i, _i, _i, _dp, _vp, _l, _l, _vp, _l, _l, _dp, _vp, _l, _l,
                      _i, _i], _i),
@@ -87,6 +89,8 @@ _SIGS = {
     "fisdf_fft3d": ([_vp, _vp, _vp, _i, _ip], _i),
     "fisdf_coulg": ([_vp, _ip, _dp, _dp, _d, _i, _vp], _i),
     "fisdf_pivoted_cholesky": ([_vp, _vp, _i, _i, _i, _d, _ip, _ip], _i),
+    "fisdf_cholesky": ([_vp, _vp, _i, _i, _d, _ip], _i),
+    "fisdf_tri_inverse": ([_vp, _vp, _i, _i, _vp], _i),
 }
 
 
@@ -105,6 +109,8 @@ def load(path: str = LIB_PATH):
             f"'import __graft_entry__ as g; g.build()')")
     lib = C.CDLL(path)
     for name, (args, res) in _SIGS.items():
+        if os.environ.get("FISDF_LIB_VARIANT") and not hasattr(lib, name):
+            continue  # an A/B build of an older tree may lack newer entry points
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res

@@ -18,7 +18,6 @@ Differences from the reference, all deliberate:
 from __future__ import annotations
 
 import logging
-import os
 import time
 
 import numpy as np
@@ -68,7 +67,9 @@ class _Device:
         self.stream = torch.cuda.current_stream(self.dev)
         self.ctx = _lib.Context(int(device), self.stream.cuda_stream)
         self.comm = comm
-        if comm is not None:
+        if isinstance(comm, kshard.EmulatedGroup):
+            self.rank, self.size = comm.rank, comm.size
+        elif comm is not None:
             import torch.distributed as dist
             self.rank = dist.get_rank(comm)
             self.size = dist.get_world_size(comm)
@@ -78,6 +79,16 @@ class _Device:
     def shard(self, nk):
         """Contiguous q-range of this rank."""
         return kshard.shard_range(nk, self.rank, self.size)
+
+    def sharded(self, df_obj):
+        """Whether this build takes the collective (k-sharded) code path."""
+        if self.size > 1:
+            return True
+        if getattr(df_obj, "force_sharded", False):
+            if self.comm is None:
+                raise ValueError("ISDF.force_sharded needs a torch.distributed group (comm)")
+            return True
+        return False
 
     def empty(self, shape, dtype="c128"):
         t = self.torch
@@ -130,6 +141,10 @@ class InterpolativeSeparableDensityFitting:
     # multi-rank selection: False (default) replicates the 1-GPU Gram + pivots on every rank
     # (rank-count-invariant pivots); True k-shards the Gram and all-reduces it
     sharded_gram = False
+    # run the sharded (collective) code path even in a one-rank group: grid-sliced y, the chunked
+    # all-to-all, the W_s all-reduce and W_0 broadcast, the get_jk all-reduces — how the RCCL path
+    # is exercised on a single GPU (tests/test_gpu_rccl.py); needs ``comm``
+    force_sharded = False
 
     def __init__(self, cell, kpts, m0=None, c0=20.0, device=None, comm=None):
         self.cell = cell
@@ -439,7 +454,7 @@ class InterpolativeSeparableDensityFitting:
         st = self._dev_state
         d = self.device
         nk = int(np.prod(self.kmesh))
-        if d.size == 1:
+        if d.size == 1 or isinstance(d.comm, kshard.EmulatedGroup):
             parts = [(self.my_qs, st["Wq"].cpu().numpy())]
         else:
             import torch.distributed as dist
@@ -516,16 +531,13 @@ def build(df_obj):
         if nq:
             d.ctx.call("fisdf_factor_x4_async", _lib.ptr(x4), qs_c, nq, nip,
                        float(df_obj.fit_tol), km_p if df_obj.real_self_conjugate else None)
-    after_y = os.environ.get("FISDF_FACTOR_AFTER_Y", "1") != "0"
-    if not after_y:
-        factor_async()
-        factor_async = lambda: None          # noqa: E731
     # fx_{-k} = conj(fx_k) for real AOs: fx_k computed for half the k-mesh (:76)
     d.ctx.call("fisdf_set_time_reversal", 1 if df_obj.time_reversal else 0)
     d.ctx.call("fisdf_set_omega", float(getattr(df_obj, "_fit_omega", 0.0)))
     df_obj._omega_dfs = {}                   # range-separated states of an earlier build
     yT = d.empty((nq, nip, ngrid))
-    if d.size == 1:
+    sharded = d.sharded(df_obj)
+    if not sharded:
         d.ctx.call("fisdf_build_y_qs", _lib.ptr(f), ngrid * nao, 0, ngrid, ngrid, _lib.ptr(X),
                    nip, nao, km_p, a_p, qs_c, nq, _lib.ptr(yT))                 # :67-87
         factor_async()
@@ -555,7 +567,7 @@ def build(df_obj):
         d.ctx.call("fisdf_min_norm_info", byref(used))
         df_obj.min_norm_slots = int(used.value)
     Wq = d.empty((nq, nip, nip))
-    if d.size == 1:
+    if not sharded:
         if nq:
             d.ctx.call("fisdf_fit_coulomb_qs", qs_c, nq, _lib.ptr(yT), nip, mesh_p, km_p, a_p,
                        _lib.ptr(Wq))
@@ -576,15 +588,29 @@ def build(df_obj):
         del send, pieces
     del yT
 
-    Ws = d.empty((nk, nip, nip))
-    d.ctx.call("fisdf_build_ws_qs", _lib.ptr(Wq), qs_c, my_wt.ctypes.data_as(_lib._dp), nq, nip,
-               km_p, a_p, _lib.ptr(Ws))                                          # :204-207
-    if d.size > 1:
-        kshard.allreduce_real_part(Ws, d.comm)                           # k-sum of W_s
+    if sharded:
+        # W_s = sqrt(nk) Re(sum_q Phi[R,q] W_q) (:204-207) mixes every rank's q; get_k on rank r
+        # contracts only its interpolation-point rows, so each rank forms every rank's row block of
+        # its partial sum and the blocks are reduce-scattered (W_s rows stay distributed)
+        rows = [kshard.shard_range(nip, r, d.size) for r in range(d.size)]
+        chunk = nk * max(b - a for a, b in rows) * nip
+        Wsb = d.empty((chunk * d.size,))
+        for r, (i0, i1) in enumerate(rows):
+            if i1 > i0:
+                d.ctx.call("fisdf_build_ws_rows", _lib.ptr(Wq), qs_c,
+                           my_wt.ctypes.data_as(_lib._dp), nq, nip, km_p, a_p, i0, i1,
+                           _lib.ptr(Wsb[r * chunk:]))
+        i0, i1 = rows[d.rank]
+        Ws = kshard.reduce_scatter_real(Wsb, chunk, nk * (i1 - i0) * nip, d.rank, d.size,
+                                        d.comm).reshape(nk, i1 - i0, nip)
+        del Wsb
         owner0 = next(r for r, (a, b) in enumerate(chunks) if b > a)     # fit_qs[0] == 0
         W0 = Wq[0].clone() if d.rank == owner0 else d.empty((nip, nip))
         kshard.broadcast_w0(W0, nk, d.comm, src_local=owner0)           # W_0 for get_j
     else:
+        Ws = d.empty((nk, nip, nip))
+        d.ctx.call("fisdf_build_ws_qs", _lib.ptr(Wq), qs_c, my_wt.ctypes.data_as(_lib._dp), nq,
+                   nip, km_p, a_p, _lib.ptr(Ws))                                 # :204-207
         W0 = Wq[0]
     df_obj.fit_qs, df_obj.q_partner = fit_qs, partner
     df_obj.my_qs = my_qs
@@ -665,7 +691,8 @@ def _get_j_dev(df_obj, ddms, band=None):
     nset, nk, nao = ddms.shape[:3]
     nip = st["X"].shape[1]
     # sharded: each rank contracts its block of interpolation points, one all-reduce (:166)
-    i0, i1 = d.shard(nip) if d.size > 1 else (0, nip)
+    sharded = d.sharded(df_obj)
+    i0, i1 = d.shard(nip) if sharded else (0, nip)
     if band is None:
         vj = d.empty(ddms.shape)
         d.ctx.call("fisdf_get_j_rows", _lib.ptr(st["X"]), _lib.ptr(st["W0"]), _lib.ptr(ddms),
@@ -676,7 +703,7 @@ def _get_j_dev(df_obj, ddms, band=None):
         d.ctx.call("fisdf_get_j_band_rows", _lib.ptr(st["X"]), _lib.ptr(st["W0"]),
                    _lib.ptr(ddms), nset, nk, nip, nao, _lib.ptr(Xb), len(band), i0, i1,
                    _lib.ptr(vj))
-    if d.size > 1:  # the library runs on torch's current stream: the all-reduce is ordered
+    if sharded:  # the library runs on torch's current stream: the all-reduce is ordered
         kshard.allreduce_sum(vj, d.comm)
     return vj
 
@@ -719,10 +746,13 @@ def _get_k_dev(df_obj, ddms, exxdiv=None, band=None):
     a_c, a_p = _lib.darr(np.asarray(df_obj.cell.lattice_vectors(), float).ravel())
     vk = d.empty(ddms.shape)
     # sharded: each rank contracts its block of interpolation points, one all-reduce (:225)
-    i0, i1 = d.shard(nip) if d.size > 1 else (0, nip)
-    d.ctx.call("fisdf_get_k_rows", _lib.ptr(st["X"]), _lib.ptr(st["Ws"]), _lib.ptr(ddms), nset,
-               nip, nao, km_p, a_p, i0, i1, _lib.ptr(vk))
-    if d.size > 1:
+    sharded = d.sharded(df_obj)
+    i0, i1 = d.shard(nip) if sharded else (0, nip)
+    # sharded: the rank holds only its W_s rows (reduce-scattered by build)
+    call = "fisdf_get_k_rows_local" if sharded else "fisdf_get_k_rows"
+    d.ctx.call(call, _lib.ptr(st["X"]), _lib.ptr(st["Ws"]), _lib.ptr(ddms), nset, nip, nao, km_p,
+               a_p, i0, i1, _lib.ptr(vk))
+    if sharded:
         kshard.allreduce_sum(vk, d.comm)
     if exxdiv == "ewald":
         _ewald_exxdiv_for_G0(df_obj, ddms, vk)

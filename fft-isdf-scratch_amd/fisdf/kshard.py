@@ -20,6 +20,36 @@ tests and the RCCL path.
 from __future__ import annotations
 
 
+class EmulatedGroup:
+    """Rank `rank` of a `size`-rank k-shard, run ALONE on one GPU (bench.py --emulate-ranks):
+    every compute step of that rank's share of the sharded build runs for real — the replicated
+    selection and x4, the y build on its grid slice for all fitted q, the unpack of its
+    all-to-all pieces, the fit of its q-chunk, its W_s partial and its get_jk rows — while the
+    collectives are replaced by what they leave in this rank's memory: the all-to-all pieces are
+    handed over pre-filled (`pieces[j]`, the rank's j-th q on the whole grid in the concat-of-
+    slices layout; taken from a full 1-GPU y so the fit sees real data), the all-reduces keep
+    their local copies but add nothing, the broadcast is skipped.  Timing only: the results of
+    an emulated rank are its partial sums."""
+
+    def __init__(self, rank: int, size: int, pieces=None):
+        self.rank, self.size = int(rank), int(size)
+        self.pieces = pieces
+
+
+def emulated_pieces(yall, chunks, slices, rank: int):
+    """The all-to-all pieces rank `rank` receives, built from the full y of every fitted q
+    (yall: (nq_all, nip, ngrid) in fit order): its j-th q on each slice p, concatenated in rank
+    order p — exactly the layout exchange_y_chunked hands to the unpack."""
+    import torch
+    a0, a1 = chunks[rank]
+    return [torch.cat([yall[a0 + j, :, g0:g0 + ng].reshape(-1) for g0, ng in slices])
+            for j in range(a1 - a0)]
+
+
+def _emulated(group):
+    return isinstance(group, EmulatedGroup)
+
+
 def shard_range(nk: int, rank: int, size: int):
     """Contiguous, balanced q-range [q0, q1) of `rank` among `size` ranks."""
     base, rem = divmod(nk, size)
@@ -140,28 +170,43 @@ def exchange_y_chunked(send, nip: int, slices, rank: int, size: int, group, coun
     concat_p (nip, ng_p); call work_j.wait() (may be None) before reading recv_j."""
     import torch
     import torch.distributed as dist
+    if _emulated(group):
+        ngrid = sum(ng for _, ng in slices)
+        return [(group.pieces[j] if group.pieces is not None else
+                 send.new_empty(nip * ngrid), None) for j in range(counts[rank])]
     starts = [sum(counts[:r]) for r in range(size)]
     ng_self = slices[rank][1]
     nmax = max(counts) if counts else 0
     out = []
-    host = _host_staged(group, send)
+    # gloo has no list all-to-all: gather the pieces on the host (CPU tests, ranks sharing a GPU)
+    host = dist.get_backend(group) == "gloo"
+    hs = send.cpu() if host else None
     for j in range(nmax):
-        dst = [r for r in range(size) if j < counts[r]]
-        idx = torch.tensor([starts[r] + j for r in dst], dtype=torch.long, device=send.device)
-        sj = send.index_select(0, idx).reshape(-1) if len(dst) else send.new_empty(0)
         in_splits = [nip * ng_self if j < counts[r] else 0 for r in range(size)]
         mine = j < counts[rank]
         out_splits = [nip * slices[p][1] if mine else 0 for p in range(size)]
         rj = torch.empty(sum(out_splits), dtype=send.dtype, device=send.device)
         if host:
+            dst = [r for r in range(size) if j < counts[r]]
+            idx = torch.tensor([starts[r] + j for r in dst], dtype=torch.long)
+            sj = hs.index_select(0, idx).reshape(-1) if len(dst) else hs.new_empty(0)
             hr = rj.cpu()
-            dist.all_to_all_single(torch.view_as_real(hr), torch.view_as_real(sj.cpu()),
+            dist.all_to_all_single(torch.view_as_real(hr), torch.view_as_real(sj),
                                    out_splits, in_splits, group=group)
-            rj.copy_(hr)
+            if rj.data_ptr() != hr.data_ptr():
+                rj.copy_(hr)
             work = None
         else:
-            work = dist.all_to_all_single(torch.view_as_real(rj), torch.view_as_real(sj),
-                                          out_splits, in_splits, group=group, async_op=True)
+            # the piece for rank r is send[starts[r] + j], a contiguous (nip, ng_self) block: the
+            # list form sends every piece from its place (no gather copy of the send buffer)
+            empty = torch.view_as_real(send.new_empty(0))
+            ins = [torch.view_as_real(send[starts[r] + j].reshape(-1)) if j < counts[r] else empty
+                   for r in range(size)]
+            outs, off = [], 0
+            for n in out_splits:
+                outs.append(torch.view_as_real(rj[off:off + n]))
+                off += n
+            work = dist.all_to_all(outs, ins, group=group, async_op=True)
         if mine:
             out.append((rj, work))
         elif work is not None:
@@ -180,6 +225,29 @@ def allreduce_real_part(t, group=None):
     return t
 
 
+def reduce_scatter_real(blocks, chunk: int, nloc: int, rank: int, size: int, group=None):
+    """Sum over ranks of `blocks` (complex, imaginary part zero; rank c's block of the sum at
+    [c*chunk, c*chunk + n_c), chunks padded to one size) and return THIS rank's block, the first
+    `nloc` elements of its chunk, as a complex tensor with zero imaginary part: W_s reduced and
+    scattered by interpolation-point rows (fftisdf.py:204-207; each rank's get_k needs only its
+    rows).  Only the real parts travel: half the bytes of a complex all-reduce, and (size-1)/size
+    of one W_s per rank instead of the all-reduce's 2 (size-1)/size."""
+    import torch
+    import torch.distributed as dist
+    re = torch.view_as_real(blocks)[..., 0].contiguous()
+    if _emulated(group):
+        mine = re[rank * chunk:rank * chunk + nloc]
+    elif _host_staged(group, re):
+        h = re.cpu()
+        dist.all_reduce(h, group=group)
+        mine = h[rank * chunk:rank * chunk + nloc].to(re.device)
+    else:
+        out = torch.empty(chunk, dtype=re.dtype, device=re.device)
+        dist.reduce_scatter_tensor(out, re[:chunk * size], group=group)
+        mine = out[:nloc]
+    return torch.complex(mine, torch.zeros_like(mine))
+
+
 def _host_staged(group, *tensors):
     """gloo moves host tensors only: device tensors are staged through host copies (used
     when several ranks share one GPU in tests; the multi-GPU path uses RCCL directly)."""
@@ -191,6 +259,8 @@ def allreduce_sum(t, group=None):
     """In-place sum over ranks (complex tensors are reduced through their real view)."""
     import torch
     import torch.distributed as dist
+    if _emulated(group):
+        return t
     if _host_staged(group, t):
         h = t.cpu()
         allreduce_sum(h, group)
@@ -200,15 +270,12 @@ def allreduce_sum(t, group=None):
     return t
 
 
-def allreduce_ws(ws, group=None):
-    """Sum the per-rank partial W_s (complex tensor, imaginary part zero) in place."""
-    return allreduce_sum(ws, group)
-
-
 def broadcast_w0(w0, nk: int, group=None, src_local=None):
     """Broadcast W_0 from the rank that owns q = 0 (default: contiguous q-ranges over nk)."""
     import torch
     import torch.distributed as dist
+    if _emulated(group):
+        return w0
     size = dist.get_world_size(group)
     if src_local is None:
         src_local = owner_of(0, nk, size)

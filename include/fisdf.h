@@ -239,6 +239,14 @@ int fisdf_build_ws(fisdf_ctx* ctx, const void* d_Wq, int q0, int q1, int nip,
 int fisdf_build_ws_qs(fisdf_ctx* ctx, const void* d_Wq, const int* h_qs, const double* h_wt,
                       int nq, int nip, const int kmesh[3], const double a[9], void* d_Ws);
 
+/* Row block [i0, i1) of W_s for a q-list: d_Ws (nk, i1-i0, nip) = rows i0..i1 of every W_s[R] of
+ * fisdf_build_ws_qs.  A k-sharded build forms every rank's block of its partial sum and
+ * REDUCE-SCATTERS them (each rank then holds the rows its get_k contracts, half the bytes of the
+ * all-reduce of the whole W_s).  asynchronous. */
+int fisdf_build_ws_rows(fisdf_ctx* ctx, const void* d_Wq, const int* h_qs, const double* h_wt,
+                        int nq, int nip, const int kmesh[3], const double a[9], int i0, int i1,
+                        void* d_Ws);
+
 /* ---- A7: get_j_kpts (fftisdf.py:133-171) ------------------------------------
  * d_dms (nset, nk, nao, nao); d_vj same shape (complex; caller takes .real for Gamma). */
 int fisdf_get_j(fisdf_ctx* ctx, const void* d_X, const void* d_W0, const void* d_dms, int nset,
@@ -257,6 +265,10 @@ int fisdf_get_j_rows(fisdf_ctx* ctx, const void* d_X, const void* d_W0, const vo
 int fisdf_get_k_rows(fisdf_ctx* ctx, const void* d_X, const void* d_Ws, const void* d_dms,
                      int nset, int nip, int nao, const int kmesh[3], const double a[9], int i0,
                      int i1, void* d_vk);
+/* the same with only this block's W_s rows at hand: d_Ws_rows (nk, i1-i0, nip) */
+int fisdf_get_k_rows_local(fisdf_ctx* ctx, const void* d_X, const void* d_Ws_rows,
+                           const void* d_dms, int nset, int nip, int nao, const int kmesh[3],
+                           const double a[9], int i0, int i1, void* d_vk);
 /* J at band k-points (get_jk kpts_band; the reference asserts nband == nkpt, fftisdf.py:164):
  * rho and v = W0 rho from the k-mesh dms as fisdf_get_j, then J_k' = Xb_k'^H diag(v) Xb_k' with
  * d_Xb (nkb, nip, nao) the AOs at the interpolation points for the band k-points (the q = 0 pair
@@ -295,6 +307,15 @@ int fisdf_min_norm_operator(fisdf_ctx* ctx, const void* d_A, int n, double tol_r
 /* batched pivoted Cholesky (pivots + ranks to host; synchronous) */
 int fisdf_pivoted_cholesky(fisdf_ctx* ctx, const void* d_A, int n, int batch, int rmax,
                            double tol_rel, int* h_piv /* batch*rmax */, int* h_rank /* batch */);
+/* the fit's unpivoted blocked Cholesky of batch Hermitian PD n x n matrices, in place (lower
+ * triangle = L on return; 64-column blocks, the diagonal blocks factored and inverted in LDS);
+ * h_fail[b] = 1 when a pivot fell below tol_rel * max(diag) (the fit then refactors with
+ * pivoting).  synchronous */
+int fisdf_cholesky(fisdf_ctx* ctx, void* d_A, int n, int batch, double tol_rel, int* h_fail);
+/* L^{-1} of batch lower-triangular n x n matrices by the factor stage's block-row substitution
+ * (the operator the fit's triangular GEMM applies); a matrix's result does not depend on the
+ * batch it is computed in */
+int fisdf_tri_inverse(fisdf_ctx* ctx, const void* d_L, int n, int batch, void* d_Linv);
 
 #ifdef __cplusplus
 }

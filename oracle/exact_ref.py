@@ -43,8 +43,9 @@ def exact_k(chi, dms, a, mesh, kpts, coords):
             vG = fft(pair.reshape(-1, ngrid), mesh) * coulG
             vR = ifft(vG, mesh).reshape(nao, nao, ngrid) * em.conj()
             for i, dm in enumerate(dms):
-                # ao3[s, g] = sum_l D[l, s]... contraction: K[m,n] += sum_{l,s} vR[m,l,g] D[l,s] chi*_{k2,s}(g) chi_{k1,n}(g)
-                t = np.einsum("mlg,ls,gs->mg", vR, dm[k2], chi[k2].conj())
+                # K[m,n] += sum_{l,s,g} vR[m,l,g] D[l,s] chi*_{k2,s}(g) chi_{k1,n}(g)
+                u = dm[k2] @ chi[k2].conj().T                          # (l, g)
+                t = np.einsum("mlg,lg->mg", vR, u)
                 out[i, k1] += t @ chi[k1] * (vol / ngrid) / nk
     return out
 

@@ -87,18 +87,37 @@ def get_coulG(a, k, mesh, Gv=None, wrap_around=True, omega=None):
     return coulG
 
 
+def _fft_workers():
+    """Threads for the oracle's FFTs (PySCF's tools.fft is a multithreaded FFTW/NumPy engine;
+    the transform itself is the same): the process's CPU share — OMP_NUM_THREADS where the
+    host sets it (the GPU pool gives each one-GPU box 16 of the host's CPUs), else the CPUs this
+    process may run on."""
+    import os
+    n = os.environ.get("OMP_NUM_THREADS", "")
+    if n.isdigit() and int(n) > 0:
+        return int(n)
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def fft(f, mesh):
     """[pyscf] tools.fft: unnormalised fftn over mesh (fftisdf.py:113)."""
+    import scipy.fft
     f = np.asarray(f)
     n = f.shape[0]
-    return np.fft.fftn(f.reshape(n, *mesh), axes=(1, 2, 3)).reshape(n, -1)
+    return scipy.fft.fftn(f.reshape(n, *mesh), axes=(1, 2, 3),
+                          workers=_fft_workers()).reshape(n, -1)
 
 
 def ifft(f, mesh):
     """[pyscf] tools.ifft: ifftn (1/N) over mesh (fftisdf.py:118)."""
+    import scipy.fft
     f = np.asarray(f)
     n = f.shape[0]
-    return np.fft.ifftn(f.reshape(n, *mesh), axes=(1, 2, 3)).reshape(n, -1)
+    return scipy.fft.ifftn(f.reshape(n, *mesh), axes=(1, 2, 3),
+                           workers=_fft_workers()).reshape(n, -1)
 
 
 def pivoted_cholesky(A, tol=-1.0):

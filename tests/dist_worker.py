@@ -45,13 +45,20 @@ def main():
         from oracle import isdf_ref as R
         from fisdf.cell import madelung
         _, vk_e = df.get_jk(dm, exxdiv="ewald")
-        S = np.einsum("kgm,kgn->kmn", chi.conj(), chi) * (cell.vol / chi.shape[1])
-        vke0 = vk0 + madelung(cell, kmesh) * np.einsum("kmp,xkpq,kqn->xkmn", S, dm, S)
-        vj_w, vk_w = df.get_jk(dm, omega=0.4)
+        # every reference below is the oracle on THIS build's interpolation points (df.perm),
+        # whether or not they are dpstrf's: the checks hold on every run
         xip = x0[:, df.perm]
-        ob = R.build(xip, chi, coords, cell.a, kmesh, cell.mesh, omega=0.4)
         kpts = R.get_kpts(cell.a, kmesh)
         phase = R.get_phase(cell.a, kpts, kmesh)
+        if np.array_equal(df.perm, o["perm"]):
+            vk_own = vk0
+        else:
+            ob0 = R.build(xip, chi, coords, cell.a, kmesh, cell.mesh)
+            vk_own = R.get_k_kpts(xip, ob0["wq"], dm, phase)
+        S = np.einsum("kgm,kgn->kmn", chi.conj(), chi) * (cell.vol / chi.shape[1])
+        vke0 = vk_own + madelung(cell, kmesh) * np.einsum("kmp,xkpq,kqn->xkmn", S, dm, S)
+        vj_w, vk_w = df.get_jk(dm, omega=0.4)
+        ob = R.build(xip, chi, coords, cell.a, kmesh, cell.mesh, omega=0.4)
         extra = dict(vk_e=vk_e, vke0=vke0, vj_w=vj_w, vk_w=vk_w,
                      vjw0=R.get_j_kpts(xip, ob["w0"], dm), vkw0=R.get_k_kpts(xip, ob["wq"], dm, phase))
     np.savez(out, vj=vj, vk=vk, perm=df.perm, ranks=df.ranks, vj0=vj0, vk0=vk0,

@@ -26,11 +26,11 @@ JK_TOL = 1e-8        # Ha, north_star
 M_REL_TOL = 1e-8     # max |dM_q| / max |M_q|, M_q the AO-pair projection of W_q (below)
 
 
-def _gpu_build(cfg):
+def _gpu_build(cfg, c0=None):
     import bench
     from fisdf import ISDF
-    cell, kmesh, m0, c0, x0, chi, dm = bench.setup(cfg)
-    df = ISDF(cell, cell.get_kpts(kmesh), m0=list(m0), c0=c0)
+    cell, kmesh, m0, c0_cfg, x0, chi, dm = bench.setup(cfg)
+    df = ISDF(cell, cell.get_kpts(kmesh), m0=list(m0), c0=c0_cfg if c0 is None else c0)
     if cfg == "c4":          # C4 is the "SVD fit" configuration (BASELINE.json configs[3])
         df.fit = "svd"
     d = df.device
@@ -91,3 +91,93 @@ def test_config_parity_full_size(cfg):
         relw = abs(wq[q] - out["wq"][q]).max() / abs(out["wq"][q]).max()
         print(f"{cfg}: q {q} rel |dM_q| {rel:.2e} (raw rel |dW_q| {relw:.2e})", flush=True)
         assert rel < M_REL_TOL, (q, rel)
+
+
+def _oracle_jk(cell, kmesh, x0, chi, dm, perm):
+    """The reference CPU path (fftisdf.py:22-228, gelsy fit) on the interpolation points perm."""
+    from oracle import isdf_ref as R
+    xip = x0[:, perm]
+    out = R.build(xip, chi, cell.gen_uniform_grids(cell.mesh), cell.a, kmesh, cell.mesh)
+    kpts = R.get_kpts(cell.a, kmesh)
+    phase = R.get_phase(cell.a, kpts, kmesh)
+    dms = dm[None]
+    vj = R.get_j_kpts(xip, out["w0"], dms, kpts_band_is_zero=bool(abs(kpts).max() < 1e-9))[0]
+    vk = R.get_k_kpts(xip, out["wq"], dms, phase)[0]
+    return vj, vk, out
+
+
+SEL_RATIO = 1.5      # GPU build's error vs exact FFT-grid J/K, relative to the reference's own
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_jk_vs_reference_selection(cfg):
+    """End to end against the reference path on ITS OWN selection (LAPACK dpstrf pivots,
+    fftisdf.py:357-388), not on the GPU's points.
+
+    The parent-grid Gram of the diamond cell has exactly tied diagonal entries (symmetry-
+    equivalent grid points), so dpstrf's greedy pivots are decided by the last bits of x2: the
+    reference itself picks a different point set when x2 is summed in another valid order (C2:
+    pivots diverge at step 1, 51 % shared, J/K differ by 1.6e-3 / 2.5e-4 Ha —
+    tests/experiments/selection_sensitivity.py, profiles/r03_selection_sensitivity.log).  J/K of
+    two selections therefore differ at the ISDF-approximation level, not at rounding level, and
+    the 1e-8 bar applies on a common point set (test_config_parity_full_size).  What is asserted
+    here is that the GPU's selection is as good as the reference's: its error against the exact
+    FFT-grid J (and K at C2; oracle/exact_ref.py, PySCF fft_jk semantics) is within SEL_RATIO of
+    the reference build's, and the GPU-vs-reference difference is explained by that error."""
+    from oracle import exact_ref as E
+    from oracle import isdf_ref as R
+    df, cell, kmesh, x0, chi, dm, vj, vk, mi = _gpu_build(cfg)
+    t0 = time.perf_counter()
+    perm_ref, rank_ref, nip_ref, _ = R.select_interpolation_points(x0, cell.nao_nr(), df.c0)
+    shared = len(set(perm_ref.tolist()) & set(df.perm.tolist())) / len(perm_ref)
+    first = next((i for i in range(min(len(perm_ref), len(df.perm)))
+                  if perm_ref[i] != df.perm[i]), None)
+    vj_ref, vk_ref, _ = _oracle_jk(cell, kmesh, x0, chi, dm, perm_ref)
+    dj, dk = abs(vj - vj_ref).max(), abs(vk - vk_ref).max()
+    print(f"\n{cfg}: GPU vs reference on its own dpstrf pivots (nip {nip_ref}, first divergence "
+          f"{first}, shared {100 * shared:.0f}%): |dJ| {dj:.2e} |dK| {dk:.2e} "
+          f"(oracle {time.perf_counter() - t0:.1f} s)", flush=True)
+    if np.array_equal(perm_ref, df.perm):
+        assert dj < JK_TOL and dk < JK_TOL
+        return
+    t0 = time.perf_counter()
+    kpts = R.get_kpts(cell.a, kmesh)
+    dms = dm[None]
+    vje = E.exact_j(chi, dms, cell.a, cell.mesh)[0]
+    if abs(kpts).max() < 1e-9:
+        vje = vje.real
+    ej_gpu, ej_ref = abs(vj - vje).max(), abs(vj_ref - vje).max()
+    msg = f"{cfg}: vs exact FFT-grid J: GPU {ej_gpu:.2e}, reference {ej_ref:.2e}"
+    if cfg == "c2":   # exact K: nk^2 pair FFTs, affordable at 2x2x2
+        vke = E.exact_k(chi, dms, cell.a, cell.mesh, kpts, cell.gen_uniform_grids(cell.mesh))[0]
+        ek_gpu, ek_ref = abs(vk - vke).max(), abs(vk_ref - vke).max()
+        msg += f"; K: GPU {ek_gpu:.2e}, reference {ek_ref:.2e}"
+        assert ek_gpu <= SEL_RATIO * ek_ref, msg
+        assert dk <= 2 * max(ek_gpu, ek_ref), msg
+    print(msg + f" (exact {time.perf_counter() - t0:.1f} s)", flush=True)
+    assert ej_gpu <= SEL_RATIO * ej_ref, msg
+    assert dj <= 2 * max(ej_gpu, ej_ref), msg
+
+
+@pytest.mark.timeout(900)
+def test_min_norm_fit_full_size_rank_regime():
+    """The reference demo's regime at full size (fftisdf.py:455-461: c0 = 40, nip reaches the
+    parent-Gram rank through :383): C2's cell, basis, mesh and k-mesh with c0 large enough that
+    nip = rank (~1594 points), so every x4_q is rank-deficient and the fit takes the minimum-norm
+    path — against the gelsy oracle on the same points, < 1e-8 Ha."""
+    from oracle import isdf_ref as R
+    df, cell, kmesh, x0, chi, dm, vj, vk, mi = _gpu_build("c2", c0=1e4)
+    ng0 = x0.shape[1]
+    print(f"\nc2 rank regime: nip {df.nip} (parent grid {ng0}), x4_q ranks "
+          f"{df.ranks.min()}-{df.ranks.max()}, min-norm q {df.min_norm_slots}/{len(df.fit_qs)} "
+          f"max_imag {mi}", flush=True)
+    assert df.nip < ng0 and df.min_norm_slots == len(df.fit_qs)
+    assert max(mi) < 1e-10, mi
+    t0 = time.perf_counter()
+    vj0, vk0, out = _oracle_jk(cell, kmesh, x0, chi, dm, df.perm)
+    ej, ek = abs(vj - vj0).max(), abs(vk - vk0).max()
+    print(f"c2 rank regime: oracle {time.perf_counter() - t0:.1f} s, gelsy ranks "
+          f"{min(out['ranks'])}-{max(out['ranks'])}; |dJ| {ej:.2e} |dK| {ek:.2e} "
+          f"(margin {JK_TOL / max(ej, ek):.1f}x)", flush=True)
+    assert ej < JK_TOL and ek < JK_TOL

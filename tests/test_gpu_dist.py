@@ -97,8 +97,8 @@ def test_sharded_build_matches_single_gpu(name, world):
             ee = abs(o["vk_e"] - o["vke0"]).max()
             ewj, ewk = abs(o["vj_w"] - o["vjw0"]).max(), abs(o["vk_w"] - o["vkw0"]).max()
             print(f"  ewald |dK|={ee:.2e}  omega=0.4 |dJ|={ewj:.2e} |dK|={ewk:.2e}")
-            if np.array_equal(o["perm"], o["perm0"]):
-                assert ee < 1e-8 and ewj < 1e-8 and ewk < 1e-8
+            # references on the build's own points (dist_worker): asserted on every run
+            assert ee < 1e-8 and ewj < 1e-8 and ewk < 1e-8
             assert abs(o["vk_w"] - outs[0]["vk_w"]).max() == 0.0
         # every rank returns the same J/K and the same pivots
         assert abs(o["vj"] - outs[0]["vj"]).max() == 0.0

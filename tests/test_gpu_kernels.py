@@ -248,3 +248,64 @@ def test_build_y_kmesh_paths(env, kmesh, npts):
         print(f"kmesh {kmesh} time_reversal={tr}: max rel |y - y_oracle| = {rel:.2e}")
         assert rel < 1e-12
     ctx.call("fisdf_set_time_reversal", 0)
+
+
+@pytest.mark.parametrize("n", [1, 17, 36, 44, 64, 65, 81, 100, 128, 145, 236])
+def test_cholesky_unpivoted_partial_blocks(env, n):
+    """fisdf_cholesky (the fit's unpivoted blocked Cholesky: 64-column blocks, diagonal blocks
+    factored and 16x16-block inverted in LDS, panel by the block inverse^H, HERK trailing update)
+    vs numpy on random Hermitian PD matrices whose size leaves a partial last block (n % 64 in
+    {1, 17, 36, 44, 0, ...}); batch of 3, one with a diagonal block of condition ~1e10."""
+    torch, L, ctx = env
+    rng = np.random.default_rng(100 + n)
+    batch = 3
+    A = np.empty((batch, n, n), complex)
+    for b in range(batch):
+        B = rnd(rng, n, n + 8)
+        if b == 2:  # ill-conditioned: a geometric spectrum over 1e10 (every 64-block sees it)
+            Q, _ = np.linalg.qr(rnd(rng, n, n))
+            A[b] = (Q * np.logspace(0, -10, n)) @ Q.conj().T
+        else:
+            A[b] = B @ B.conj().T / n + np.eye(n)
+        A[b] = 0.5 * (A[b] + A[b].conj().T)
+    dA = dev(torch, A)
+    fail = np.zeros(batch, np.int32)
+    ctx.call("fisdf_cholesky", L.ptr(dA), n, batch, 1e-14, fail.ctypes.data_as(L._ip))
+    assert (fail == 0).all(), fail
+    out = dA.cpu().numpy()
+    for b in range(batch):
+        Lg = np.tril(out[b])
+        Lr = np.linalg.cholesky(A[b])
+        rel = abs(Lg - Lr).max() / abs(Lr).max()
+        res = abs(Lg @ Lg.conj().T - A[b]).max() / abs(A[b]).max()
+        print(f"n={n} b={b}: rel |L - L_np| {rel:.1e}, rel |L L^H - A| {res:.1e}")
+        assert res < 1e-13
+        # forward error bounded by the conditioning of the factor
+        assert rel < (1e-12 if b < 2 else 1e-4)
+
+
+@pytest.mark.parametrize("n", [300, 600])
+def test_tri_inverse_batch_invariant(env, n):
+    """L^{-1} by the factor stage's merged block-row substitution (split-K on the long block rows
+    for nip >= 256): a matrix inverted alone equals, bit for bit, the same matrix inverted inside
+    a batch of 8 (the k-sharded build factors fewer q per call than the 1-GPU build),
+    and matches numpy to the conditioning."""
+    torch, L, ctx = env
+    rng = np.random.default_rng(n)
+    batch = 8
+    Ls = np.tril(rnd(rng, batch, n, n)) * 0.3 / np.sqrt(n)
+    for b in range(batch):
+        Ls[b][np.diag_indices(n)] = 1.0 + rng.random(n)
+    dL = dev(torch, Ls)
+    dI = torch.empty_like(dL)
+    ctx.call("fisdf_tri_inverse", L.ptr(dL), n, batch, L.ptr(dI))
+    inv_b = dI.cpu().numpy()
+    for b in (0, 5):
+        d1 = dev(torch, Ls[b:b + 1])
+        o1 = torch.empty_like(d1)
+        ctx.call("fisdf_tri_inverse", L.ptr(d1), n, 1, L.ptr(o1))
+        one = o1.cpu().numpy()[0]
+        assert np.array_equal(one, inv_b[b]), abs(one - inv_b[b]).max()
+        ref = np.linalg.inv(Ls[b])
+        rel = abs(inv_b[b] - ref).max() / abs(ref).max()
+        assert rel < 1e-12, rel

@@ -138,18 +138,34 @@ def _worker(rank, size, port, result):
                                            cell.mesh, cell.vol, Gv)[0] for q in range(q0, q1)])
     ws = np.sqrt(nk) * (phase[:, q0:q1] @ wq_own.reshape(q1 - q0, -1)).real
     Ws = torch.from_numpy(ws.astype(np.complex128))
-    kshard.allreduce_ws(Ws, None)
+    kshard.allreduce_real_part(Ws, None)
     W0 = torch.from_numpy(wq_own[0].copy()) if q0 == 0 else torch.zeros(o["w0"].shape, dtype=torch.complex128)
     kshard.broadcast_w0(W0, nk, None)
     ws_full = np.sqrt(nk) * (phase @ o["wq"].reshape(nk, -1)).real
     err_ws = abs(Ws.numpy().real - ws_full).max() / abs(ws_full).max()
     err_w0 = abs(W0.numpy() - o["w0"]).max()
+    # the build's form: every rank's row block of the partial W_s, reduce-scattered by rows
+    nip = o["w0"].shape[0]
+    rows = [kshard.shard_range(nip, r, size) for r in range(size)]
+    chunk = nk * max(b - a for a, b in rows) * nip
+    blocks = torch.zeros(chunk * size, dtype=torch.complex128)
+    wsp = ws.reshape(nk, nip, nip)
+    for r, (i0, i1) in enumerate(rows):
+        blocks[r * chunk:r * chunk + nk * (i1 - i0) * nip] = torch.from_numpy(
+            np.ascontiguousarray(wsp[:, i0:i1]).ravel().astype(np.complex128))
+    i0, i1 = rows[rank]
+    mine = kshard.reduce_scatter_real(blocks, chunk, nk * (i1 - i0) * nip, rank, size, None)
+    ref_rows = ws_full.reshape(nk, nip, nip)[:, i0:i1]
+    err_ws = max(err_ws, abs(mine.numpy().reshape(nk, i1 - i0, nip) - ref_rows).max()
+                 / abs(ws_full).max())
+    assert abs(mine.numpy().imag).max() == 0.0
     result.put((rank, err_ws, err_w0))
     dist.destroy_process_group()
 
 
 def test_kshard_gloo_world2():
-    """N>1 path on CPU: per-rank q-shards + all-reduce(W_s) + broadcast(W_0) == unsharded."""
+    """N>1 path on CPU: per-rank q-shards + all-reduce(W_s) / the row-block reduce-scatter of W_s
+    + broadcast(W_0) == unsharded."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
