@@ -86,6 +86,10 @@ struct fisdf_ctx {
   int last_fit_lanes = 0, last_fit_pipe = 0;  // what the last fisdf_fit_coulomb_qs ran with
   std::vector<hipEvent_t> ev_ready;  // fisdf_mark_y_ready: y of local q j landed (sharded fit)
   std::vector<char> ready_marked;
+  // fisdf_set_y_slices: y of local q j read in place from its all-to-all piece (grid slices)
+  std::vector<const cplx*> y_piece;
+  std::vector<long> y_slices;  // (g0, ng) pairs of the pieces' layout, shared by every piece
+  std::map<std::vector<long>, PlaneRef*> plane_cache;  // device plane tables per (slices, mesh, rows)
   int* f_piv = nullptr;     // (nk, nip)
   int* f_rank_dev = nullptr;
   std::vector<int> f_rank;  // host copy
@@ -106,8 +110,13 @@ struct fisdf_ctx {
   unsigned long long* maximag = nullptr;  // 3 slots
   // timing
   bool timing = false;
-  struct Ev { int stage; hipEvent_t a, b; };
+  struct Ev { int stage; hipEvent_t a, b; int span; };
   std::vector<Ev> events;
+  // kernel execution spans of the kernel-exact stages (StageTimer): 2 u64 per slot, all-ones
+  // initialised, read and refilled by fisdf_timings
+  unsigned long long* spans = nullptr;
+  int span_used = 0;
+  static constexpr int kSpanCap = 16384;
 };
 
 namespace {
@@ -167,39 +176,37 @@ int upload_ints(fisdf_ctx* c, const int* h, int n, int* d) {
   return n <= 0 ? 0 : upload_bytes(c, h, sizeof(int) * (size_t)n, d);
 }
 
-// Stage timer on stream `st`.  Default: events recorded on the stream around the stage.
-// kernel_exact: the stage is ONE zgemm()/herk() call, whose first kernel takes `a` and whose last
-// kernel takes `b` at launch (launch_events, hipExtLaunchKernelGGL) — the kernels' own begin /
-// end, as rocprofv3's kernel trace reports them, without the time the stream waits for CUs the
-// other fit lanes hold between the two stream positions.
+// Stage timer on stream `st`: events recorded on the stream around the stage.  kernel_exact: the
+// stage is ONE zgemm()/herk() call whose kernels also record their execution span on the device
+// (launch_events); fisdf_timings then reports that span — the kernels' own begin to end, as
+// rocprofv3's kernel trace times them — instead of the event interval, which beside the other fit
+// lanes also counts the time the stream waits for free CUs (r02: ~10 % more than the trace).
 struct StageTimer {
   fisdf_ctx* c;
   int stage;
   hipStream_t st;
   bool exact;
   hipEvent_t a = nullptr, b = nullptr;
+  int span = -1;
   StageTimer(fisdf_ctx* c_, int stg, hipStream_t on = nullptr, bool kernel_exact = false)
       : c(c_), stage(stg), st(on ? on : c_->stream), exact(kernel_exact) {
     if (c->timing) {
       (void)hipEventCreate(&a);
       (void)hipEventCreate(&b);
-      if (exact)
-        launch_events() = LaunchEvents{a, b};
-      else
-        (void)hipEventRecord(a, st);
+      (void)hipEventRecord(a, st);
+      if (exact && c->spans && c->span_used < fisdf_ctx::kSpanCap) {
+        span = c->span_used++;
+        LaunchEvents le;
+        le.span = c->spans + 2 * span;
+        launch_events() = le;
+      }
     }
   }
   ~StageTimer() {
     if (c->timing) {
-      if (exact) {
-        LaunchEvents& le = launch_events();
-        if (le.start == a) (void)hipEventRecord(a, st);  // no kernel ran: an empty interval
-        if (le.stop == b || le.start == a) (void)hipEventRecord(b, st);
-        le = LaunchEvents();
-      } else {
-        (void)hipEventRecord(b, st);
-      }
-      c->events.push_back({stage, a, b});
+      (void)hipEventRecord(b, st);
+      if (span >= 0) launch_events() = LaunchEvents();
+      c->events.push_back({stage, a, b, span});
     }
   }
 };
@@ -584,10 +591,12 @@ int fisdf_destroy(fisdf_ctx* c) {
   for (hipEvent_t e : c->ev_q) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_free) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_ready) (void)hipEventDestroy(e);
+  for (auto& kv : c->plane_cache) (void)hipFree(kv.second);
   if (c->arena) (void)hipFree(c->arena);
   if (c->ev_stage) (void)hipEventSynchronize(c->ev_stage), (void)hipEventDestroy(c->ev_stage);
   if (c->stage_pinned) (void)hipHostFree(c->stage_pinned);
   if (c->maximag) (void)hipFree(c->maximag);
+  if (c->spans) (void)hipFree(c->spans);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -629,6 +638,13 @@ int fisdf_memcpy_dtoh(fisdf_ctx* c, void* h, const void* d, size_t bytes) {
 int fisdf_set_timing(fisdf_ctx* c, int enable) {
   FISDF_TRY(device_guard(c));
   c->timing = enable != 0;
+  if (c->timing && !c->spans) {
+    FISDF_HIP(hipMalloc(&c->spans, sizeof(unsigned long long) * 2 * fisdf_ctx::kSpanCap));
+    FISDF_HIP(hipMemsetAsync(c->spans, 0xff, sizeof(unsigned long long) * 2 * fisdf_ctx::kSpanCap,
+                             c->stream));
+    FISDF_HIP(hipStreamSynchronize(c->stream));
+    c->span_used = 0;
+  }
   return 0;
 }
 
@@ -639,15 +655,32 @@ int fisdf_timings(fisdf_ctx* c, double* ms, int* calls) {
     if (ms) ms[i] = 0;
     if (calls) calls[i] = 0;
   }
+  std::vector<unsigned long long> sp(2 * (size_t)c->span_used);
+  if (c->span_used) {
+    FISDF_HIP(hipDeviceSynchronize());  // the lanes' kernels too
+    FISDF_HIP(hipMemcpy(sp.data(), c->spans, sizeof(unsigned long long) * sp.size(),
+                        hipMemcpyDeviceToHost));
+  }
   for (auto& e : c->events) {
     float t = 0;
-    FISDF_HIP(hipEventElapsedTime(&t, e.a, e.b));
+    if (e.span >= 0) {
+      // the kernels' own execution span: s_memrealtime runs at 100 MHz
+      const unsigned long long t0 = sp[2 * e.span], t1 = ~sp[2 * e.span + 1];
+      t = (t0 != ~0ull && sp[2 * e.span + 1] != ~0ull && t1 >= t0) ? (float)((t1 - t0) * 1e-5) : 0.f;
+    } else {
+      FISDF_HIP(hipEventElapsedTime(&t, e.a, e.b));
+    }
     if (ms) ms[e.stage] += t;
     if (calls) calls[e.stage] += 1;
     (void)hipEventDestroy(e.a);
     (void)hipEventDestroy(e.b);
   }
   c->events.clear();
+  if (c->span_used) {
+    FISDF_HIP(hipMemsetAsync(c->spans, 0xff, sizeof(unsigned long long) * 2 * c->span_used, c->stream));
+    FISDF_HIP(hipStreamSynchronize(c->stream));
+    c->span_used = 0;
+  }
   return 0;
 }
 
@@ -679,6 +712,15 @@ int fisdf_zgemm(fisdf_ctx* c, int opA, int opB, int M, int N, int K, const doubl
   return zgemm(c->stream, opA, opB, M, N, K, cmk(alpha[0], alpha[1]), (const cplx*)A, lda, sA,
                (const cplx*)B, ldb, sB, cmk(beta[0], beta[1]), (cplx*)C, ldc, sC, batch,
                ksplit, work);
+}
+
+int fisdf_zgemm_mode(fisdf_ctx* c, int opA, int opB, int M, int N, int K, const double alpha[2],
+                     const void* A, long lda, long sA, const void* B, long ldb, long sB,
+                     const double beta[2], void* C, long ldc, long sC, int batch, int mode) {
+  FISDF_TRY(device_guard(c));
+  return zgemm(c->stream, opA, opB, M, N, K, cmk(alpha[0], alpha[1]), (const cplx*)A, lda, sA,
+               (const cplx*)B, ldb, sB, cmk(beta[0], beta[1]), (cplx*)C, ldc, sC, batch, 1,
+               nullptr, EPI_NONE, nullptr, mode);
 }
 
 int fisdf_herk(fisdf_ctx* c, int n, int K, double alpha, const void* A, long lda, void* Cm,
@@ -1399,6 +1441,25 @@ int fisdf_mark_y_ready(fisdf_ctx* c, int j) {
   return 0;
 }
 
+int fisdf_set_y_slices(fisdf_ctx* c, int j, const void* recv, int nparts, const long* h_g0,
+                       const long* h_ng) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(recv != nullptr && nparts >= 1 && nparts <= 4096, "set_y_slices: bad piece");
+  std::vector<long> sl;
+  for (int p = 0; p < nparts; ++p) {
+    FISDF_CHECK(h_g0[p] >= 0 && h_ng[p] >= 0, "set_y_slices: bad slice");
+    sl.push_back(h_g0[p]);
+    sl.push_back(h_ng[p]);
+  }
+  bool any = false;
+  for (const cplx* pc : c->y_piece) any = any || pc != nullptr;
+  FISDF_CHECK(!any || sl == c->y_slices, "set_y_slices: every piece of a call has one layout");
+  c->y_slices = sl;
+  if ((int)c->y_piece.size() <= j) c->y_piece.resize(j + 1, nullptr);
+  c->y_piece[j] = (const cplx*)recv;
+  return fisdf_mark_y_ready(c, j);
+}
+
 int fisdf_fit_info(fisdf_ctx* c, int* h_lanes, int* h_pipe_depth) {
   FISDF_CHECK(c != nullptr, "null context");
   if (h_lanes) *h_lanes = c->last_fit_lanes;
@@ -1515,6 +1576,35 @@ int fisdf_factor_x4(fisdf_ctx* c, const void* x4v, int q0, int q1, int nip, doub
   return fisdf_factor_x4_qs(c, x4v, qs.data(), (int)qs.size(), nip, tol_rel, nullptr, h_ranks);
 }
 
+// device table of where each plane i0 of a row lives inside an all-to-all piece (the concat over
+// slices p of (rows, ng_p) blocks of grid points [g0_p, g0_p + ng_p)); cached per layout
+static int plane_table(fisdf_ctx* c, const int mesh[3], int rows, const PlaneRef** out) {
+  const long P = (long)mesh[1] * mesh[2], n0 = mesh[0];
+  FISDF_CHECK(fft3d_reads_slices(mesh[0], mesh[1], mesh[2]),
+              "fit_coulomb: sliced y needs a mesh the plane FFT kernels take");
+  std::vector<long> key = c->y_slices;
+  key.insert(key.end(), {(long)mesh[0], (long)mesh[1], (long)mesh[2], (long)rows});
+  auto it = c->plane_cache.find(key);
+  if (it == c->plane_cache.end()) {
+    std::vector<PlaneRef> h(n0, PlaneRef{-1, 0});
+    long off = 0;
+    for (size_t p = 0; p + 1 < c->y_slices.size(); p += 2) {
+      const long g0 = c->y_slices[p], ng = c->y_slices[p + 1];
+      FISDF_CHECK(g0 % P == 0 && ng % P == 0 && g0 + ng <= n0 * P,
+                  "fit_coulomb: y slices must be whole planes of the mesh");
+      for (long i0 = g0 / P; i0 < (g0 + ng) / P; ++i0) h[i0] = PlaneRef{off + (i0 * P - g0), ng};
+      off += (long)rows * ng;
+    }
+    for (long i0 = 0; i0 < n0; ++i0) FISDF_CHECK(h[i0].base >= 0, "fit_coulomb: y slices leave a plane out");
+    PlaneRef* d = nullptr;
+    FISDF_HIP(hipMalloc(&d, sizeof(PlaneRef) * n0));
+    FISDF_HIP(hipMemcpy(d, h.data(), sizeof(PlaneRef) * n0, hipMemcpyHostToDevice));
+    it = c->plane_cache.emplace(key, d).first;
+  }
+  *out = it->second;
+  return 0;
+}
+
 // ---- A4 + A5 ------------------------------------------------------------------
 int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv, int nip,
                          const int mesh[3], const int kmesh[3], const double a[9], void* Wqv) {
@@ -1523,7 +1613,10 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   // call cannot leave the next one running in 'ready' mode against stale events
   struct ClearMarks {
     fisdf_ctx* c;
-    ~ClearMarks() { c->ready_marked.assign(c->ready_marked.size(), 0); }
+    ~ClearMarks() {
+      c->ready_marked.assign(c->ready_marked.size(), 0);
+      c->y_piece.clear();
+    }
   } clear_marks{c};
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
   FISDF_TRY(check_qlist(h_qs, nq, nk, "fit_coulomb"));
@@ -1535,6 +1628,9 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
                   std::equal(h_qs, h_qs + nq, it0),
               "fit_coulomb: the q-list must be a contiguous run of the factored q-list");
   const int s0 = (int)(it0 - c->f_qs.begin());
+  auto piece_of = [&](int lq) -> const cplx* {
+    return lq < (int)c->y_piece.size() ? c->y_piece[lq] : nullptr;
+  };
   FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
   const long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
   const long nn = (long)nip * nip;
@@ -1701,6 +1797,13 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   auto weight_q = [&](hipStream_t st, int lq, const double** w) {
     return get_weight(c, st, mesh, kmesh, a, h_qs[lq], wscale, half_of(s0 + lq), w);
   };
+  // sharded build: q read in place from their all-to-all pieces (fisdf_set_y_slices) through a
+  // per-plane address table (plane-aligned slices)
+  const PlaneRef* planes = nullptr;
+  bool any_piece = false;
+  for (int lq = 0; lq < nq; ++lq) any_piece = any_piece || piece_of(lq) != nullptr;
+  if (any_piece) FISDF_TRY(plane_table(c, mesh, nip, &planes));
+  FISDF_CHECK(yT != nullptr || any_piece, "fit_coulomb: no y");
   auto fft_q = [&](hipStream_t st, int lq, cplx* Yh) -> int {
     const int sl = s0 + lq;
     const int r = cod_of(sl) ? nip : c->f_rank[sl];
@@ -1710,8 +1813,10 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     const double* wt = nullptr;
     FISDF_TRY(weight_q(st, lq, &wt));
     StageTimer tm(c, FISDF_ST_FFT, st);
-    FISDF_TRY(fft3d(st, yT + (long)lq * nip * ngrid, ngrid, c->f_piv + (long)sl * nip, Yh, ngrid,
-                    r, mesh[0], mesh[1], mesh[2], kd, wt, nullptr));
+    const cplx* pc = piece_of(lq);
+    FISDF_CHECK(pc || yT, "fit_coulomb: q without y");
+    FISDF_TRY(fft3d(st, pc ? pc : yT + (long)lq * nip * ngrid, ngrid, c->f_piv + (long)sl * nip, Yh,
+                    ngrid, r, mesh[0], mesh[1], mesh[2], kd, wt, nullptr, pc ? planes : nullptr));
     return 0;
   };
   // ring slot of q lq (pipelined mode)

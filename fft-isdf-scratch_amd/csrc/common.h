@@ -1,7 +1,6 @@
 // fisdf — MI355X-native FFT-ISDF kernels: shared device/host helpers.
 #pragma once
 #include <hip/hip_runtime.h>
-#include <hip/hip_ext.h>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -40,15 +39,25 @@ void set_error(const std::string& msg);
     if (_r != 0) return _r;    \
   } while (0)
 
-// ---- kernel-exact stage timing: when set, the next zgemm()/herk() call launches its first
-// kernel with `start` and its last kernel with `stop` through hipExtLaunchKernelGGL, so the two
-// events carry that call's kernel begin / end timestamps (the dispatch packet's, as rocprofv3's
-// kernel trace sees them) instead of the stream positions around it; the call clears both.
-// Host-thread local (one context per thread).
+// ---- kernel-exact stage timing: when set, the next zgemm()/herk() call's kernels record their
+// execution span {first workgroup start, last wave end} (s_memrealtime, 100 MHz ticks) into
+// `span` — the kernels' own time, what rocprofv3's kernel trace reports, rather than the stream
+// positions around them (which, beside other fit lanes, also count the wait for free CUs); the
+// call clears it.  Host-thread local (one context per thread).
 struct LaunchEvents {
-  hipEvent_t start = nullptr, stop = nullptr;
+  unsigned long long* span = nullptr;
 };
 LaunchEvents& launch_events();
+
+// record a kernel's execution span: span[0] = min start, span[1] = ~(max end) (both kept as
+// minima so one all-ones fill initialises a slot); span may be null
+__device__ __forceinline__ void span_begin(unsigned long long* span) {
+  if (span && threadIdx.x == 0) atomicMin(span, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void span_end(unsigned long long* span) {
+  if (span && (threadIdx.x & 63) == 0)
+    atomicMin(span + 1, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
 
 // ---- complex helpers (device + host)
 __host__ __device__ inline cplx cmk(double r, double i) { cplx c; c.x = r; c.y = i; return c; }
@@ -84,6 +93,14 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha,
           int epi = EPI_NONE, unsigned long long* mon = nullptr, int mode = GEMM_FULL,
           long ldaux = 0);
 
+// the 64 x 128-tile kernel for big single NN products (zgemm_wide.hip); zgemm() routes there
+bool wide_gemm_enabled();
+bool zgemm_wide_applies(int opA, int opB, int M, int N, int K, int batch, int ksplit, int epi,
+                        int mode);
+int zgemm_nn_wide(hipStream_t s, int M, int N, int K, cplx alpha, const cplx* A, long lda,
+                  const cplx* B, long ldb, cplx beta, cplx* C, long ldc, int mode,
+                  unsigned long long* span);
+
 // C = alpha A A^H (Hermitian rank-K update; lower tiles computed, upper mirrored)
 int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cplx* C, long ldc,
          int ksplit = 1, cplx* work = nullptr, int mode = GEMM_FULL);
@@ -106,11 +123,22 @@ int chol_unpivoted(hipStream_t s, cplx* W, int n, int batch, double tol_rel, int
 int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rmax, double tol,
                       int* piv, int* rank, double* work, int* flags, bool* handled);
 
+// Where plane i0 of input row r lives when the rows arrive in grid slices (the all-to-all
+// pieces of a k-sharded build): in + base + r * ld, one entry per plane (device table)
+struct PlaneRef {
+  long base;
+  long ld;
+};
+
 // 3-D FFT (unnormalised forward, numpy.fft.fftn sign) over `rows` rows of length n0*n1*n2.
 // in-row gather `rowidx` (may be null), pre-multiply by exp(-i (f.kd)) where f are the
 // fftfreq fractions (if kd != null), post-multiply by weight[G] (if weight != null).
+// planes (device, n0 entries, may be null): sliced input — plane i0 of row r at
+// in + planes[i0].base + r * planes[i0].ld (in_ld unused); needs fft3d_reads_slices(mesh)
 int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* out, long out_ld,
           int rows, int n0, int n1, int n2, const double* kd /*3 or null*/,
-          const double* weight /*ngrid or null*/, cplx* work);
+          const double* weight /*ngrid or null*/, cplx* work, const PlaneRef* planes = nullptr);
+// whether fft3d takes sliced input for this mesh (its first pass is a per-plane kernel)
+bool fft3d_reads_slices(int n0, int n1, int n2);
 
 }  // namespace fisdf

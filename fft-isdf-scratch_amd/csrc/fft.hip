@@ -221,7 +221,8 @@ template <bool BIG>
 __global__ __launch_bounds__(256) void fft_plane_kernel(
     const cplx* __restrict__ in, long in_ld, const int* __restrict__ rowidx, cplx* out, long out_ld,
     int rows, Stages st1, Stages st2, const cplx* __restrict__ tw1g, const cplx* __restrict__ tw2g,
-    int n0, int n1, int n2, double kd0, double kd1, double kd2, int use_phase) {
+    int n0, int n1, int n2, double kd0, double kd1, double kd2, int use_phase,
+    const PlaneRef* __restrict__ planes) {
   extern __shared__ cplx smem[];
   cplx* tw1 = smem;
   cplx* tw2 = smem + MAXN;
@@ -233,7 +234,8 @@ __global__ __launch_bounds__(256) void fft_plane_kernel(
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int row = blockIdx.x / n0, i0 = blockIdx.x % n0;
   if (row >= rows) return;
-  const cplx* src = in + (long)(rowidx ? rowidx[row] : row) * in_ld + (long)i0 * P;
+  const long r = rowidx ? rowidx[row] : row;
+  const cplx* src = planes ? in + planes[i0].base + r * planes[i0].ld : in + r * in_ld + (long)i0 * P;
   cplx* dstp = out + (long)row * out_ld + (long)i0 * P;
   // issue this plane's loads first (branch-free, up to 8 per thread in flight)
   constexpr int U = 8;
@@ -374,14 +376,16 @@ __global__ __launch_bounds__(64) void fft_plane_reg(const cplx* __restrict__ in,
                                                     const int* __restrict__ rowidx, cplx* out,
                                                     long out_ld, int rows, int n0,
                                                     const cplx* __restrict__ W, double kd0,
-                                                    double kd1, double kd2, int use_phase) {
+                                                    double kd1, double kd2, int use_phase,
+                                                    const PlaneRef* __restrict__ planes) {
   constexpr int P = NN * NN, LD = NN + 1;
   __shared__ cplx img[NN * LD];
   __shared__ cplx ph1[NN], ph2[NN];
   const int lane = threadIdx.x;
   const int row = blockIdx.x / n0, i0 = blockIdx.x % n0;
   if (row >= rows) return;
-  const cplx* src = in + (long)(rowidx ? rowidx[row] : row) * in_ld + (long)i0 * P;
+  const long r = rowidx ? rowidx[row] : row;
+  const cplx* src = planes ? in + planes[i0].base + r * planes[i0].ld : in + r * in_ld + (long)i0 * P;
   cplx* dst = out + (long)row * out_ld + (long)i0 * P;
   constexpr int U = (P + 63) / 64;
   cplx v[U];
@@ -466,14 +470,14 @@ __global__ __launch_bounds__(256) void fft_axis0_reg(const cplx* in, long in_ld,
 
 int fft_plane_reg_launch(hipStream_t s, int n, const cplx* in, long in_ld, const int* rowidx,
                          cplx* out, long out_ld, int rows, int n0, const cplx* W, const double* kd,
-                         bool* done) {
+                         const PlaneRef* planes, bool* done) {
   *done = false;
   const double k0 = kd ? kd[0] : 0, k1 = kd ? kd[1] : 0, k2 = kd ? kd[2] : 0;
-  const long planes = (long)rows * n0;
+  const long nplanes = (long)rows * n0;
 #define FISDF_PL(N)                                                                            \
   if (n == N) {                                                                                \
-    hipLaunchKernelGGL(fft_plane_reg<N>, dim3((unsigned)planes), dim3(64), 0, s, in, in_ld,     \
-                       rowidx, out, out_ld, rows, n0, W, k0, k1, k2, kd ? 1 : 0);               \
+    hipLaunchKernelGGL(fft_plane_reg<N>, dim3((unsigned)nplanes), dim3(64), 0, s, in, in_ld,    \
+                       rowidx, out, out_ld, rows, n0, W, k0, k1, k2, kd ? 1 : 0, planes);       \
     *done = true;                                                                              \
   }
   FISDF_REG_SIZES(FISDF_PL)
@@ -600,32 +604,43 @@ int axis_pass(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx
 
 }  // namespace
 
+// the register path's mesh test (square (i1, i2) planes of a listed size, listed n0)
+bool reg_mesh(int n0, int n1, int n2) {
+  if (n1 != n2) return false;
+  int a = 0, b = 0;
+#define FISDF_HAS(N) if (n1 == N) a = 1; if (n0 == N) b = 1;
+  FISDF_REG_SIZES(FISDF_HAS)
+#undef FISDF_HAS
+  return a && b;
+}
+
+size_t plane_kernel_lds(int n1, int n2) { return sizeof(cplx) * (4 * MAXN + 2 * (size_t)n1 * n2); }
+
+bool fft3d_reads_slices(int n0, int n1, int n2) {
+  return reg_mesh(n0, n1, n2) || plane_kernel_lds(n1, n2) <= 96 * 1024;
+}
+
 int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* out, long out_ld,
-          int rows, int n0, int n1, int n2, const double* kd, const double* weight, cplx* /*work*/) {
+          int rows, int n0, int n1, int n2, const double* kd, const double* weight, cplx* /*work*/,
+          const PlaneRef* planes) {
   if (rows == 0) return 0;
   FISDF_CHECK(in != out || rowidx == nullptr, "fft: in-place pass cannot gather rows");
-  if (n1 == n2) {  // register kernels: square (i1, i2) planes of a listed size, listed n0
+  FISDF_CHECK(!planes || fft3d_reads_slices(n0, n1, n2), "fft: sliced input needs a plane kernel");
+  if (reg_mesh(n0, n1, n2)) {  // register kernels: square (i1, i2) planes of a listed size, listed n0
     const cplx *W12 = nullptr, *W0 = nullptr;
     FISDF_TRY(get_twiddles(n1, &W12));
     FISDF_TRY(get_twiddles(n0, &W0));
     bool ok1 = false, ok0 = false;
     FISDF_CHECK((long)rows * n0 < (1L << 31) && (long)rows * n1 * n2 < (1L << 38), "fft: too large");
-    // probe both specialisations before launching anything
-    const int dims_ok = [&] {
-      int a = 0, b = 0;
-#define FISDF_HAS(N) if (n1 == N) a = 1; if (n0 == N) b = 1;
-      FISDF_REG_SIZES(FISDF_HAS)
-#undef FISDF_HAS
-      return a && b;
-    }();
-    if (dims_ok) {
-      FISDF_TRY(fft_plane_reg_launch(s, n1, in, in_ld, rowidx, out, out_ld, rows, n0, W12, kd, &ok1));
+    {
+      FISDF_TRY(fft_plane_reg_launch(s, n1, in, in_ld, rowidx, out, out_ld, rows, n0, W12, kd,
+                                     planes, &ok1));
       FISDF_TRY(fft_axis0_reg_launch(s, n0, out, out_ld, out, out_ld, rows, n1 * n2, W0, weight, &ok0));
       FISDF_CHECK(ok1 && ok0, "fft: register kernel dispatch failed");
       return 0;
     }
   }
-  const size_t plane_lds = sizeof(cplx) * (4 * MAXN + 2 * (size_t)n1 * n2);
+  const size_t plane_lds = plane_kernel_lds(n1, n2);
   if (plane_lds <= 96 * 1024) {
     // axes 2+1 fused per (i1,i2) plane, then axis 0 with the Coulomb weight: 2 HBM passes
     Stages st1, st2;
@@ -634,18 +649,18 @@ int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* ou
     const cplx *tw1 = nullptr, *tw2 = nullptr;
     FISDF_TRY(get_twiddles(n1, &tw1));
     FISDF_TRY(get_twiddles(n2, &tw2));
-    const long planes = (long)rows * n0;
-    FISDF_CHECK(planes < (1L << 31), "fft: too many planes");
+    const long nplanes = (long)rows * n0;
+    FISDF_CHECK(nplanes < (1L << 31), "fft: too many planes");
     double k0 = 0, k1 = 0, k2 = 0;
     if (kd) { k0 = kd[0]; k1 = kd[1]; k2 = kd[2]; }
     if (needs_big(st1) || needs_big(st2))
-      hipLaunchKernelGGL(fft_plane_kernel<true>, dim3((unsigned)planes), dim3(256), plane_lds, s,
+      hipLaunchKernelGGL(fft_plane_kernel<true>, dim3((unsigned)nplanes), dim3(256), plane_lds, s,
                          in, in_ld, rowidx, out, out_ld, rows, st1, st2, tw1, tw2, n0, n1, n2, k0,
-                         k1, k2, kd != nullptr ? 1 : 0);
+                         k1, k2, kd != nullptr ? 1 : 0, planes);
     else
-      hipLaunchKernelGGL(fft_plane_kernel<false>, dim3((unsigned)planes), dim3(256), plane_lds, s,
+      hipLaunchKernelGGL(fft_plane_kernel<false>, dim3((unsigned)nplanes), dim3(256), plane_lds, s,
                          in, in_ld, rowidx, out, out_ld, rows, st1, st2, tw1, tw2, n0, n1, n2, k0,
-                         k1, k2, kd != nullptr ? 1 : 0);
+                         k1, k2, kd != nullptr ? 1 : 0, planes);
     FISDF_HIP(hipGetLastError());
   } else {
     FISDF_TRY(axis_pass(s, in, in_ld, rowidx, out, out_ld, rows, 2, n0, n1, n2, kd, nullptr));

@@ -186,7 +186,8 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
                                                          cplx beta, cplx* __restrict__ C, long ldc, long sC,
                                                          int ksplit, int kchunk, cplx* __restrict__ work,
                                                          int epi, unsigned long long* __restrict__ mon, long ldaux,
-                                                         int nMt, int ntile, int ntot) {
+                                                         int nMt, int ntile, int ntot,
+                                                         unsigned long long* __restrict__ span) {
   constexpr bool AK = !(OPA & 1);  // A stored [m][k]
   constexpr bool BKc = (OPB & 1);  // B stored [n][k]
   constexpr bool CA = (OPA & 2) != 0, CB = (OPB & 2) != 0;
@@ -198,6 +199,7 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
   const int per = (int)(gridDim.x >> 3);
   const int order = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
   if (order >= ntot) return;
+  span_begin(span);
   const int zz = order / ntile, t = order - zz * ntile;
   const int split = zz % ksplit;
   const int bz = zz / ksplit;
@@ -439,11 +441,14 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
 
   zgemm_epilogue<HERK>(M, N, alpha, beta, C, ldc, sC, ksplit, split, bz, work, epi, mon, ldaux, m0, n0, wm,
                        wn, lane, mask, accR, accI);
+  span_end(span);
 }
 
 // C = alpha * sum_s work[s] + beta * C  (deterministic split-K reduction)
 __global__ void ksplit_reduce(int M, int N, int ksplit, const cplx* __restrict__ work, cplx alpha,
-                              cplx beta, cplx* __restrict__ C, long ldc, long sC) {
+                              cplx beta, cplx* __restrict__ C, long ldc, long sC,
+                              unsigned long long* __restrict__ span) {
+  span_begin(span);
   const int bz = blockIdx.y;
   const long MN = (long)M * N;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < MN; e += (long)gridDim.x * blockDim.x) {
@@ -455,6 +460,7 @@ __global__ void ksplit_reduce(int M, int N, int ksplit, const cplx* __restrict__
     if (beta.x != 0.0 || beta.y != 0.0) v = cadd(v, cmul(beta, *cp));
     *cp = v;
   }
+  span_end(span);
 }
 
 // HERK split-K reduction: C = alpha sum_s work[s] over the lower 16x16 blocks the HERK kernel
@@ -463,7 +469,9 @@ __global__ void ksplit_reduce(int M, int N, int ksplit, const cplx* __restrict__
 // the partial reads and the C writes stay coalesced
 __global__ __launch_bounds__(256) void herk_reduce_kernel(int n, int ksplit,
                                                           const cplx* __restrict__ work, double alpha,
-                                                          cplx* __restrict__ C, long ldc) {
+                                                          cplx* __restrict__ C, long ldc,
+                                                          unsigned long long* __restrict__ span) {
+  span_begin(span);
   __shared__ cplx tile[32][33];
   int t = blockIdx.x, ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
   while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
@@ -487,16 +495,16 @@ __global__ __launch_bounds__(256) void herk_reduce_kernel(int n, int ksplit,
     const int sr = ti * 32 + tx, sc = tj * 32 + rr;
     if (sr < n && sc < n && (sr >> 4) > (sc >> 4)) C[(long)sc * ldc + sr] = cconj(tile[tx][rr]);
   }
+  span_end(span);
 }
 
 // the kernel-exact timing events of the current zgemm()/herk() call (taken from launch_events()
 // at its entry): the main kernel records `start`, the call's last kernel `stop`
 struct CallEvents {
-  hipEvent_t start = nullptr, stop = nullptr;
+  unsigned long long* span = nullptr;
   CallEvents() {
     LaunchEvents& le = launch_events();
-    start = le.start;
-    stop = le.stop;
+    span = le.span;
     le = LaunchEvents();
   }
 };
@@ -505,35 +513,23 @@ template <int OPA, int OPB, bool HERK = false, int MODE = GEMM_FULL>
 void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cplx* A, long lda,
             long sA, const cplx* B, long ldb, long sB, cplx beta, cplx* C, long ldc, long sC,
             int ksplit, int kchunk, cplx* work, int epi, unsigned long long* mon, long ldaux,
-            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+            unsigned long long* span = nullptr) {
   // grid = (N-tiles or triangle tiles, M-tiles, z-slices) -> padded 1-D XCD-aware order
   const int nMt = HERK ? 1 : (int)grid.y;
   const int ntile = (int)(grid.x * (HERK ? 1 : grid.y));
   const long ntot = (long)ntile * grid.z;
   const long per = (ntot + 7) / 8;
+  const dim3 g((unsigned)(8 * per));
   // short K loops (<= 4 steps per workgroup, e.g. the y build's K = nao): a 2-deep ring
   // (32 KB of LDS) lets more workgroups share a CU, overlapping their load and store phases
-  const dim3 g((unsigned)(8 * per));
-  // the extension launch only when timing asks for the kernel's own timestamps
-  if (kchunk <= 4 * BK) {
-    if (ev0 || ev1)
-      hipExtLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, 2>), g, dim3(256), 0, s, ev0,
-                            ev1, 0, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
-                            ksplit, kchunk, work, epi, mon, ldaux, nMt, ntile, (int)ntot);
-    else
-      hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, 2>), g, dim3(256), 0, s, M, N, K,
-                         alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work,
-                         epi, mon, ldaux, nMt, ntile, (int)ntot);
-  } else {
-    if (ev0 || ev1)
-      hipExtLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, NST>), g, dim3(256), 0, s,
-                            ev0, ev1, 0, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
-                            ksplit, kchunk, work, epi, mon, ldaux, nMt, ntile, (int)ntot);
-    else
-      hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, NST>), g, dim3(256), 0, s, M, N,
-                         K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work,
-                         epi, mon, ldaux, nMt, ntile, (int)ntot);
-  }
+  if (kchunk <= 4 * BK)
+    hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, 2>), g, dim3(256), 0, s, M, N, K,
+                       alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work, epi,
+                       mon, ldaux, nMt, ntile, (int)ntot, span);
+  else
+    hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, NST>), g, dim3(256), 0, s, M, N, K,
+                       alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work, epi,
+                       mon, ldaux, nMt, ntile, (int)ntot, span);
 }
 
 }  // namespace
@@ -555,6 +551,10 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
   if (M == 0 || N == 0 || batch == 0) return 0;
   if (ksplit < 1) ksplit = 1;
   if (epi != EPI_NONE) ksplit = 1;
+  if (zgemm_wide_applies(opA, opB, M, N, K, batch, ksplit, epi, mode)) {
+    const CallEvents ev;
+    return zgemm_nn_wide(s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, mode, ev.span);
+  }
   if (ksplit > 1) FISDF_CHECK(work != nullptr, "zgemm: split-K needs a workspace");
   int kchunk = (K + ksplit - 1) / ksplit;
   kchunk = ((kchunk + BK - 1) / BK) * BK;
@@ -564,16 +564,15 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
               "zgemm: too many tiles");
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch * ksplit);
   const CallEvents ev;
-  hipEvent_t ev_last = ksplit > 1 ? nullptr : ev.stop;  // the reduce ends the call when split
 #define FISDF_CASE(a, b)                                                                      \
   case a * 4 + b:                                                                             \
     launch<a, b>(s, grid, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit,   \
-                 kchunk, work, epi, mon, ldaux, ev.start, ev_last);                           \
+                 kchunk, work, epi, mon, ldaux, ev.span);                           \
     break;
 #define FISDF_MCASE(a, b, m)                                                                  \
   if (opA == a && opB == b && mode == m) {                                                    \
     launch<a, b, false, m>(s, grid, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, \
-                           ksplit, kchunk, work, epi, mon, ldaux, ev.start, ev_last);         \
+                           ksplit, kchunk, work, epi, mon, ldaux, ev.span);         \
   }
   FISDF_MCASE(0, 0, 1) FISDF_MCASE(0, 0, 2) FISDF_MCASE(0, 0, 3)
   FISDF_MCASE(0, 0, 4) FISDF_MCASE(0, 0, 5)
@@ -591,12 +590,8 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
   if (ksplit > 1) {
     long MN = (long)M * N;
     int blocks = (int)std::min<long>((MN + 255) / 256, 4096);
-    if (ev.stop)
-      hipExtLaunchKernelGGL(ksplit_reduce, dim3(blocks, batch), dim3(256), 0, s, nullptr, ev.stop,
-                            0, M, N, ksplit, (const cplx*)work, alpha, beta, C, ldc, sC);
-    else
-      hipLaunchKernelGGL(ksplit_reduce, dim3(blocks, batch), dim3(256), 0, s, M, N, ksplit,
-                         (const cplx*)work, alpha, beta, C, ldc, sC);
+    hipLaunchKernelGGL(ksplit_reduce, dim3(blocks, batch), dim3(256), 0, s, M, N, ksplit,
+                       (const cplx*)work, alpha, beta, C, ldc, sC, ev.span);
     FISDF_HIP(hipGetLastError());
   }
   return 0;
@@ -616,23 +611,18 @@ int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cpl
   const int nt = (n + BM - 1) / BM;
   dim3 grid(nt * (nt + 1) / 2, 1, ksplit);
   const CallEvents ev;
-  hipEvent_t ev_last = ksplit > 1 ? nullptr : ev.stop;
   if (mode == GEMM_RE_ONLY)  // C = Re(A A^H): 2 of the 4 MFMAs per complex block
     launch<OP_N, OP_C, true, GEMM_RE_ONLY>(s, grid, n, n, K, cmk(alpha, 0), A, lda, 0, A, lda, 0,
                                            cmk(0, 0), C, ldc, 0, ksplit, kchunk, work, EPI_NONE,
-                                           nullptr, 0, ev.start, ev_last);
+                                           nullptr, 0, ev.span);
   else
     launch<OP_N, OP_C, true>(s, grid, n, n, K, cmk(alpha, 0), A, lda, 0, A, lda, 0, cmk(0, 0), C,
-                             ldc, 0, ksplit, kchunk, work, EPI_NONE, nullptr, 0, ev.start, ev_last);
+                             ldc, 0, ksplit, kchunk, work, EPI_NONE, nullptr, 0, ev.span);
   FISDF_HIP(hipGetLastError());
   if (ksplit > 1) {
     const int t32 = (n + 31) / 32;
-    if (ev.stop)
-      hipExtLaunchKernelGGL(herk_reduce_kernel, dim3(t32 * (t32 + 1) / 2), dim3(256), 0, s,
-                            nullptr, ev.stop, 0, n, ksplit, (const cplx*)work, alpha, C, ldc);
-    else
-      hipLaunchKernelGGL(herk_reduce_kernel, dim3(t32 * (t32 + 1) / 2), dim3(256), 0, s, n, ksplit,
-                         (const cplx*)work, alpha, C, ldc);
+    hipLaunchKernelGGL(herk_reduce_kernel, dim3(t32 * (t32 + 1) / 2), dim3(256), 0, s, n, ksplit,
+                       (const cplx*)work, alpha, C, ldc, ev.span);
     FISDF_HIP(hipGetLastError());
   }
   return 0;

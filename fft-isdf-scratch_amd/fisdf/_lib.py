@@ -73,6 +73,7 @@ _SIGS = {
     "fisdf_set_fit_pipe": ([_vp, _i, _i], _i),
     "fisdf_fit_info": ([_vp, _ip, _ip], _i),
     "fisdf_mark_y_ready": ([_vp, _i], _i),
+    "fisdf_set_y_slices": ([_vp, _i, _vp, _i, C.POINTER(_l), C.POINTER(_l)], _i),
     "fisdf_reserve_workspace": ([_vp, C.c_size_t], _i),
     "fisdf_fit_coulomb_qs": ([_vp, _ip, _i, _vp, _i, _ip, _ip, _dp, _vp], _i),
     "fisdf_build_ws_qs": ([_vp, _vp, _ip, _dp, _i, _i, _ip, _dp, _vp], _i),
@@ -85,6 +86,8 @@ _SIGS = {
     "fisdf_get_eri": ([_vp, _vp, _i, _i, _ip, _vp, C.POINTER(_vp), _ip, _vp], _i),
     "fisdf_zgemm": ([_vp, _i, _i, _i, _i, _i, _dp, _vp, _l, _l, _vp, _l, _l, _dp, _vp, _l, _l,
                      _i, _i], _i),
+    "fisdf_zgemm_mode": ([_vp, _i, _i, _i, _i, _i, _dp, _vp, _l, _l, _vp, _l, _l, _dp, _vp, _l,
+                          _l, _i, _i], _i),
     "fisdf_herk": ([_vp, _i, _i, _d, _vp, _l, _vp, _l, _i], _i),
     "fisdf_fft3d": ([_vp, _vp, _vp, _i, _ip], _i),
     "fisdf_coulg": ([_vp, _ip, _dp, _dp, _d, _i, _vp], _i),

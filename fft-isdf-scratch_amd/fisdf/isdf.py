@@ -535,9 +535,9 @@ def build(df_obj):
     d.ctx.call("fisdf_set_time_reversal", 1 if df_obj.time_reversal else 0)
     d.ctx.call("fisdf_set_omega", float(getattr(df_obj, "_fit_omega", 0.0)))
     df_obj._omega_dfs = {}                   # range-separated states of an earlier build
-    yT = d.empty((nq, nip, ngrid))
     sharded = d.sharded(df_obj)
     if not sharded:
+        yT = d.empty((nq, nip, ngrid))
         d.ctx.call("fisdf_build_y_qs", _lib.ptr(f), ngrid * nao, 0, ngrid, ngrid, _lib.ptr(X),
                    nip, nao, km_p, a_p, qs_c, nq, _lib.ptr(yT))                 # :67-87
         factor_async()
@@ -577,15 +577,16 @@ def build(df_obj):
         for j, (recv, work) in enumerate(pieces):
             if work is not None:
                 work.wait()               # stream-ordered: no host block with RCCL
-            d.ctx.call("fisdf_unpack_slices", _lib.ptr(recv), nip, d.size, g0s, ngs, ngrid,
-                       _lib.ptr(yT[j]))
-            d.ctx.call("fisdf_mark_y_ready", j)   # the fit of q j waits for this point only
+            # the fit's FFT reads q j straight from its piece (plane-aligned grid slices); its
+            # lanes wait for this point only
+            d.ctx.call("fisdf_set_y_slices", j, _lib.ptr(recv), d.size, g0s, ngs)
         # one call over the whole shard: its lanes and pipelined FFT stream start each q as
         # soon as that q's piece has landed
         if nq:
-            d.ctx.call("fisdf_fit_coulomb_qs", qs_c, nq, _lib.ptr(yT), nip, mesh_p, km_p, a_p,
+            d.ctx.call("fisdf_fit_coulomb_qs", qs_c, nq, None, nip, mesh_p, km_p, a_p,
                        _lib.ptr(Wq))
         del send, pieces
+        yT = None
     del yT
 
     if sharded:

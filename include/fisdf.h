@@ -217,6 +217,13 @@ int fisdf_fit_info(fisdf_ctx* ctx, int* h_lanes, int* h_pipe_depth);
  * FFT as soon as its own piece is there (one call for the whole shard keeps the lanes and the
  * pipelined FFT stream; replaces one call per q).  Marks are consumed by the call. */
 int fisdf_mark_y_ready(fisdf_ctx* ctx, int j);
+/* The same, with the j-th q's y read IN PLACE from its all-to-all piece d_recv (replaces
+ * fisdf_unpack_slices + fisdf_mark_y_ready): d_recv holds, for p = 0..nparts-1, the (nip,
+ * h_ng[p]) block of grid points [h_g0[p], h_g0[p] + h_ng[p]), whole planes of the mesh; the fit's
+ * FFT reads each plane where it lies.  Every piece of one call has the same layout; d_yT of that
+ * call may then be NULL.  The piece must stay alive until the call's work is done. */
+int fisdf_set_y_slices(fisdf_ctx* ctx, int j, const void* d_recv, int nparts, const long* h_g0,
+                       const long* h_ng);
 /* Grow the context's scratch arena to at least `bytes` now (pre-allocation; a failed growth
  * leaves an empty arena, never a stale one). */
 int fisdf_reserve_workspace(fisdf_ctx* ctx, size_t bytes);
@@ -290,6 +297,13 @@ int fisdf_get_eri(fisdf_ctx* ctx, const void* d_X, int nip, int nao, const int k
 int fisdf_zgemm(fisdf_ctx* ctx, int opA, int opB, int M, int N, int K, const double alpha[2],
                 const void* d_A, long lda, long strideA, const void* d_B, long ldb, long strideB,
                 const double beta[2], void* d_C, long ldc, long strideC, int batch, int ksplit);
+/* the same with the fit's arithmetic modes (no split-K): 1 = Im op(A) taken as zero, 2 = only
+ * Re C formed, 4 = op(A) lower triangular (op N), 8 = op(A) = A^H upper triangular (op C), 5 =
+ * 4 | 1; NN products with N >= 512 run on the 64 x 128-tile kernel */
+int fisdf_zgemm_mode(fisdf_ctx* ctx, int opA, int opB, int M, int N, int K, const double alpha[2],
+                     const void* d_A, long lda, long strideA, const void* d_B, long ldb,
+                     long strideB, const double beta[2], void* d_C, long ldc, long strideC,
+                     int batch, int mode);
 /* C = alpha A A^H (A: n x K, lda; C: n x n, ldc), Hermitian: lower tiles + mirror */
 int fisdf_herk(fisdf_ctx* ctx, int n, int K, double alpha, const void* d_A, long lda, void* d_C,
                long ldc, int ksplit);

@@ -160,13 +160,44 @@ def test_jk_vs_reference_selection(cfg):
     assert dj <= 2 * max(ej_gpu, ej_ref), msg
 
 
+def _gelsy_jk(cell, kmesh, x0, chi, dm, perm, cond):
+    """J/K of the reference path with gelsy at rcond `cond` (None: scipy's default, eps)."""
+    import scipy.linalg as sl
+    from oracle import isdf_ref as R
+    xip = x0[:, perm]
+    kpts = R.get_kpts(cell.a, kmesh)
+    phase = R.get_phase(cell.a, kpts, kmesh)
+    coords = cell.gen_uniform_grids(cell.mesh)
+    x4 = R.build_x4(xip, phase)
+    N = coords.shape[0]
+    yall = np.empty((len(kpts), N, xip.shape[1]), complex)
+    for g0 in range(0, N, 8000):
+        yall[:, g0:g0 + 8000] = R.build_y(chi[:, g0:g0 + 8000], xip, phase)
+    Gv = R.get_Gv(cell.a, cell.mesh)
+    ws, ranks = [], []
+    for q, vq in enumerate(kpts):
+        fq = np.exp(-1j * coords @ vq)
+        z, _, r, _ = sl.lstsq(x4[q], yall[q].T, cond=cond, lapack_driver="gelsy")  # :108
+        zeta = R.fft(z * fq, cell.mesh) * R.get_coulG(cell.a, vq, cell.mesh, Gv=Gv) * (cell.vol / N)
+        ws.append((R.ifft(zeta, cell.mesh) * fq.conj()) @ z.conj().T)
+        ranks.append(r)
+    w = np.asarray(ws)
+    dms = dm[None]
+    return (R.get_j_kpts(xip, w[0], dms, kpts_band_is_zero=bool(abs(kpts).max() < 1e-9))[0],
+            R.get_k_kpts(xip, w, dms, phase)[0], ranks)
+
+
 @pytest.mark.timeout(900)
 def test_min_norm_fit_full_size_rank_regime():
     """The reference demo's regime at full size (fftisdf.py:455-461: c0 = 40, nip reaches the
     parent-Gram rank through :383): C2's cell, basis, mesh and k-mesh with c0 large enough that
-    nip = rank (~1594 points), so every x4_q is rank-deficient and the fit takes the minimum-norm
-    path — against the gelsy oracle on the same points, < 1e-8 Ha."""
-    from oracle import isdf_ref as R
+    nip = rank (~1500-1600 points), so every x4_q is rank-deficient (cond ~1e16: directions at
+    the rounding level decide the solution) and the fit takes the minimum-norm path (DESIGN
+    §3.4).  Here the reference's own answer is only defined to the level its solver moves under
+    a change of rcond: gelsy at 4x and 1/4x its default rcond differs from itself by ~1.5e-7 Ha
+    (J) / ~2.5e-8 (K) (tests/experiments/rank_regime_c2.py, profiles/r03_rank_regime_c2.log),
+    above the 1e-8 bar.  Asserted: the GPU's J/K sit within 2x of that band around gelsy at its
+    default rcond, on the GPU's points."""
     df, cell, kmesh, x0, chi, dm, vj, vk, mi = _gpu_build("c2", c0=1e4)
     ng0 = x0.shape[1]
     print(f"\nc2 rank regime: nip {df.nip} (parent grid {ng0}), x4_q ranks "
@@ -175,9 +206,18 @@ def test_min_norm_fit_full_size_rank_regime():
     assert df.nip < ng0 and df.min_norm_slots == len(df.fit_qs)
     assert max(mi) < 1e-10, mi
     t0 = time.perf_counter()
-    vj0, vk0, out = _oracle_jk(cell, kmesh, x0, chi, dm, df.perm)
+    eps = np.finfo(float).eps
+    vj0, vk0, r0 = _gelsy_jk(cell, kmesh, x0, chi, dm, df.perm, None)
+    band_j = band_k = 0.0
+    for cond in (4 * eps, eps / 4):
+        vj1, vk1, r1 = _gelsy_jk(cell, kmesh, x0, chi, dm, df.perm, cond)
+        band_j = max(band_j, abs(vj1 - vj0).max())
+        band_k = max(band_k, abs(vk1 - vk0).max())
+        print(f"c2 rank regime: gelsy rcond {cond:.1e} (ranks {min(r1)}-{max(r1)}) vs default "
+              f"(ranks {min(r0)}-{max(r0)}): |dJ| {abs(vj1 - vj0).max():.2e} "
+              f"|dK| {abs(vk1 - vk0).max():.2e}", flush=True)
     ej, ek = abs(vj - vj0).max(), abs(vk - vk0).max()
-    print(f"c2 rank regime: oracle {time.perf_counter() - t0:.1f} s, gelsy ranks "
-          f"{min(out['ranks'])}-{max(out['ranks'])}; |dJ| {ej:.2e} |dK| {ek:.2e} "
-          f"(margin {JK_TOL / max(ej, ek):.1f}x)", flush=True)
-    assert ej < JK_TOL and ek < JK_TOL
+    print(f"c2 rank regime: GPU vs gelsy: |dJ| {ej:.2e} |dK| {ek:.2e}; gelsy's own rcond band "
+          f"|dJ| {band_j:.2e} |dK| {band_k:.2e} (margins {2 * band_j / ej:.1f}x / "
+          f"{2 * band_k / ek:.1f}x; oracle {time.perf_counter() - t0:.1f} s)", flush=True)
+    assert ej <= 2 * band_j and ek <= 2 * band_k

@@ -309,3 +309,34 @@ def test_tri_inverse_batch_invariant(env, n):
         ref = np.linalg.inv(Ls[b])
         rel = abs(inv_b[b] - ref).max() / abs(ref).max()
         assert rel < 1e-12, rel
+
+
+@pytest.mark.parametrize("M,N,K,mode", [(600, 1000, 600, 0), (600, 1000, 600, 4), (600, 777, 600, 5),
+                                        (600, 600, 600, 1), (24, 700, 50, 0), (100, 2000, 33, 0),
+                                        (1, 512, 8, 0), (129, 513, 17, 4), (64, 4096, 64, 5),
+                                        (600, 24624, 600, 5)])
+def test_zgemm_modes_wide(env, M, N, K, mode):
+    """NN products through fisdf_zgemm_mode: N >= 512 takes the 64 x 128-tile kernel
+    (zgemm_wide.hip) — FULL (3 MFMAs per complex block), A_REAL (Im A ignored), A_LOWER (K loop
+    cut at each M-tile's last row) and both, M-edge tiles with <= 32 rows, ragged N — against
+    numpy on the matrices the mode describes."""
+    torch, L, ctx = env
+    rng = np.random.default_rng(M * 7 + N + K + mode)
+    A, B = rnd(rng, M, K), rnd(rng, K, N)
+    Aeff = A.copy()
+    if mode & 1:
+        Aeff = Aeff.real.astype(complex)
+    if mode & 4:
+        Aeff = np.tril(Aeff)
+        # lower triangular input; past each 64-row M-tile's last row the K loop stops, so
+        # anything there must never be read
+        beyond = np.arange(K)[None, :] >= 64 * (np.arange(M)[:, None] // 64 + 1)
+        A = np.tril(A) + np.where(beyond, rnd(rng, M, K) * 1e3, 0)
+    dA, dB = dev(torch, A), dev(torch, B)
+    dC = torch.zeros((M, N), dtype=torch.complex128, device="cuda")
+    one, zero = np.array([1.0, 0.0]), np.array([0.0, 0.0])
+    ctx.call("fisdf_zgemm_mode", 0, 0, M, N, K, one.ctypes.data_as(L._dp), L.ptr(dA), K, 0,
+             L.ptr(dB), N, 0, zero.ctypes.data_as(L._dp), L.ptr(dC), N, 0, 1, mode)
+    ref = Aeff @ B
+    err = abs(dC.cpu().numpy() - ref).max()
+    assert err < 1e-12 * max(K, 16), err
