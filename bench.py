@@ -57,6 +57,8 @@ def parse():
                    help="time, on this one GPU, each rank's share of an N-rank k-sharded build "
                         "(its compute; collectives replaced by their local effect, kshard."
                         "EmulatedGroup) and print one JSON line with the per-rank step times")
+    p.add_argument("--emulate-only", type=int, default=None, metavar="R",
+                   help="with --emulate-ranks: time rank R only (profiling one rank's share)")
     return p.parse_args()
 
 
@@ -187,7 +189,7 @@ def emulate_ranks(args):
     chunks = kshard.balanced_chunks(np.where(real_q, 0.6, 1.0), N)
     slices = kshard.grid_slices(cell.mesh, N)
     per_rank = []
-    for R in range(N):
+    for R in range(N) if args.emulate_only is None else [args.emulate_only]:
         pieces = kshard.emulated_pieces(yall, chunks, slices, R)
         df = ISDF(cell, cell.get_kpts(kmesh), m0=list(m0), c0=c0,
                   comm=kshard.EmulatedGroup(R, N, pieces))

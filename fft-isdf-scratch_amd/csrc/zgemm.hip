@@ -179,7 +179,7 @@ constexpr int NST = FISDF_NST;  // LDS ring depth; loads run NST-1 K-steps ahead
 constexpr int LPW = TILE / (64 * 4);  // glds wave-instructions per operand per step per wave
 __device__ cplx g_zero_page[64];      // zero-initialised device global
 
-template <int OPA, int OPB, bool HERK, int MODE, int NS>
+template <int OPA, int OPB, bool HERK, int MODE, int NS, bool PIPE = false>
 __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cplx alpha,
                                                          const cplx* __restrict__ A, long lda, long sA,
                                                          const cplx* __restrict__ B, long ldb, long sB,
@@ -316,12 +316,146 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
     }
 
   const int nsteps = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  const int i16 = lane & 15, kq = lane >> 4;
+  if constexpr (PIPE && M3) {
+    // Software-pipelined 3-multiplication loop (host-checked: K and the K-chunk multiples of BK,
+    // operand extents < 4 GB).  The next K-substep's LDS fragments are read while the current
+    // substep's P3 = (ar + ai')(br + bi') group runs (P1 and P2 are the last uses of the raw
+    // fragments, so the reads reuse their registers); the next K-step's barrier sits between
+    // the last substep's P1/P2 and P3 groups.  Rows / columns outside the matrix read a clamped
+    // in-range row / column (they only feed C entries that are never stored), so every lane
+    // advances by one uniform stride: per-lane 32-bit byte offsets from a wave-uniform base
+    // (the SADDR form of the LDS-DMA load).  No loads past the last K-step.
+    (void)rowA;
+    (void)rowB;
+    unsigned oA[LPW], oB[LPW];
+#pragma unroll
+    for (int j = 0; j < LPW; ++j) {
+      const int sl = (w * LPW + j) * 64 + lane;
+      int x, k;
+      if (AK) { x = sl / BK; k = (sl % BK) ^ (x & (BK - 1)); }
+      else { x = sl % 64; k = sl / 64; }
+      const long xa = min(m0 + x, M - 1);
+      oA[j] = (unsigned)((AK ? xa * lda + k : (long)k * lda + xa) * 16);
+      if (BKc) { x = sl / BK; k = (sl % BK) ^ (x & (BK - 1)); }
+      else { x = sl % 64; k = sl / 64; }
+      const long xb = min(n0 + x, N - 1);
+      oB[j] = (unsigned)((BKc ? xb * ldb + k : (long)k * ldb + xb) * 16);
+    }
+    const cplx* baseA = A + (AK ? (long)kbeg : (long)kbeg * lda);
+    const cplx* baseB = B + (BKc ? (long)kbeg : (long)kbeg * ldb);
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    auto gldss = [&](const cplx* base, unsigned off, unsigned lds_byte) {
+      unsigned keep;
+      const unsigned dst = __builtin_amdgcn_readfirstlane(lds_byte);
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(off), "s"(base), "s"(dst) : "memory");
+    };
+    auto issue_p = [&](int st) {
+      const int buf = st % NS;
+      const unsigned la = lds0 + (unsigned)((buf * 2 + 0) * TILE) * 16u;
+      const unsigned lb = lds0 + (unsigned)((buf * 2 + 1) * TILE) * 16u;
+      const cplx* ba = baseA + st * stepA;
+      const cplx* bb = baseB + st * stepB;
+#pragma unroll
+      for (int j = 0; j < LPW; ++j) {
+        gldss(ba, oA[j], la + (unsigned)((wu * LPW + j) * 64) * 16u);
+        gldss(bb, oB[j], lb + (unsigned)((wu * LPW + j) * 64) * 16u);
+      }
+    };
+    auto pipeloop = [&](auto maskc) {
+      constexpr int MASK = decltype(maskc)::value;
+      if (nsteps == 0) return;
+#pragma unroll
+      for (int st = 0; st < NS - 1; ++st)
+        if (st < nsteps) issue_p(st);
+      if (nsteps > 1)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * LPW * (NS - 2)) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      cplx fa[2], fb[2];
+      auto rd = [&](int slot, int kk) {
+        const cplx* as = sm + (long)(slot * 2 + 0) * TILE;
+        const cplx* bs = sm + (long)(slot * 2 + 1) * TILE;
+        const int k = kk + kq;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          fa[u] = as[SA::slot((wm + u * 16 + i16) & 63, k)];
+          fb[u] = bs[SB::slot((wn + u * 16 + i16) & 63, k)];
+        }
+      };
+      rd(0, 0);
+      if (NS - 1 < nsteps) issue_p(NS - 1);
+      double sa[2], sb[2];
+      auto p12 = [&]() {
+        double ar[2], ai[2], br[2], bi[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          ar[u] = fa[u].x;
+          ai[u] = CA ? -fa[u].y : fa[u].y;
+          br[u] = fb[u].x;
+          bi[u] = CB ? -fb[u].y : fb[u].y;
+          sa[u] = ar[u] + ai[u];
+          sb[u] = br[u] + bi[u];
+        }
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            if ((MASK >> (mi * 2 + ni)) & 1)
+              accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], accR[mi][ni], 0, 0, 0);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            if ((MASK >> (mi * 2 + ni)) & 1)
+              accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], bi[ni], accI[mi][ni], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      auto p3 = [&]() {
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            if ((MASK >> (mi * 2 + ni)) & 1)
+              acc3[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(sa[mi], sb[ni], acc3[mi][ni], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      for (int s = 0; s < nsteps; ++s) {
+        const int cur = s % NS;
+        p12();
+        rd(cur, 4);
+        __builtin_amdgcn_sched_barrier(0);
+        p3();
+        p12();
+        if (s + 1 < nsteps) {
+          if (s + 2 < nsteps)
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * LPW * (NS - 2)) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          rd((s + 1) % NS, 0);
+          if (s + NS < nsteps) issue_p(s + NS);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        p3();
+      }
+    };
+    switch (mask) {
+      case 13: pipeloop(std::integral_constant<int, 13>{}); break;
+      case 5: pipeloop(std::integral_constant<int, 5>{}); break;
+      case 3: pipeloop(std::integral_constant<int, 3>{}); break;
+      case 1: pipeloop(std::integral_constant<int, 1>{}); break;
+      case 0: pipeloop(std::integral_constant<int, 0>{}); break;
+      default: pipeloop(std::integral_constant<int, 15>{}); break;
+    }
+  } else {
   // (steps past the end load the zero page: the counted waits assume NST-1 steps in flight)
   if (nsteps > 0) {
 #pragma unroll
     for (int st = 0; st < NS - 1; ++st) issue(st);
   }
-  const int i16 = lane & 15, kq = lane >> 4;
   auto mainloop = [&](auto maskc) {
     constexpr int MASK = decltype(maskc)::value;
     for (int s = 0; s < nsteps; ++s) {
@@ -424,6 +558,7 @@ __global__ __launch_bounds__(256) void zgemm_glds_kernel(int M, int N, int K, cp
     case 0: mainloop(std::integral_constant<int, 0>{}); break;
     default: mainloop(std::integral_constant<int, 15>{}); break;
   }
+  }
   // drain the (zero-page / unused) loads still in flight before the workgroup exits
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (M3) {
@@ -509,6 +644,15 @@ struct CallEvents {
   }
 };
 
+// FISDF_GEMM_PIPE=0: the unpipelined main loop for every launch (A/B on one box)
+bool pipe_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FISDF_GEMM_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int OPA, int OPB, bool HERK = false, int MODE = GEMM_FULL>
 void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cplx* A, long lda,
             long sA, const cplx* B, long ldb, long sB, cplx beta, cplx* C, long ldc, long sC,
@@ -522,9 +666,19 @@ void launch(hipStream_t s, dim3 grid, int M, int N, int K, cplx alpha, const cpl
   const dim3 g((unsigned)(8 * per));
   // short K loops (<= 4 steps per workgroup, e.g. the y build's K = nao): a 2-deep ring
   // (32 KB of LDS) lets more workgroups share a CU, overlapping their load and store phases
+  // the software-pipelined 3-multiplication loop: every workgroup's K range a whole number of
+  // K-steps, per-lane operand offsets within 32 bits
+  constexpr bool M3 = FISDF_GEMM_3M && (MODE & (GEMM_A_REAL | GEMM_RE_ONLY)) == 0;
+  auto fits32 = [](long rows, long ld) { return rows * ld * 16 < (1L << 32); };
+  const bool pipe = M3 && pipe_enabled() && K % BK == 0 && kchunk % BK == 0 &&
+                    fits32(!(OPA & 1) ? M : K, lda) && fits32((OPB & 1) ? N : K, ldb);
   if (kchunk <= 4 * BK)
     hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, 2>), g, dim3(256), 0, s, M, N, K,
                        alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work, epi,
+                       mon, ldaux, nMt, ntile, (int)ntot, span);
+  else if (pipe)
+    hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, NST, M3>), g, dim3(256), 0, s, M, N,
+                       K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, ksplit, kchunk, work, epi,
                        mon, ldaux, nMt, ntile, (int)ntot, span);
   else
     hipLaunchKernelGGL((zgemm_glds_kernel<OPA, OPB, HERK, MODE, NST>), g, dim3(256), 0, s, M, N, K,

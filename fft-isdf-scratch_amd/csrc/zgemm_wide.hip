@@ -19,6 +19,10 @@ namespace fisdf {
 
 namespace {
 
+#ifndef FISDF_WIDE_PIPE
+#define FISDF_WIDE_PIPE 1
+#endif
+
 constexpr int WBM = 64, WBN = 128, WBK = 8;
 constexpr int TA = WBM * WBK;   // complex elements of one A stage (8 KB)
 constexpr int TB = WBN * WBK;   // one B stage (16 KB)
@@ -110,11 +114,151 @@ __global__ __launch_bounds__(256, 2) void zgemm_nn_wide_kernel(
     }
 
   const int nsteps = kend > 0 ? (kend + WBK - 1) / WBK : 0;
+  const int i16 = lane & 15, kq = lane >> 4;
+#if FISDF_WIDE_PIPE
+  // Software-pipelined main loop (kend % WBK == 0, checked by zgemm_wide_applies): the LDS
+  // fragments of the next K-substep are read while the current substep's third MFMA group
+  // (P3 = (ar + ai)(br + bi)) runs — after P1 and P2 the raw fragments are dead, so the reads
+  // reuse their registers — and the barrier of the next K-step sits inside the last substep,
+  // between its P1/P2 and P3 groups.  Per-lane operand pointers advance by a fixed stride (the
+  // zero page at stride 0 for rows / columns outside the matrix); no loads past the last step.
+  // rows / columns outside the matrix read a clamped in-range row / column instead of the zero
+  // page: they only feed C rows / columns that are never stored, and every lane then advances
+  // by the same (scalar) stride
+  (void)kA;
+  (void)kB;
+  // per-lane 32-bit byte offsets from a wave-uniform base (the SADDR form of the LDS-DMA load):
+  // one VGPR per piece, the K advance in scalar registers
+  unsigned oA[LPA], oB[LPB];
+#pragma unroll
+  for (int j = 0; j < LPA; ++j) {
+    const int sl = (w * LPA + j) * 64 + lane;
+    const int x = sl / WBK, k = (sl % WBK) ^ (x & (WBK - 1));
+    oA[j] = (unsigned)(((long)min(m0 + x, M - 1) * lda + k) * 16);
+  }
+#pragma unroll
+  for (int j = 0; j < LPB; ++j) {
+    const int sl = (w * LPB + j) * 64 + lane;
+    const int x = sl % WBN, k = sl / WBN;
+    oB[j] = (unsigned)(((long)k * ldb + min(n0 + x, N - 1)) * 16);
+  }
+  const long dBs = (long)WBK * ldb;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto gldss = [&](const cplx* base, unsigned off, unsigned lds_byte) {
+    unsigned keep;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_byte);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(off), "s"(base), "s"(dst) : "memory");
+  };
+  auto issue_p = [&](int st) {  // K-step st -> ring slot st % NS
+    const int buf = st % NS;
+    const unsigned la = lds0 + (unsigned)(buf * (TA + TB)) * 16u;
+    const unsigned lb = la + (unsigned)TA * 16u;
+    const cplx* ba = A + (long)st * WBK;
+    const cplx* bb = B + st * dBs;
+#pragma unroll
+    for (int j = 0; j < LPA; ++j) gldss(ba, oA[j], la + (unsigned)((wu * LPA + j) * 64) * 16u);
+#pragma unroll
+    for (int j = 0; j < LPB; ++j) gldss(bb, oB[j], lb + (unsigned)((wu * LPB + j) * 64) * 16u);
+  };
+  auto pipeloop = [&](auto nbc) {
+    constexpr int NB = decltype(nbc)::value;
+    if (nsteps == 0) return;
+#pragma unroll
+    for (int st = 0; st < NS - 1; ++st)
+      if (st < nsteps) issue_p(st);
+    if (nsteps > 1)
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((LPA + LPB) * (NS - 2)) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    cplx fa[2], fb[NB];
+    auto rd = [&](int slot, int kk) {
+      const cplx* as = sm + (long)slot * (TA + TB);
+      const cplx* bs = as + TA;
+      const int k = kk + kq;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int x = wm + u * 16 + i16;
+        fa[u] = as[x * WBK + (k ^ (x & (WBK - 1)))];
+      }
+#pragma unroll
+      for (int u = 0; u < NB; ++u) fb[u] = bs[k * WBN + wn + u * 16 + i16];
+    };
+    rd(0, 0);
+    if (NS - 1 < nsteps) issue_p(NS - 1);
+    double sa[2], sb[NB];
+    auto p12 = [&]() {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) sa[u] = fa[u].x + fa[u].y;
+#pragma unroll
+      for (int u = 0; u < NB; ++u) sb[u] = fb[u].x + fb[u].y;
+      if constexpr (AREAL) {
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NB; ++ni)
+            accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mi].x, fb[ni].x, accR[mi][ni], 0, 0, 0);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NB; ++ni)
+            accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mi].x, fb[ni].y, accI[mi][ni], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NB; ++ni)
+            accR[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mi].x, fb[ni].x, accR[mi][ni], 0, 0, 0);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NB; ++ni)
+            accI[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mi].y, fb[ni].y, accI[mi][ni], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto p3 = [&]() {
+      if constexpr (!AREAL) {
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NB; ++ni)
+            acc3[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(sa[mi], sb[ni], acc3[mi][ni], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    for (int s = 0; s < nsteps; ++s) {
+      const int cur = s % NS;
+      p12();
+      rd(cur, 4);
+      __builtin_amdgcn_sched_barrier(0);
+      p3();
+      p12();
+      if (s + 1 < nsteps) {
+        // step s+1 landed (step s+2's pieces may stay in flight) and every wave is done with
+        // step s's slot, which issue_p(s + NS) refills
+        if (s + 2 < nsteps)
+          asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((LPA + LPB) * (NS - 2)) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        rd((s + 1) % NS, 0);
+        if (s + NS < nsteps) issue_p(s + NS);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      p3();
+    }
+  };
+  if (edge)
+    pipeloop(std::integral_constant<int, 2>{});
+  else
+    pipeloop(std::integral_constant<int, 4>{});
+#else
   if (nsteps > 0) {
 #pragma unroll
     for (int st = 0; st < NS - 1; ++st) issue(st);
   }
-  const int i16 = lane & 15, kq = lane >> 4;
   auto mainloop = [&](auto nbc) {
     constexpr int NB = decltype(nbc)::value;  // column blocks per wave (4, or 2 on an edge tile)
     for (int s = 0; s < nsteps; ++s) {
@@ -185,6 +329,7 @@ __global__ __launch_bounds__(256, 2) void zgemm_nn_wide_kernel(
     mainloop(std::integral_constant<int, 2>{});
   else
     mainloop(std::integral_constant<int, 4>{});
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the zero-page pieces in flight
 
   const int nb = edge ? 2 : 4;
@@ -242,8 +387,8 @@ bool wide_gemm_enabled() {
 bool zgemm_wide_applies(int opA, int opB, int M, int N, int K, int batch, int ksplit, int epi,
                         int mode) {
   (void)M;
-  (void)K;
   return opA == OP_N && opB == OP_N && batch == 1 && ksplit <= 1 && epi == EPI_NONE &&
+         K % WBK == 0 &&
          (mode & ~(GEMM_A_REAL | GEMM_A_LOWER)) == 0 && N >= 4 * WBN && wide_gemm_enabled();
 }
 

@@ -10,7 +10,7 @@ make -s
 D=/tmp/fisdf_var_$NAME
 mkdir -p $D
 OBJS=""
-for s in api zgemm fft pchol linalg ao; do
+for s in api zgemm zgemm_wide fft pchol linalg ao; do
   if [[ " $SRCS " == *" $s.hip "* ]]; then
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
       -I../../include -mllvm -amdgpu-mfma-vgpr-form=1 $FL -c $s.hip -o $D/$s.o
