@@ -693,11 +693,16 @@ __global__ void diag_max_kernel(const cplx* __restrict__ A, int n, long sA, doub
 }
 
 // factor + invert the m x m diagonal block at (b0, b0) of W (ld n); writes L_bb (lower) in
-// place and L_bb^{-1} to Linv (64 x 64, batch stride 4096).  Register-blocked: thread t owns
-// the 4 x 4 block (rows 4 (t >> 4), cols 4 (t & 15)) of the block in registers, so a step
-// moves only column k (and row k of the inverse) through LDS — one barrier per step, the
-// column double-buffered by step parity (the LDS-resident version spent ~200 us per block on
-// re-reading the trailing matrix each step).
+// place and L_bb^{-1} to Linv (64 x 64, batch stride 4096; identity on the padding).
+// Register-blocked: thread t owns the 4 x 4 block (rows 4 (t >> 4), cols 4 (t & 15)) of both the
+// trailing matrix A and the inverse X, and one step k does the right-looking Cholesky update and
+// the matching forward-substitution step of X = L^{-1} together: column k of A and row k of X go
+// through LDS (double-buffered by parity, one barrier per step), then every thread updates
+//   A[i][j] -= l_ik conj(l_jk)   (i, j > k)        X[i][:] -= l_ik X[k][:] / l_kk   (i > k)
+// with the masks folded into zeroed operands (no divergent branches in the update).  The
+// round-2 kernel factored first and then inverted by 16 x 16 blocks with exec-masked branches
+// around every element update (89 us per 64-column block at batch 4, the serial chain of the
+// N-rank factorisation).
 __global__ __launch_bounds__(256) void chol_diag_kernel(cplx* __restrict__ W, int n, long sW,
                                                         int b0, int m,
                                                         const double* __restrict__ thr,
@@ -709,30 +714,22 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(cplx* __restrict__ W, in
   // the diagonal blocks are the serial chain of the factorisation, which runs beside the y
   // build's throughput kernels on the same CUs: raise the wave priority so the SIMD arbiter
   // issues this chain's instructions first
-#ifndef FISDF_DIAG_PRIO
-#define FISDF_DIAG_PRIO 3
-#endif
-  __builtin_amdgcn_s_setprio(FISDF_DIAG_PRIO);
-  // inverse phase: L in the lower triangle of Ls, X = L^{-1} (lower) transposed into its upper
-  // triangle — X(i, j), j <= i, at Ls[j][i + 1] — so the block needs one 64 x 65 array
-  __shared__ cplx Ls[64][65];
-  __shared__ cplx Ts[3][16][17];
-  __shared__ cplx vec[2][64];  // column k of the factor / row k of the inverse, by parity
-  __shared__ double dsq[2];
-  __shared__ int bad;
+  __builtin_amdgcn_s_setprio(3);
+  __shared__ cplx colA[2][64];  // column k of A, by step parity
+  __shared__ cplx rowX[2][64];  // row k of X (not yet scaled by 1 / l_kk), by step parity
   const int t = threadIdx.x;
   const int bi = t >> 4, bj = t & 15, r0 = bi * 4, c0 = bj * 4;
-  if (t == 0) bad = 0;
-  cplx a[4][4];
+  cplx a[4][4], x[4][4];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int i = r0 + r, j = c0 + c;
       a[r][c] = (i < m && j <= i) ? W[(long)(b0 + i) * n + b0 + j] : cmk(0, 0);
+      x[r][c] = cmk(i == j ? 1.0 : 0.0, 0.0);
     }
   const double th = thr[b];
-  __syncthreads();
+  bool bad = false;
   // k = 4 kb + kc with kc unrolled: register arrays are indexed with compile-time indices
   // only (a runtime index demotes them to scratch memory)
   for (int kb = 0; 4 * kb < m; ++kb) {
@@ -740,37 +737,44 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(cplx* __restrict__ W, in
     for (int kc = 0; kc < 4; ++kc) {
       const int k = 4 * kb + kc, p = kc & 1;
       if (k >= m) break;
-      if (bj == kb && bi >= kb) {  // owners of column k publish it (rows >= k) and sqrt(A_kk)
+      if (bj == kb) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (r0 + r >= k) vec[p][r0 + r] = a[r][kc];
-          if (r0 + r == k) {
-            const double dk = a[r][kc].x;
-            dsq[p] = sqrt(fmax(dk, 1e-300));
-            if (!(dk > th)) bad = 1;
-          }
-        }
+        for (int r = 0; r < 4; ++r) colA[p][r0 + r] = a[r][kc];
+      }
+      if (bi == kb) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) rowX[p][c0 + c] = x[kc][c];
       }
       __syncthreads();
-      const double lk = dsq[p], inv = 1.0 / lk;
-      cplx li[4], lj[4];
+      const double dk = colA[p][k].x;
+      bad = bad || !(dk > th);
+      const double lk = sqrt(fmax(dk, 1e-300)), inv = 1.0 / lk;
+      cplx li[4], lj[4], xk[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        li[r] = (r0 + r > k && r0 + r < m) ? cscale(vec[p][r0 + r], inv) : cmk(0, 0);
-        lj[r] = (c0 + r > k && c0 + r < m) ? cscale(vec[p][c0 + r], inv) : cmk(0, 0);
+        const cplx vi = colA[p][r0 + r], vj = colA[p][c0 + r], vx = rowX[p][c0 + r];
+        const double si = r0 + r > k ? inv : 0.0, sj = c0 + r > k ? inv : 0.0;
+        li[r] = cscale(vi, si);
+        lj[r] = cscale(vj, sj);
+        xk[r] = cscale(vx, inv);
       }
-      // A[i][j] -= l_ik conj(l_jk),  k < j <= i
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (c0 + c > k && r0 + r >= c0 + c) a[r][c] = csub(a[r][c], cmul(li[r], cconj(lj[c])));
-      if (bj == kb) {  // column k final
+        for (int c = 0; c < 4; ++c) {
+          a[r][c] = csub(a[r][c], cmul(li[r], cconj(lj[c])));
+          x[r][c] = csub(x[r][c], cmul(li[r], xk[c]));
+        }
+      if (bj == kb) {  // column k of L final
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          if (r0 + r > k) a[r][kc] = li[r];
-          else if (r0 + r == k) a[r][kc] = cmk(lk, 0.0);
+          const int i = r0 + r;
+          a[r][kc] = i > k ? li[r] : (i == k ? cmk(lk, 0.0) : a[r][kc]);
         }
+      }
+      if (bi == kb) {  // row k of X final
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x[kc][c] = xk[c];
       }
     }
   }
@@ -779,62 +783,10 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(cplx* __restrict__ W, in
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int i = r0 + r, j = c0 + c;
-      Ls[i][j] = a[r][c];
       if (i < m && j <= i) W[(long)(b0 + i) * n + b0 + j] = a[r][c];
+      Linv[i * 64 + j] = (i < m && j < m) ? (j <= i ? x[r][c] : cmk(0, 0))
+                                          : cmk(i == j ? 1.0 : 0.0, 0.0);
     }
-  __syncthreads();
-  // inverse of the lower-triangular block, 16 x 16 blocked: wave w inverts diagonal block w by
-  // forward substitution (all four in the same 16 barrier steps), then the off-diagonal blocks
-  // by block diagonals, X_ij = -X_ii sum_{k=j}^{i-1} L_ik X_kj (d = i - j = 1, 2, 3: two
-  // barriers each) — 22 barrier steps instead of 64
-  {
-    const int w = t >> 6, lane = t & 63, rr = lane >> 2, cc = (lane & 3) * 4, o = 16 * w;
-    cplx x[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) x[c] = cmk(rr == cc + c ? 1.0 : 0.0, 0.0);
-    for (int k = 0; k < 16; ++k) {
-      if (rr == k) {
-        const double d = o + k < m ? 1.0 / Ls[o + k][o + k].x : 1.0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          x[c] = cscale(x[c], d);
-          if (cc + c <= k) Ls[o + cc + c][o + k + 1] = x[c];
-        }
-      }
-      __syncthreads();
-      if (rr > k) {
-        const cplx l = Ls[o + rr][o + k];
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (cc + c <= k) x[c] = csub(x[c], cmul(l, Ls[o + cc + c][o + k + 1]));
-      }
-    }
-  }
-  {
-    const int r = t >> 4, cidx = t & 15;
-    for (int d = 1; d < 4; ++d) {
-      for (int j = 0; j + d < 4; ++j) {  // T_j = sum_{k=j}^{i-1} L_ik X_kj, i = j + d
-        const int i = j + d;
-        cplx acc = cmk(0, 0);
-        for (int l = 16 * j + cidx; l < 16 * i; ++l)  // X(l, c) = 0 for c > l
-          acc = cadd(acc, cmul(Ls[16 * i + r][l], Ls[16 * j + cidx][l + 1]));
-        Ts[j][r][cidx] = acc;
-      }
-      __syncthreads();
-      for (int j = 0; j + d < 4; ++j) {  // X_ij = -X_ii T_j
-        const int i = j + d;
-        cplx acc = cmk(0, 0);
-        for (int l = 0; l <= r; ++l) acc = cadd(acc, cmul(Ls[16 * i + l][16 * i + r + 1], Ts[j][l][cidx]));
-        Ls[16 * j + cidx][16 * i + r + 1] = cmk(-acc.x, -acc.y);
-      }
-      __syncthreads();
-    }
-  }
-  for (int e = t; e < 4096; e += 256) {
-    const int i = e >> 6, j = e & 63;
-    Linv[e] = (i < m && j < m) ? (j <= i ? Ls[j][i + 1] : cmk(0, 0)) : cmk(i == j ? 1.0 : 0.0, 0.0);
-  }
-  __syncthreads();
   if (t == 0 && bad) fail[b] = 1;
 }
 
