@@ -93,8 +93,10 @@ struct fisdf_ctx {
   int* f_piv = nullptr;     // (nk, nip)
   int* f_rank_dev = nullptr;
   std::vector<int> f_rank;  // host copy
-  // the factorisation runs on a side stream, overlapped with the y build on `stream`
+  // the factorisation runs on a side stream, overlapped with the y build on `stream`, at the
+  // priority fisdf_set_factor_priority asked for (side_hi: the priority it was created with)
   hipStream_t side = nullptr;
+  int factor_hi = 0, side_hi = -1;
   hipEvent_t ev_x4 = nullptr, ev_fac = nullptr, ev_chol = nullptr;
   bool f_fac_unjoined = false;  // ev_fac not yet waited on by the main stream (fit lanes do)
   bool f_pending = false;
@@ -1254,17 +1256,36 @@ int factor_pivoted_slots(fisdf_ctx* c, hipStream_t s, const std::vector<int>& sl
 }
 
 static int ensure_side(fisdf_ctx* c) {
+  // 1-GPU build: the factor chain (small latency-bound kernels) on the device's LEAST priority,
+  // the y build and the fit go first and the chain fills the gaps (at normal priority the factor
+  // ends 2 ms sooner but the C3 step is 5 ms slower).  A k-shard's y build is 1/N as long, so
+  // there the chain is the critical path to the first TRSM and runs at the GREATEST priority
+  // (fisdf_set_factor_priority).  One side stream at a time: an extra stream changes
+  // how HIP maps the context's streams onto the process's hardware queues (4 here), and two
+  // fit lanes sharing a queue serialise (C3 +5 ms/step measured with a second side stream)
+  if (c->side && c->side_hi != c->factor_hi) {
+    FISDF_HIP(hipStreamSynchronize(c->side));
+    FISDF_HIP(hipStreamDestroy(c->side));
+    c->side = nullptr;
+  }
   if (!c->side) {
-    // the factor chain (small latency-bound kernels) on the device's LEAST priority: the y
-    // build and the fit go first, the chain fills the gaps (at normal priority the factor ends
-    // 2 ms sooner but the C3 step is 5 ms slower: r03 A/B)
     int least = 0, greatest = 0;
     FISDF_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    FISDF_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, least));
+    FISDF_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking,
+                                          c->factor_hi ? greatest : least));
+    c->side_hi = c->factor_hi;
+  }
+  if (!c->ev_x4) {
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_x4, hipEventDisableTiming));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_fac, hipEventDisableTiming));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_chol, hipEventDisableTiming));
   }
+  return 0;
+}
+
+int fisdf_set_factor_priority(fisdf_ctx* c, int high) {
+  FISDF_CHECK(c != nullptr && (high == 0 || high == 1), "set_factor_priority: 0 or 1");
+  c->factor_hi = high;
   return 0;
 }
 
@@ -1284,7 +1305,7 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   FISDF_CHECK(nk > 0 && nip > 0, "factor_x4: bad sizes");
   FISDF_TRY(check_qlist(h_qs, nq, 1 << 30, "factor_x4"));
   if (c->f_pending) FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
-  FISDF_TRY(ensure_side(c));
+  if (!c->x4_marked) FISDF_TRY(ensure_side(c));
   const int nb = c->f_nb;
   const int nblk = (nip + nb - 1) / nb;
   const long nn = (long)nip * nip;

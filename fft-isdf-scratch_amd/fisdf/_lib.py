@@ -69,6 +69,7 @@ _SIGS = {
     "fisdf_min_norm_operator": ([_vp, _vp, _i, _d, _vp, _vp, _vp, _ip, _ip], _i),
     "fisdf_min_norm_info": ([_vp, _ip], _i),
     "fisdf_set_fit_lanes": ([_vp, _i], _i),
+    "fisdf_set_factor_priority": ([_vp, _i], _i),
     "fisdf_set_time_reversal": ([_vp, _i], _i),
     "fisdf_set_fit_pipe": ([_vp, _i, _i], _i),
     "fisdf_fit_info": ([_vp, _ip, _ip], _i),

@@ -524,6 +524,9 @@ def build(df_obj):
     d.ctx.call("fisdf_set_half_grid", -1 if df_obj.half_grid is None else int(bool(df_obj.half_grid)))
     # the side stream starts from here (x4 built); the factor chain itself is enqueued after
     # the y build, since it reads ranks back to the host part-way (a blocking copy)
+    sharded = d.sharded(df_obj)
+    # a k-shard's 1/N-grid y build is short, so its factor chain runs at the greatest priority
+    d.ctx.call("fisdf_set_factor_priority", 1 if sharded else 0)
     if nq:
         d.ctx.call("fisdf_factor_x4_mark")
 
@@ -535,7 +538,6 @@ def build(df_obj):
     d.ctx.call("fisdf_set_time_reversal", 1 if df_obj.time_reversal else 0)
     d.ctx.call("fisdf_set_omega", float(getattr(df_obj, "_fit_omega", 0.0)))
     df_obj._omega_dfs = {}                   # range-separated states of an earlier build
-    sharded = d.sharded(df_obj)
     if not sharded:
         yT = d.empty((nq, nip, ngrid))
         d.ctx.call("fisdf_build_y_qs", _lib.ptr(f), ngrid * nao, 0, ngrid, ngrid, _lib.ptr(X),

@@ -203,6 +203,10 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* ctx, const int* h_qs, int nq, const void* d_
  * MFMA-bound TRSM); 0 (default): FISDF_FIT_LANES from the environment, else 2.  Results do
  * not depend on it (same kernels, same per-q arithmetic). */
 int fisdf_set_fit_lanes(fisdf_ctx* ctx, int lanes);
+/* Stream priority of the x4_q factorisation chain (fisdf_factor_x4_async): 0 (default) = the
+ * device's least priority (the 1-GPU build, where the chain hides behind the y build), 1 = the
+ * greatest (a k-shard, whose 1/N-grid y build leaves the chain on the critical path). */
+int fisdf_set_factor_priority(fisdf_ctx* ctx, int high);
 /* Pipelined FFT stream of the fit (with >= 2 lanes): mode -1 = FISDF_FIT_PIPE from the
  * environment (default on), 0 off (the FFT runs in its lane), 1 on; the FFTs run ahead of the
  * lanes into a ring of `depth` Yhat slots (0: FISDF_PIPE_DEPTH or lanes + 2), i.e.
