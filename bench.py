@@ -296,8 +296,9 @@ def main():
     # algorithmic work, 4 r^2 N flop (2 r^2 N for a self-conjugate q, real arithmetic):
     #   trsm: U = L^-1 Yhat, one lower-triangular GEMM (half of the 8 r^2 N of a full GEMM),
     #   herk: G = U U^H (Coulomb-weighted, Hermitian: lower tiles only).
-    # HIP events around each launch on the library's stream; the one with more time is
-    # `roofline`, the other `roofline_secondary`.
+    # Timed by the kernels' own execution span (first workgroup start to last wave end, summed
+    # over the launches of the timed steps); the one with more time is `roofline`,
+    # the other `roofline_secondary`.
     ngrid = int(np.prod(cell.mesh))
     ranks = np.asarray(df.ranks, dtype=np.float64)
     real = np.array([bool(df.real_self_conjugate and df.q_partner[q] == q) for q in df.my_qs])
@@ -316,9 +317,8 @@ def main():
         ncols.append(nh * n1 * n2)
     flop_step = float(np.sum(np.where(real, 2.0, 4.0) * ranks ** 2 * np.asarray(ncols, float)))
     KERNELS = {
-        "trsm": ("zgemm_glds_kernel<0,0,false,4|5,3> (lower-triangular GEMM U = L^-1 Yhat)",
-                 "trsm_gemm"),
-        "herk": ("zgemm_glds_kernel<0,3,true,*,3> (HERK W_q, split-K) + reduce", "herk"),
+        "trsm": ("zgemm_nn_wide_kernel<4|5,3> (lower-triangular GEMM U = L^-1 Yhat)", "trsm_gemm"),
+        "herk": ("zgemm_glds_kernel<0,3,true,0|2,3> (HERK W_q, split-K) + herk_reduce_kernel", "herk"),
     }
     roofs = {}
     for name, (label, _) in KERNELS.items():

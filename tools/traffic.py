@@ -9,12 +9,12 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {  # label: (name substring, grid-size filter on the largest launches)
-    "herk": "zgemm_glds_kernel<0, 3, true, 0, 3>",
-    "trsm_gemm": "zgemm_glds_kernel<0, 0, false, 4, 3>",   # lower-triangular GEMM (GEMM_A_LOWER)
+KERNELS = {  # label: kernel-name substring (the hot launches: the grid carrying the most bytes)
+    "herk": "zgemm_glds_kernel<0, 3, true, 0, 3, true>",    # Coulomb HERK, pipelined 3M loop
+    "trsm_gemm": "zgemm_nn_wide_kernel<4, 3>",             # lower-triangular GEMM U = L^-1 Yhat
     "fft_plane": "fft_plane_reg<36>",
     "fft_axis0": "fft_axis0_reg<36>",
-    "kmesh_y": "kmesh_y_reg_kernel<4, 4, 4>",
+    "y_fused": "y_fused_kernel<4, 4, 4>",
 }
 
 
