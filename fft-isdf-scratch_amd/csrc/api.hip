@@ -2020,7 +2020,7 @@ int fisdf_build_ws_qs(fisdf_ctx* c, const void* Wqv, const int* h_qs, const doub
   FISDF_TRY(check_qlist(h_qs, nq, nk, "build_ws"));
   const long nn = (long)nip * nip;
   if (nq == 0) {
-    FISDF_HIP(hipMemsetAsync(Wsv, 0, sizeof(cplx) * nk * nn, c->stream));
+    FISDF_HIP(hipMemsetAsync(Wsv, 0, sizeof(double) * nk * nn, c->stream));
     return 0;
   }
   // Phi_sel[R, i] = wt_i Phi[R, q_i]  (host; nk x nq)
@@ -2045,9 +2045,9 @@ int fisdf_build_ws_qs(fisdf_ctx* c, const void* Wqv, const int* h_qs, const doub
   FISDF_TRY(arena_get(c, cv.off, &base));
   cplx* dph = (cplx*)((char*)base + oP);
   FISDF_TRY(upload_bytes(c, ph.data(), sizeof(cplx) * ph.size(), dph));
-  // ws = Phi W (:205), real part * sqrt(nk) (:207) in the GEMM's epilogue.  With time-reversal
-  // representatives the partner -q contributes conj(Phi[R,q] W_q), so Re(.) of the pair is
-  // 2 Re(Phi[R,q] W_q): wt = 2.
+  // ws = Phi W (:205), real part * sqrt(nk) (:207) in the GEMM's epilogue, stored real (the
+  // reference keeps W_s = ws.real, a real array).  With time-reversal representatives the
+  // partner -q contributes conj(Phi[R,q] W_q), so Re(.) of the pair is 2 Re(Phi[R,q] W_q): wt = 2.
   FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nn, nq, cmk(std::sqrt((double)nk), 0), dph, nq, 0,
                   (const cplx*)Wqv, nn, 0, ZERO, (cplx*)Wsv, nn, 0, 1, 1, nullptr, EPI_REAL,
                   nullptr));
@@ -2065,7 +2065,7 @@ int fisdf_build_ws_rows(fisdf_ctx* c, const void* Wqv, const int* h_qs, const do
   const long nb = i1 - i0, nn = (long)nip * nip;
   if (nb == 0) return 0;
   if (nq == 0) {
-    FISDF_HIP(hipMemsetAsync(Wsv, 0, sizeof(cplx) * nk * nb * nip, c->stream));
+    FISDF_HIP(hipMemsetAsync(Wsv, 0, sizeof(double) * nk * nb * nip, c->stream));
     return 0;
   }
   CellGeom g;
@@ -2238,7 +2238,7 @@ int fisdf_get_j(fisdf_ctx* c, const void* Xv, const void* W0, const void* dmsv, 
 }
 
 // ---- A8 -----------------------------------------------------------------------
-static int get_k_block(fisdf_ctx* c, const void* Xv, const cplx* Ws_rows, long ws_Rstride,
+static int get_k_block(fisdf_ctx* c, const void* Xv, const double* Ws_rows, long ws_Rstride,
                        const void* dmsv, int nset, int nip, int nao, const int kmesh[3],
                        const double a[9], int i0, int i1, void* vkv);
 
@@ -2248,7 +2248,7 @@ int fisdf_get_k_rows(fisdf_ctx* c, const void* Xv, const void* Wsv, const void* 
   FISDF_TRY(device_guard(c));
   FISDF_CHECK(0 <= i0 && i0 <= i1 && i1 <= nip, "get_k: bad row range");
   // rows i0.. of W_s[R] inside the full (nk, nip, nip) array
-  return get_k_block(c, Xv, (const cplx*)Wsv + (long)i0 * nip, (long)nip * nip, dmsv, nset, nip,
+  return get_k_block(c, Xv, (const double*)Wsv + (long)i0 * nip, (long)nip * nip, dmsv, nset, nip,
                      nao, kmesh, a, i0, i1, vkv);
 }
 
@@ -2258,11 +2258,11 @@ int fisdf_get_k_rows_local(fisdf_ctx* c, const void* Xv, const void* Ws_rows, co
   FISDF_TRY(device_guard(c));
   FISDF_CHECK(0 <= i0 && i0 <= i1 && i1 <= nip, "get_k: bad row range");
   // this rank's rows only: (nk, i1 - i0, nip) from fisdf_build_ws_rows + a reduce-scatter
-  return get_k_block(c, Xv, (const cplx*)Ws_rows, (long)(i1 - i0) * nip, dmsv, nset, nip, nao,
+  return get_k_block(c, Xv, (const double*)Ws_rows, (long)(i1 - i0) * nip, dmsv, nset, nip, nao,
                      kmesh, a, i0, i1, vkv);
 }
 
-static int get_k_block(fisdf_ctx* c, const void* Xv, const cplx* Ws_rows, long ws_Rstride,
+static int get_k_block(fisdf_ctx* c, const void* Xv, const double* Ws_rows, long ws_Rstride,
                        const void* dmsv, int nset, int nip, int nao, const int kmesh[3],
                        const double a[9], int i0, int i1, void* vkv) {
   StageTimer tm(c, FISDF_ST_K);
@@ -2298,7 +2298,7 @@ static int get_k_block(fisdf_ctx* c, const void* Xv, const cplx* Ws_rows, long w
       // Gamma only (Phi = 1): rho_s = Re(rho_k) (:215-216) and V = W_s * rho_s^T (:219) in this
       // GEMM's epilogue; V_k = V_s (:222)
       FISDF_TRY(zgemm(c->stream, OP_N, OP_T, nb, nip, nao, ONE, T, nao, ba, X, nao, xs, ZERO, B1,
-                      nip, bn, 1, 1, (cplx*)Ws_rows, EPI_WSRHO, c->maximag + 2, GEMM_FULL,
+                      nip, bn, 1, 1, (cplx*)(void*)Ws_rows, EPI_WSRHO, c->maximag + 2, GEMM_FULL,
                       (long)nip));
     } else {
       FISDF_TRY(zgemm(c->stream, OP_N, OP_T, nb, nip, nao, ONE, T, nao, ba, X, nao, xs, ZERO, B1,
@@ -2306,7 +2306,7 @@ static int get_k_block(fisdf_ctx* c, const void* Xv, const cplx* Ws_rows, long w
       // rho_s = Phi rho_k (:215), real (:216), and V_s = W_s * rho_s^T (:219) for the block
       // rows, both in the GEMM's epilogue (EPI_WSRHO: Re(W_s) Re(.), max |Im rho_s| recorded)
       FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, bn, nk, ONE, phase, nk, 0, B1, bn, 0, ZERO, B2,
-                      bn, 0, 1, 1, (cplx*)Ws_rows, EPI_WSRHO, c->maximag + 2, GEMM_FULL,
+                      bn, 0, 1, 1, (cplx*)(void*)Ws_rows, EPI_WSRHO, c->maximag + 2, GEMM_FULL,
                       ws_Rstride));
       // V_k = Phi^T V_s (:222)
       FISDF_TRY(zgemm(c->stream, OP_T, OP_N, nk, bn, nk, ONE, phase, nk, 0, B2, bn, 0, ZERO, B1,

@@ -76,8 +76,9 @@ enum Op { OP_N = 0, OP_T = 1, OP_R = 2 /*conj only*/, OP_C = 3 /*conj-transpose*
 // epilogues: EPI_STREAM: C = alpha acc (beta = 0) with non-temporal stores (a large output
 // read back only much later, e.g. the y build's fx blocks)
 // EPI_CSQUARE: C = (alpha acc)^2 elementwise (beta = 0), max |Im(alpha acc)| recorded in *mon
-// EPI_REAL: C = Re(alpha acc) + 0i; EPI_WSRHO: C = Re(aux) Re(alpha acc) + 0i with aux passed
-// as `work` (row stride ldaux); both record max |Im(alpha acc)| in *mon (nullable)
+// EPI_REAL: C = Re(alpha acc) written as REAL doubles (C is a double*, ldc in doubles; batch 1);
+// EPI_WSRHO: C = aux Re(alpha acc) + 0i with aux real (a double* passed as `work`, row stride
+// ldaux doubles); both record max |Im(alpha acc)| in *mon (nullable)
 enum Epi { EPI_NONE = 0, EPI_STREAM = 2, EPI_CSQUARE = 4, EPI_REAL = 5, EPI_WSRHO = 6 };
 // arithmetic modes (MFMA work skipped): GEMM_A_REAL: Im(op(A)) is taken as zero (2 of the 4
 // real MFMAs per complex block); GEMM_RE_ONLY: only Re(C) is formed (Im(C) written as 0).

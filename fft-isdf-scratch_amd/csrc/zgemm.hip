@@ -98,8 +98,11 @@ __device__ __forceinline__ void zgemm_epilogue(int M, int N, cplx alpha, cplx be
     return;
   }
   if (epi == EPI_REAL || epi == EPI_WSRHO) {
-    // EPI_REAL: C = Re(alpha acc) + 0i; EPI_WSRHO: C = Re(aux[row][col]) Re(alpha acc) + 0i
-    // (aux = work, row stride ldaux); both record max |Im(alpha acc)| in *mon
+    // EPI_REAL: C (REAL: double*, row stride ldc doubles; batch 1) = Re(alpha acc);
+    // EPI_WSRHO: C = aux[row][col] Re(alpha acc) + 0i with aux real (double*, row stride
+    // ldaux doubles, passed as work); both record max |Im(alpha acc)| in *mon
+    double* Cd = (double*)(C - (long)bz * sC);
+    const double* auxd = (const double*)work;
     double mx = 0.0;
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -112,8 +115,10 @@ __device__ __forceinline__ void zgemm_epilogue(int M, int N, cplx alpha, cplx be
           if (((mask >> (mi * 2 + ni)) & 1) && row < M && col < N) {
             const cplx v = cmul(alpha, cmk(accR[mi][ni][r], accI[mi][ni][r]));
             mx = fmax(mx, fabs(v.y));
-            const double f = epi == EPI_WSRHO ? work[(long)row * ldaux + col].x : 1.0;
-            C[(long)row * ldc + col] = cmk(f * v.x, 0.0);
+            if (epi == EPI_WSRHO)
+              C[(long)row * ldc + col] = cmk(auxd[(long)row * ldaux + col] * v.x, 0.0);
+            else
+              Cd[(long)row * ldc + col] = v.x;
           }
         }
 #pragma unroll

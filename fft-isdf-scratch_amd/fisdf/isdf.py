@@ -597,21 +597,21 @@ def build(df_obj):
         # its partial sum and the blocks are reduce-scattered (W_s rows stay distributed)
         rows = [kshard.shard_range(nip, r, d.size) for r in range(d.size)]
         chunk = nk * max(b - a for a, b in rows) * nip
-        Wsb = d.empty((chunk * d.size,))
+        Wsb = d.empty((chunk * d.size,), "f64")         # W_s is real (fftisdf.py:207)
         for r, (i0, i1) in enumerate(rows):
             if i1 > i0:
                 d.ctx.call("fisdf_build_ws_rows", _lib.ptr(Wq), qs_c,
                            my_wt.ctypes.data_as(_lib._dp), nq, nip, km_p, a_p, i0, i1,
                            _lib.ptr(Wsb[r * chunk:]))
         i0, i1 = rows[d.rank]
-        Ws = kshard.reduce_scatter_real(Wsb, chunk, nk * (i1 - i0) * nip, d.rank, d.size,
+        Ws = kshard.reduce_scatter_rows(Wsb, chunk, nk * (i1 - i0) * nip, d.rank, d.size,
                                         d.comm).reshape(nk, i1 - i0, nip)
         del Wsb
         owner0 = next(r for r, (a, b) in enumerate(chunks) if b > a)     # fit_qs[0] == 0
         W0 = Wq[0].clone() if d.rank == owner0 else d.empty((nip, nip))
         kshard.broadcast_w0(W0, nk, d.comm, src_local=owner0)           # W_0 for get_j
     else:
-        Ws = d.empty((nk, nip, nip))
+        Ws = d.empty((nk, nip, nip), "f64")              # W_s is real (fftisdf.py:207)
         d.ctx.call("fisdf_build_ws_qs", _lib.ptr(Wq), qs_c, my_wt.ctypes.data_as(_lib._dp), nq,
                    nip, km_p, a_p, _lib.ptr(Ws))                                 # :204-207
         W0 = Wq[0]

@@ -225,27 +225,23 @@ def allreduce_real_part(t, group=None):
     return t
 
 
-def reduce_scatter_real(blocks, chunk: int, nloc: int, rank: int, size: int, group=None):
-    """Sum over ranks of `blocks` (complex, imaginary part zero; rank c's block of the sum at
-    [c*chunk, c*chunk + n_c), chunks padded to one size) and return THIS rank's block, the first
-    `nloc` elements of its chunk, as a complex tensor with zero imaginary part: W_s reduced and
-    scattered by interpolation-point rows (fftisdf.py:204-207; each rank's get_k needs only its
-    rows).  Only the real parts travel: half the bytes of a complex all-reduce, and (size-1)/size
-    of one W_s per rank instead of the all-reduce's 2 (size-1)/size."""
+def reduce_scatter_rows(blocks, chunk: int, nloc: int, rank: int, size: int, group=None):
+    """Sum over ranks of the real `blocks` (rank c's block of the sum at [c*chunk, c*chunk + n_c),
+    chunks padded to one size) and return THIS rank's block, the first `nloc` elements of its
+    chunk: W_s reduced and scattered by interpolation-point rows (fftisdf.py:204-207; W_s is
+    real, and each rank's get_k needs only its rows).  (size-1)/size of one W_s per rank travels,
+    half the bytes of an all-reduce of the same array."""
     import torch
     import torch.distributed as dist
-    re = torch.view_as_real(blocks)[..., 0].contiguous()
     if _emulated(group):
-        mine = re[rank * chunk:rank * chunk + nloc]
-    elif _host_staged(group, re):
-        h = re.cpu()
+        return blocks[rank * chunk:rank * chunk + nloc]
+    if _host_staged(group, blocks):
+        h = blocks.cpu()
         dist.all_reduce(h, group=group)
-        mine = h[rank * chunk:rank * chunk + nloc].to(re.device)
-    else:
-        out = torch.empty(chunk, dtype=re.dtype, device=re.device)
-        dist.reduce_scatter_tensor(out, re[:chunk * size], group=group)
-        mine = out[:nloc]
-    return torch.complex(mine, torch.zeros_like(mine))
+        return h[rank * chunk:rank * chunk + nloc].to(blocks.device)
+    out = torch.empty(chunk, dtype=blocks.dtype, device=blocks.device)
+    dist.reduce_scatter_tensor(out, blocks[:chunk * size], group=group)
+    return out[:nloc]
 
 
 def _host_staged(group, *tensors):

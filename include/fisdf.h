@@ -241,8 +241,8 @@ int fisdf_set_omega(fisdf_ctx* ctx, double omega);
 int fisdf_set_time_reversal(fisdf_ctx* ctx, int on);
 
 /* ---- A8 prep: W_s[R] = sqrt(nk) Re(sum_{q in [q0,q1)} Phi[R,q] W_q) (fftisdf.py:204-207)
- * d_Wq: (q1-q0, nip, nip) shard; d_Ws: (nimg, nip, nip) c128 with zero imaginary part
- * (partial sum for a q-shard; shards are summed with an all-reduce). */
+ * d_Wq: (q1-q0, nip, nip) shard; d_Ws: (nimg, nip, nip) REAL float64 (the reference keeps
+ * W_s = ws.real, :207; a partial sum for a q-shard, summed over the shards). */
 int fisdf_build_ws(fisdf_ctx* ctx, const void* d_Wq, int q0, int q1, int nip,
                    const int kmesh[3], const double a[9], void* d_Ws);
 /* q-list form: W_s[R] = sqrt(nk) Re(sum_i h_wt[i] Phi[R,q_i] W_{q_i}) (h_wt NULL: all 1;
@@ -250,7 +250,7 @@ int fisdf_build_ws(fisdf_ctx* ctx, const void* d_Wq, int q0, int q1, int nip,
 int fisdf_build_ws_qs(fisdf_ctx* ctx, const void* d_Wq, const int* h_qs, const double* h_wt,
                       int nq, int nip, const int kmesh[3], const double a[9], void* d_Ws);
 
-/* Row block [i0, i1) of W_s for a q-list: d_Ws (nk, i1-i0, nip) = rows i0..i1 of every W_s[R] of
+/* Row block [i0, i1) of W_s for a q-list: d_Ws (nk, i1-i0, nip) float64 = rows i0..i1 of every W_s[R] of
  * fisdf_build_ws_qs.  A k-sharded build forms every rank's block of its partial sum and
  * REDUCE-SCATTERS them (each rank then holds the rows its get_k contracts, half the bytes of the
  * all-reduce of the whole W_s).  asynchronous. */
@@ -276,7 +276,8 @@ int fisdf_get_j_rows(fisdf_ctx* ctx, const void* d_X, const void* d_W0, const vo
 int fisdf_get_k_rows(fisdf_ctx* ctx, const void* d_X, const void* d_Ws, const void* d_dms,
                      int nset, int nip, int nao, const int kmesh[3], const double a[9], int i0,
                      int i1, void* d_vk);
-/* the same with only this block's W_s rows at hand: d_Ws_rows (nk, i1-i0, nip) */
+/* the same with only this block's W_s rows at hand: d_Ws_rows (nk, i1-i0, nip) float64.  d_Ws
+ * of fisdf_get_k / fisdf_get_k_rows is the real (nk, nip, nip) array of fisdf_build_ws_qs. */
 int fisdf_get_k_rows_local(fisdf_ctx* ctx, const void* d_X, const void* d_Ws_rows,
                            const void* d_dms, int nset, int nip, int nao, const int kmesh[3],
                            const double a[9], int i0, int i1, void* d_vk);
