@@ -106,6 +106,8 @@ struct fisdf_ctx {
   size_t f_scratch_size = 0;
   // pinned staging of small host arrays copied asynchronously (q-lists)
   int* stage_pinned = nullptr;
+  int* sel_pinned = nullptr;  // selection read-back {error flag, rank, pivots} (pinned)
+  size_t sel_cap = 0;
   size_t stage_cap = 0;
   hipEvent_t ev_stage = nullptr;
   // reality-invariant monitors
@@ -597,6 +599,7 @@ int fisdf_destroy(fisdf_ctx* c) {
   if (c->arena) (void)hipFree(c->arena);
   if (c->ev_stage) (void)hipEventSynchronize(c->ev_stage), (void)hipEventDestroy(c->ev_stage);
   if (c->stage_pinned) (void)hipHostFree(c->stage_pinned);
+  if (c->sel_pinned) (void)hipHostFree(c->sel_pinned);
   if (c->maximag) (void)hipFree(c->maximag);
   if (c->spans) (void)hipFree(c->spans);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -847,6 +850,47 @@ int fisdf_tri_inverse(fisdf_ctx* c, const void* L, int n, int batch, void* Linv)
 }
 
 // ---- A1 ---------------------------------------------------------------------
+// The selection's pivots on the device: the cooperative kernel, the blocked or the generic pivoted
+// Cholesky (in that order of preference), then ONE pinned read-back of {error flag, rank, pivots}
+// and one stream synchronisation (round 2 synchronised twice through pageable copies); a
+// cooperative run that reports a stalled step is redone on the non-cooperative paths.
+static int select_pivots_dev(fisdf_ctx* c, const cplx* X2, double scale, int ng0, int nip_max,
+                             double tol, cplx* X4, int* piv, int* rank, cplx* L, double* d,
+                             int* flags, double* w, int* h_perm, int* h_rank) {
+  const size_t nint = 2 + (size_t)nip_max;
+  if (c->sel_cap < nint) {
+    if (c->sel_pinned) FISDF_HIP(hipHostFree(c->sel_pinned));
+    c->sel_pinned = nullptr;
+    c->sel_cap = 0;
+    FISDF_HIP(hipHostMalloc((void**)&c->sel_pinned, sizeof(int) * nint, hipHostMallocDefault));
+    c->sel_cap = nint;
+  }
+  for (int pass = 0; pass < 2; ++pass) {
+    bool handled = false;
+    const int* coop_err = nullptr;
+    FISDF_TRY(pchol_select_real(c->stream, X2, scale, ng0, nip_max, tol, piv, rank, (double*)X4,
+                                flags, &handled, pass == 0, &coop_err));
+    if (!handled) {
+      FISDF_TRY(square_scale(c->stream, X2, scale, X4, (long)ng0 * ng0));
+      FISDF_TRY(pchol(c->stream, X4, ng0, 0, ng0, 1, nip_max, tol, 0.0, L, piv, rank, d, flags, w));
+    }
+    int* hp = c->sel_pinned;
+    hp[0] = 0;
+    if (coop_err)
+      FISDF_HIP(hipMemcpyAsync(hp, coop_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    FISDF_HIP(hipMemcpyAsync(hp + 1, rank, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    FISDF_HIP(hipMemcpyAsync(hp + 2, piv, sizeof(int) * nip_max, hipMemcpyDeviceToHost, c->stream));
+    FISDF_HIP(hipStreamSynchronize(c->stream));
+    if (hp[0] == 0) {
+      *h_rank = hp[1];
+      std::memcpy(h_perm, hp + 2, sizeof(int) * nip_max);
+      return 0;
+    }
+  }
+  FISDF_CHECK(false, "select: pivoted Cholesky failed on every path");
+  return 0;
+}
+
 int fisdf_select_points(fisdf_ctx* c, const void* x0v, int nk, int ng0, int nao, int nip_max,
                         double tol, int* h_perm, int* h_npiv, int* h_full_rank) {
   FISDF_TRY(device_guard(c));
@@ -874,19 +918,10 @@ int fisdf_select_points(fisdf_ctx* c, const void* x0v, int nk, int ng0, int nao,
   FISDF_TRY(select_gram(c, x0, nk, 0, nk, ng0, nao, X2, (cplx*)(b + oPm)));
   // x4 = Re(x2)^2 / nk (:379) and the greedy pivoted Cholesky (:381-384), first nip_max
   // pivots: real blocked panels (X4's storage holds the real trailing matrix)
-  bool handled = false;
-  FISDF_TRY(pchol_select_real(c->stream, X2, 1.0 / nk, ng0, nip_max, tol, (int*)(b + oP),
-                              (int*)(b + oR), (double*)X4, (int*)(b + oF), &handled));
-  if (!handled) {
-    FISDF_TRY(square_scale(c->stream, X2, 1.0 / nk, X4, (long)ng0 * ng0));
-    FISDF_TRY(pchol(c->stream, X4, ng0, 0, ng0, 1, nip_max, tol, 0.0, (cplx*)(b + oL),
-                    (int*)(b + oP), (int*)(b + oR), (double*)(b + oD), (int*)(b + oF),
-                    (double*)(b + oW)));
-  }
   int rank = 0;
-  FISDF_HIP(hipMemcpyAsync(&rank, b + oR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-  FISDF_HIP(hipMemcpyAsync(h_perm, b + oP, sizeof(int) * nip_max, hipMemcpyDeviceToHost, c->stream));
-  FISDF_HIP(hipStreamSynchronize(c->stream));
+  FISDF_TRY(select_pivots_dev(c, X2, 1.0 / nk, ng0, nip_max, tol, X4, (int*)(b + oP),
+                              (int*)(b + oR), (cplx*)(b + oL), (double*)(b + oD), (int*)(b + oF),
+                              (double*)(b + oW), h_perm, &rank));
   *h_npiv = rank;
   if (h_full_rank) *h_full_rank = rank < nip_max ? 1 : 0;
   return 0;
@@ -924,20 +959,10 @@ int fisdf_select_pivots(fisdf_ctx* c, const void* x2, int nk, int ng0, int nip_m
   FISDF_TRY(arena_get(c, cv.off, &base));
   char* b = (char*)base;
   cplx* X4 = (cplx*)(b + oX4);
-  bool handled = false;  // x4 = Re(x2)^2/nk (:379) + pivoted Cholesky (:381-384)
-  FISDF_TRY(pchol_select_real(c->stream, (const cplx*)x2, 1.0 / nk, ng0, nip_max, tol,
-                              (int*)(b + oP), (int*)(b + oR), (double*)X4, (int*)(b + oF),
-                              &handled));
-  if (!handled) {
-    FISDF_TRY(square_scale(c->stream, (const cplx*)x2, 1.0 / nk, X4, (long)ng0 * ng0));
-    FISDF_TRY(pchol(c->stream, X4, ng0, 0, ng0, 1, nip_max, tol, 0.0, (cplx*)(b + oL),
-                    (int*)(b + oP), (int*)(b + oR), (double*)(b + oD), (int*)(b + oF),
-                    (double*)(b + oW)));
-  }
-  int rank = 0;
-  FISDF_HIP(hipMemcpyAsync(&rank, b + oR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-  FISDF_HIP(hipMemcpyAsync(h_perm, b + oP, sizeof(int) * nip_max, hipMemcpyDeviceToHost, c->stream));
-  FISDF_HIP(hipStreamSynchronize(c->stream));
+  int rank = 0;  // x4 = Re(x2)^2/nk (:379) + pivoted Cholesky (:381-384)
+  FISDF_TRY(select_pivots_dev(c, (const cplx*)x2, 1.0 / nk, ng0, nip_max, tol, X4, (int*)(b + oP),
+                              (int*)(b + oR), (cplx*)(b + oL), (double*)(b + oD), (int*)(b + oF),
+                              (double*)(b + oW), h_perm, &rank));
   *h_npiv = rank;
   if (h_full_rank) *h_full_rank = rank < nip_max ? 1 : 0;
   return 0;
@@ -1019,9 +1044,10 @@ int fisdf_gather_points(fisdf_ctx* c, const void* x0, int nk, int ng0, int nao, 
   void* base;
   FISDF_TRY(arena_get(c, sizeof(int) * (size_t)nip, &base));
   for (int i = 0; i < nip; ++i) FISDF_CHECK(h_perm[i] >= 0 && h_perm[i] < ng0, "perm out of range");
-  FISDF_HIP(hipMemcpyAsync(base, h_perm, sizeof(int) * nip, hipMemcpyHostToDevice, c->stream));
+  // through the pinned staging buffer, stream-ordered (the arena's next user is enqueued after
+  // the gather on the same stream): no host synchronisation
+  FISDF_TRY(upload_ints(c, h_perm, nip, (int*)base));
   FISDF_TRY(gather_points(c->stream, (const cplx*)x0, nk, ng0, nao, (const int*)base, nip, (cplx*)X));
-  FISDF_HIP(hipStreamSynchronize(c->stream));  // h_perm staging is reused
   return 0;
 }
 

@@ -119,10 +119,14 @@ int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int
 // unpivoted blocked Cholesky (full-rank fast path); see pchol.hip
 int chol_unpivoted(hipStream_t s, cplx* W, int n, int batch, double tol_rel, int* piv, int* rank,
                    int* fail, cplx* work);
-// selection pivots from the real Gram Re(X2)^2*scale (blocked, real; n <= 4096): *handled=false
-// otherwise.  work: n*n + 17*n + 1 doubles; piv (rmax), rank (1), flags (1) device.
+// selection pivots from the real Gram Re(X2)^2*scale (cooperative kernel, else blocked, real;
+// n <= 4096): *handled=false otherwise.  work: n*n + 17*n + 1 doubles; piv (rmax), rank (1),
+// flags (1) device.  When the cooperative kernel ran (allow_coop), *coop_err is the device address
+// of its error flag: nonzero after the stream completes = a stalled step, redo with
+// allow_coop = false.
 int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rmax, double tol,
-                      int* piv, int* rank, double* work, int* flags, bool* handled);
+                      int* piv, int* rank, double* work, int* flags, bool* handled,
+                      bool allow_coop, const int** coop_err);
 
 // Where plane i0 of input row r lives when the rows arrive in grid slices (the all-to-all
 // pieces of a k-sharded build): in + base + r * ld, one entry per plane (device table)

@@ -891,11 +891,14 @@ bool select_coop_enabled() {
 }
 
 // launches pchol_select_coop when the owned L rows fit the LDS of a co-resident grid;
-// *handled = false (nothing enqueued that matters) otherwise or if the launch is refused.
-// The cooperative launch synchronises the stream to read the barrier error flag.
+// *handled = false (nothing enqueued that matters) otherwise or if the launch is refused.  No
+// host synchronisation: *err_dev receives the device address of the kernel's error flag (a
+// stalled step), which the caller reads back with the pivots and the rank in one copy.
 int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n, int rmax,
-                             double tol, int* piv, int* rank, double* work, bool* handled) {
+                             double tol, int* piv, int* rank, double* work, bool* handled,
+                             const int** err_dev) {
   *handled = false;
+  *err_dev = nullptr;
   if (!select_coop_enabled() || n < 64) return 0;
   static const int ncu = [] {
     int dev = 0, v = 0;
@@ -952,19 +955,22 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
     (void)hipGetLastError();
     return 0;
   }
-  int h_err = 0;
-  FISDF_HIP(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, s));
-  FISDF_HIP(hipStreamSynchronize(s));
-  *handled = h_err == 0;
+  *err_dev = err;
+  *handled = true;
   return 0;
 }
 
 int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rmax, double tol,
-                      int* piv, int* rank, double* work, int* flags, bool* handled) {
+                      int* piv, int* rank, double* work, int* flags, bool* handled,
+                      bool allow_coop, const int** coop_err) {
   *handled = false;
+  *coop_err = nullptr;
   if (rmax <= 0) return 0;
-  FISDF_TRY(pchol_select_coop_launch(s, X2, scale, n, rmax, tol, piv, rank, work, handled));
-  if (*handled) return 0;
+  if (allow_coop) {
+    FISDF_TRY(pchol_select_coop_launch(s, X2, scale, n, rmax, tol, piv, rank, work, handled,
+                                       coop_err));
+    if (*handled) return 0;
+  }
   if (n > 8 * PR_THREADS) return 0;
   double* W = work;
   double* Lpan = W + (long)n * n;

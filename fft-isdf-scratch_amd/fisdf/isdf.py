@@ -308,8 +308,12 @@ class InterpolativeSeparableDensityFitting:
             vk = _get_k_dev(self, ddms, exxdiv, band)
         if with_j:
             vj = _get_j_dev(self, ddms, band)
+        if vk is not None and vj is not None and vk.shape == vj.shape:
+            # one device-to-host copy (and one synchronisation) for both
+            vk, vj = self.device.torch.stack((vk, vj)).cpu().numpy()
         if vk is not None:
-            vk = _format_band(vk.cpu().numpy(), dm, kpts_band, kpts)
+            vk = _format_band(vk if isinstance(vk, np.ndarray) else vk.cpu().numpy(), dm,
+                              kpts_band, kpts)
         if vj is not None:
             vj = _finish_j(vj, dm, kpts, kpts_band)
         return vj, vk
@@ -712,7 +716,7 @@ def _get_j_dev(df_obj, ddms, band=None):
 
 
 def _finish_j(vj, dm_kpts, kpts, kpts_band):
-    out = vj.cpu().numpy()
+    out = vj if isinstance(vj, np.ndarray) else vj.cpu().numpy()
     band = np.asarray(kpts if kpts_band is None else kpts_band)
     if abs(band).max() < 1e-9:                                           # :169-170
         out = out.real

@@ -78,10 +78,15 @@ def test_zgemm_shapes_splitk(env, M, N, K, ks):
 
 
 @pytest.mark.parametrize("n,K,ks", [(1, 7, 1), (16, 40, 1), (24, 37, 1), (40, 100, 2),
-                                    (64, 64, 1), (88, 300, 4), (100, 33, 1), (600, 700, 3)])
+                                    (64, 64, 1), (88, 300, 4), (100, 33, 1), (600, 700, 3),
+                                    # the 64 x 128 split-K kernel (n >= 128, K % 8 == 0, ks > 1):
+                                    # partial tile rows / panels, dead waves above the diagonal
+                                    (128, 64, 2), (130, 96, 2), (200, 256, 5), (333, 1000, 4),
+                                    (600, 704, 3), (640, 1024, 8)])
 def test_herk_shapes(env, n, K, ks):
     """C = A A^H through the lower-tile HERK (diagonal tiles split 3+3+2+2 over the waves,
-    edge tiles by 16-blocks), compared with NumPy on the full matrix (both triangles)."""
+    edge tiles by 16-blocks; the wide split-K kernel where it applies), compared with NumPy on
+    the full matrix (both triangles)."""
     torch, L, ctx = env
     rng = np.random.default_rng(n * 1000 + K)
     A = rnd(rng, n, K)
