@@ -8,8 +8,10 @@ are evaluated once on the host and are resident in HBM before the timed region.
 
   python bench.py [--gpus N --steps K --warmup W] [--config c3|c2|c1] [--no-cpu-baseline]
 
-For N > 1 launch with torch.distributed.run; k-points are sharded over ranks (RCCL
-all-reduce of W_s + broadcast of W_0), rank 0 prints one JSON line.
+For N > 1 launch with torch.distributed.run; the fitted q are sharded over ranks (RCCL
+all-to-all of y pieces, reduce-scatter of W_s rows, broadcast of W_0), rank 0 prints one
+JSON line.  FISDF_BENCH_BACKEND=gloo (rehearsal only: ranks may share one GPU, collectives
+staged through the host) replaces RCCL.
 """
 import argparse
 import json
@@ -245,11 +247,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    backend = os.environ.get("FISDF_BENCH_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        raise SystemExit(f"FISDF_BENCH_BACKEND must be nccl or gloo, not {backend!r}")
+    # one GPU per rank; a gloo rehearsal may place several ranks on one GPU
+    dev = local if backend == "nccl" else local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev)
     comm = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
         comm = dist.group.WORLD
 
     from fisdf import ISDF
@@ -286,7 +296,7 @@ def main():
     stages = d.ctx.timings()
     d.ctx.call("fisdf_set_timing", 0)
     if comm is not None:
-        tt = torch.tensor([dt], dtype=torch.float64, device=d.dev)
+        tt = torch.tensor([dt], dtype=torch.float64, device=d.dev if backend == "nccl" else "cpu")
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         dt = float(tt.item())
     ms_per_step = dt / args.steps * 1e3
@@ -407,7 +417,8 @@ def main():
             "dtype": "f64 (complex128)", "data": "synthetic (gth-dzvp-shaped contracted Gaussians)",
             "config": {"workload": DESC[args.config], "nk": nk, "nao": cell.nao_nr(),
                        "nip": int(df.nip), "ngrid": ngrid, "fit": "lstsq (Cholesky, factored order; min-norm on rank-deficient q)",
-                       "parallelism": f"k-shard x{world}"},
+                       "parallelism": f"k-shard x{world}"
+                       + (" (gloo rehearsal, not RCCL)" if world > 1 and backend == "gloo" else "")},
             "roofline": roof,
             "roofline_secondary": roof2,
             "step_mfma": {"flop_per_step": step_flop, "fit_flop_per_step": 2 * flop_step,
