@@ -480,11 +480,21 @@ int num_cus(int device) {
   return n;
 }
 
+// The fit's extra streams: aux[0] and aux[1] are MFMA lanes, aux[2] the pipelined FFT stream at
+// the device's LEAST priority, so the CU slots it leaves free go to the lanes first (C3 -0.45
+// ms/step over 4 interleaved pairs, profiles/r03_ab/gemm_pipe.log).  All three are created
+// together and in this order: HIP maps a process's streams onto hardware queues by creation
+// order, and leaving aux[1] uncreated when unused measured +4.5 ms/step (even with 8 queues).
 int ensure_aux(fisdf_ctx* c) {
   if (c->ev_fork) return 0;
   FISDF_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+  int least = 0, greatest = 0;
+  FISDF_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
   for (int l = 0; l < 3; ++l) {
-    FISDF_HIP(hipStreamCreateWithFlags(&c->aux[l], hipStreamNonBlocking));
+    if (l == 2)
+      FISDF_HIP(hipStreamCreateWithPriority(&c->aux[l], hipStreamNonBlocking, least));
+    else
+      FISDF_HIP(hipStreamCreateWithFlags(&c->aux[l], hipStreamNonBlocking));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_join[l], hipEventDisableTiming));
   }
   for (int l = 0; l < 4; ++l) FISDF_HIP(hipEventCreateWithFlags(&c->ev_ybuf[l], hipEventDisableTiming));
@@ -586,8 +596,11 @@ int fisdf_destroy(fisdf_ctx* c) {
   if (c->ev_fork) {
     (void)hipEventDestroy(c->ev_fork);
     for (int l = 0; l < 3; ++l) {
-      (void)hipStreamSynchronize(c->aux[l]);
-      (void)hipStreamDestroy(c->aux[l]);
+      if (c->aux[l]) {
+        (void)hipStreamSynchronize(c->aux[l]);
+        (void)hipStreamDestroy(c->aux[l]);
+        c->aux[l] = nullptr;
+      }
       (void)hipEventDestroy(c->ev_join[l]);
     }
     for (int l = 0; l < 4; ++l) (void)hipEventDestroy(c->ev_ybuf[l]);
