@@ -743,8 +743,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (I >= nip || g >= m) return;
   cplx* out = yT + (long)I * Is + goff + g;
   auto put = [&](int q, cplx v) {
-    if ((qmask >> q) & 1ull)
-      out[(long)__popcll(qmask & ((1ull << q) - 1ull)) * qs] = cmk(v.x * sc, v.y * sc);
+    if ((qmask >> q) & 1ull) {
+      // non-temporal: y (GBs, read back by the fit's FFTs much later) streams past L2, so the
+      // X / f operand lines of the MFMA phase stay cached (y -0.22 ms, the factor beside it
+      // -0.4 ms at C3, profiles/r03_ab/gemm_pipe.log)
+      typedef double dv2 __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(dv2{v.x * sc, v.y * sc},
+                                  (dv2*)(out + (long)__popcll(qmask & ((1ull << q) - 1ull)) * qs));
+    }
   };
 #pragma unroll
   for (int pi = 0; pi < NR; ++pi) {
