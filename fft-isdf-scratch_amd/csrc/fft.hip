@@ -16,6 +16,9 @@
 
 #include "common.h"
 
+typedef double fft_dv2 __attribute__((ext_vector_type(2)));
+
+
 #include <map>
 #include <mutex>
 #include <vector>
@@ -462,7 +465,12 @@ __global__ __launch_bounds__(256) void fft_axis0_reg(const cplx* in, long in_ld,
     for (int p = 0; p < N0; ++p) x[p] = cscale(x[p], weight[(long)p * P + l]);
   }
 #pragma unroll
-  for (int p = 0; p < N0; ++p) dst[(long)p * P] = x[p];
+  // the final pass's output (Yhat, 0.45 GB per q at C3, read by the fit's triangular GEMM once its
+  // lane gets there) is stored non-temporally: it streams past the L2s the MFMA lanes' operands
+  // live in (C3 -1.1 ms/step; the first pass's output, re-read at once, keeps plain stores:
+  // profiles/r03_ab/gemm_pipe.log)
+  for (int p = 0; p < N0; ++p)
+    __builtin_nontemporal_store(fft_dv2{x[p].x, x[p].y}, (fft_dv2*)(dst + (long)p * P));
 }
 
 // meshes with register kernels (cubic n^3 for the plane kernel; any n0 for axis 0)
