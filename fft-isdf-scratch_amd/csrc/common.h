@@ -96,7 +96,8 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha,
 
 // the 64 x 128-tile kernel for big single NN products (zgemm_wide.hip); zgemm() routes there
 bool wide_gemm_enabled();
-bool zgemm_wide_applies(int opA, int opB, int M, int N, int K, int batch, int ksplit, int epi,
+bool zgemm_wide_applies(int opA, int opB, int M, int N, int K, long lda, long ldb, int batch,
+                        int ksplit, int epi,
                         int mode);
 int zgemm_nn_wide(hipStream_t s, int M, int N, int K, cplx alpha, const cplx* A, long lda,
                   const cplx* B, long ldb, cplx beta, cplx* C, long ldc, int mode,

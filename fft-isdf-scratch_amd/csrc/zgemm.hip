@@ -710,7 +710,7 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
   if (M == 0 || N == 0 || batch == 0) return 0;
   if (ksplit < 1) ksplit = 1;
   if (epi != EPI_NONE) ksplit = 1;
-  if (zgemm_wide_applies(opA, opB, M, N, K, batch, ksplit, epi, mode)) {
+  if (zgemm_wide_applies(opA, opB, M, N, K, lda, ldb, batch, ksplit, epi, mode)) {
     const CallEvents ev;
     return zgemm_nn_wide(s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, mode, ev.span);
   }

@@ -384,11 +384,16 @@ bool wide_gemm_enabled() {
   return on;
 }
 
-bool zgemm_wide_applies(int opA, int opB, int M, int N, int K, int batch, int ksplit, int epi,
+bool zgemm_wide_applies(int opA, int opB, int M, int N, int K, long lda, long ldb, int batch,
+                        int ksplit, int epi,
                         int mode) {
-  (void)M;
+  // the pipelined loop addresses each lane's operand piece by a 32-bit byte offset from a
+  // wave-uniform base: A's last row up to column K, B's first WBK rows
+  const long lim = 1L << 32;
+  const bool off32 = ((long)std::max(M - 1, 0) * lda + K) * 16 < lim &&
+                     ((long)WBK * ldb + N) * 16 < lim;
   return opA == OP_N && opB == OP_N && batch == 1 && ksplit <= 1 && epi == EPI_NONE &&
-         K % WBK == 0 &&
+         K % WBK == 0 && off32 &&
          (mode & ~(GEMM_A_REAL | GEMM_A_LOWER)) == 0 && N >= 4 * WBN && wide_gemm_enabled();
 }
 

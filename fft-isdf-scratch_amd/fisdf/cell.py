@@ -321,10 +321,14 @@ def eval_ao_kpts(cell, coords, kmesh, folded=None):
 # --------------------------------------------------------------------------
 # the benchmark / test cells
 # --------------------------------------------------------------------------
-def diamond_cell(basis="gth-dzvp", mesh=(36, 36, 36)):
-    """Reference's diamond cell literal (fftdf-with-k-svd.py:189-191), Angstrom -> bohr."""
+def diamond_cell(basis="gth-dzvp", mesh=(36, 36, 36), shift=None):
+    """Reference's diamond cell literal (fftdf-with-k-svd.py:189-191), Angstrom -> bohr.
+    shift (Angstrom, 3-vector): displacement of the second C off 0.8917 (1,1,1), which breaks the
+    cell's point symmetry (no symmetry-equivalent parent-grid points, hence no exactly tied
+    pivots in the selection)."""
     a = (np.ones((3, 3)) * 3.5668 - np.eye(3) * 3.5668) / BOHR
-    atoms = [("C", np.zeros(3)), ("C", np.full(3, 0.8917) / BOHR)]
+    c2 = np.full(3, 0.8917) + (0.0 if shift is None else np.asarray(shift, float))
+    atoms = [("C", np.zeros(3)), ("C", c2 / BOHR)]
     return Cell(a=a, atoms=atoms, basis=basis, mesh=mesh)
 
 

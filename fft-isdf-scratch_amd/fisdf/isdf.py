@@ -609,7 +609,7 @@ def build(df_obj):
                            _lib.ptr(Wsb[r * chunk:]))
         i0, i1 = rows[d.rank]
         Ws = kshard.reduce_scatter_rows(Wsb, chunk, nk * (i1 - i0) * nip, d.rank, d.size,
-                                        d.comm).reshape(nk, i1 - i0, nip)
+                                        d.comm, rows=(i0, i1)).reshape(nk, i1 - i0, nip)
         del Wsb
         owner0 = next(r for r, (a, b) in enumerate(chunks) if b > a)     # fit_qs[0] == 0
         W0 = Wq[0].clone() if d.rank == owner0 else d.empty((nip, nip))

@@ -29,11 +29,22 @@ class EmulatedGroup:
     handed over pre-filled (`pieces[j]`, the rank's j-th q on the whole grid in the concat-of-
     slices layout; taken from a full 1-GPU y so the fit sees real data), the all-reduces keep
     their local copies but add nothing, the broadcast is skipped.  Timing only: the results of
-    an emulated rank are its partial sums."""
+    an emulated rank are its partial sums.
 
-    def __init__(self, rank: int, size: int, pieces=None):
+    For parity tests the other collectives can be handed over too: `w0` (the W_0 the broadcast
+    delivers), `ws_src` ((nk, nip, nip) float64, the reduced W_s whose row block the reduce-
+    scatter delivers) — then the rank's get_jk rows are exact and sum over the ranks to the full
+    J/K — and `keep_ws` records the rank's reduce-scatter input (its partial W_s row blocks of
+    every rank) in `ws_blocks`."""
+
+    def __init__(self, rank: int, size: int, pieces=None, w0=None, ws_src=None,
+                 keep_ws: bool = False):
         self.rank, self.size = int(rank), int(size)
         self.pieces = pieces
+        self.w0 = w0
+        self.ws_src = ws_src
+        self.keep_ws = keep_ws
+        self.ws_blocks = None
 
 
 def emulated_pieces(yall, chunks, slices, rank: int):
@@ -225,15 +236,22 @@ def allreduce_real_part(t, group=None):
     return t
 
 
-def reduce_scatter_rows(blocks, chunk: int, nloc: int, rank: int, size: int, group=None):
+def reduce_scatter_rows(blocks, chunk: int, nloc: int, rank: int, size: int, group=None,
+                        rows=None):
     """Sum over ranks of the real `blocks` (rank c's block of the sum at [c*chunk, c*chunk + n_c),
     chunks padded to one size) and return THIS rank's block, the first `nloc` elements of its
     chunk: W_s reduced and scattered by interpolation-point rows (fftisdf.py:204-207; W_s is
     real, and each rank's get_k needs only its rows).  (size-1)/size of one W_s per rank travels,
-    half the bytes of an all-reduce of the same array."""
+    half the bytes of an all-reduce of the same array.  rows = (i0, i1): this rank's
+    interpolation-point rows (used by an EmulatedGroup that hands the reduced W_s over)."""
     import torch
     import torch.distributed as dist
     if _emulated(group):
+        if group.keep_ws:
+            group.ws_blocks = blocks.clone()
+        if group.ws_src is not None:
+            i0, i1 = rows
+            return group.ws_src[:, i0:i1].contiguous().reshape(-1)
         return blocks[rank * chunk:rank * chunk + nloc]
     if _host_staged(group, blocks):
         h = blocks.cpu()
@@ -271,6 +289,8 @@ def broadcast_w0(w0, nk: int, group=None, src_local=None):
     import torch
     import torch.distributed as dist
     if _emulated(group):
+        if group.w0 is not None and group.rank != src_local:   # the owner keeps its own W_0
+            w0.copy_(group.w0)
         return w0
     size = dist.get_world_size(group)
     if src_local is None:

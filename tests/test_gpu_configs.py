@@ -221,3 +221,69 @@ def test_min_norm_fit_full_size_rank_regime():
           f"|dJ| {band_j:.2e} |dK| {band_k:.2e} (margins {2 * band_j / ej:.1f}x / "
           f"{2 * band_k / ek:.1f}x; oracle {time.perf_counter() - t0:.1f} s)", flush=True)
     assert ej <= 2 * band_j and ek <= 2 * band_k
+
+
+# C2 / C3 with the second C moved off its symmetric site (Angstrom): no symmetry maps the parent
+# grid onto itself, so the parent-grid Gram has no exactly tied diagonal entries
+# (this shift's smallest gap between the two largest residual diagonals along dpstrf's order,
+# relative to max diag: C2 3.7e-9, C3 2.3e-11, against rounding at ~1e-13)
+DISPLACED = {"c2d": ("c2", (0.11, -0.023, 0.067)), "c3d": ("c3", (0.11, -0.023, 0.067))}
+
+
+def _displaced_inputs(name):
+    import bench
+    from fisdf import cell as C
+    cfg, shift = DISPLACED[name]
+    kind, basis, mesh, kmesh, m0, nip = bench.CONFIGS[cfg]
+    cell = C.diamond_cell(basis=basis, mesh=mesh, shift=shift)
+    nao = cell.nao_nr()
+    c0 = (nip + 0.5) / nao
+    x0 = C.eval_ao_kpts(cell, cell.gen_uniform_grids(m0), kmesh)
+    chi = C.eval_ao_kpts(cell, cell.gen_uniform_grids(mesh), kmesh)
+    dm = C.make_dm(nao, kmesh, cell, seed=1234)
+    return cell, kmesh, m0, c0, x0, chi, dm
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name", ["c2d", "c3d"])
+def test_end_to_end_own_selection(name):
+    """North star without injected points (VERDICT r03 ask 3): the GPU build with ITS OWN
+    selection against the reference's whole CPU path with ITS OWN selection (LAPACK dpstrf,
+    fftisdf.py:357-388, then :22-228 with gelsy) on a cell without exact pivot ties.  Asserted:
+    identical pivots, then |dJ|, |dK| < 1e-8 Ha.  Should the greedy orders part anyway, the
+    residual-diagonal gap at the first divergence is printed and must be a rounding-level tie
+    (test_gpu_selection.py's certificate); J/K are then compared on the GPU's points."""
+    from fisdf import ISDF
+    from oracle import isdf_ref as R
+    from test_gpu_selection import residual_along
+    cell, kmesh, m0, c0, x0, chi, dm = _displaced_inputs(name)
+    nao = cell.nao_nr()
+    df = ISDF(cell, cell.get_kpts(kmesh), m0=list(m0), c0=c0)
+    d = df.device
+    df._kmesh()
+    df._ao_parent = d.to_dev(x0)
+    df._ao_grid = d.to_dev(chi)
+    df.build()
+    vj, vk = df.get_jk(dm)
+    t0 = time.perf_counter()
+    perm_ref, rank_ref, nip_ref, x4 = R.select_interpolation_points(x0, nao, c0)
+    assert len(df.perm) == nip_ref
+    same = df.perm == perm_ref
+    first = int(np.argmin(same)) if not same.all() else nip_ref
+    msg = f"\n{name}: nip {nip_ref}, GPU and dpstrf pivots identical for {first}/{nip_ref} steps"
+    perm_jk = perm_ref
+    if first < nip_ref:
+        tie_tol = x4.shape[0] * np.finfo(float).eps * np.diag(x4).max()
+        before, _ = residual_along(x4, df.perm)
+        dp = before[first]
+        gap = dp.max() - dp[df.perm[first]]
+        msg += f"; first divergence: residual gap {gap:.2e} (tie tolerance {tie_tol:.2e})"
+        print(msg, flush=True)
+        assert gap <= tie_tol, msg
+        perm_jk = df.perm
+    vj0, vk0, _ = _oracle_jk(cell, kmesh, x0, chi, dm, perm_jk)
+    dj, dk = abs(vj - vj0).max(), abs(vk - vk0).max()
+    print(f"{msg}; GPU vs reference path end to end: |dJ| {dj:.2e} |dK| {dk:.2e} Ha "
+          f"(max|J| {abs(vj0).max():.3f}, max|K| {abs(vk0).max():.3f}; oracle "
+          f"{time.perf_counter() - t0:.1f} s)", flush=True)
+    assert dj < JK_TOL and dk < JK_TOL

@@ -316,15 +316,18 @@ def test_tri_inverse_batch_invariant(env, n):
         assert rel < 1e-12, rel
 
 
-@pytest.mark.parametrize("M,N,K,mode", [(600, 1000, 600, 0), (600, 1000, 600, 4), (600, 777, 600, 5),
-                                        (600, 600, 600, 1), (24, 700, 50, 0), (100, 2000, 33, 0),
-                                        (1, 512, 8, 0), (129, 513, 17, 4), (64, 4096, 64, 5),
-                                        (600, 24624, 600, 5)])
-def test_zgemm_modes_wide(env, M, N, K, mode):
+@pytest.mark.parametrize("M,N,K,mode,beta", [
+    (600, 1000, 600, 0, 0), (600, 1000, 600, 4, 0), (600, 777, 600, 5, 0), (600, 600, 600, 1, 0),
+    (24, 700, 50, 0, 0), (100, 2000, 33, 0, 0), (1, 512, 8, 0, 0), (129, 513, 17, 4, 0),
+    (64, 4096, 64, 5, 0), (600, 24624, 600, 5, 0),
+    # beta != 0: the read-modify-write epilogue (trsm_blocked's trailing update B -= L X runs
+    # through this kernel with beta = 1, FULL or A_REAL)
+    (64, 1024, 128, 0, 1), (100, 777, 64, 1, 1), (33, 2048, 40, 0, 2), (600, 600, 200, 1, 2)])
+def test_zgemm_modes_wide(env, M, N, K, mode, beta):
     """NN products through fisdf_zgemm_mode: N >= 512 takes the 64 x 128-tile kernel
     (zgemm_wide.hip) — FULL (3 MFMAs per complex block), A_REAL (Im A ignored), A_LOWER (K loop
-    cut at each M-tile's last row) and both, M-edge tiles with <= 32 rows, ragged N — against
-    numpy on the matrices the mode describes."""
+    cut at each M-tile's last row) and both, M-edge tiles with <= 32 rows, ragged N, beta = 0, 1
+    or complex with a nonzero C — against numpy on the matrices the mode describes."""
     torch, L, ctx = env
     rng = np.random.default_rng(M * 7 + N + K + mode)
     A, B = rnd(rng, M, K), rnd(rng, K, N)
@@ -338,10 +341,12 @@ def test_zgemm_modes_wide(env, M, N, K, mode):
         beyond = np.arange(K)[None, :] >= 64 * (np.arange(M)[:, None] // 64 + 1)
         A = np.tril(A) + np.where(beyond, rnd(rng, M, K) * 1e3, 0)
     dA, dB = dev(torch, A), dev(torch, B)
-    dC = torch.zeros((M, N), dtype=torch.complex128, device="cuda")
-    one, zero = np.array([1.0, 0.0]), np.array([0.0, 0.0])
+    C0 = rnd(rng, M, N) if beta else np.zeros((M, N), complex)
+    dC = dev(torch, C0)
+    bv = {0: 0.0, 1: 1.0, 2: -0.5 + 0.25j}[beta]
+    one, vb = np.array([1.0, 0.0]), np.array([bv.real, bv.imag]) if beta else np.zeros(2)
     ctx.call("fisdf_zgemm_mode", 0, 0, M, N, K, one.ctypes.data_as(L._dp), L.ptr(dA), K, 0,
-             L.ptr(dB), N, 0, zero.ctypes.data_as(L._dp), L.ptr(dC), N, 0, 1, mode)
-    ref = Aeff @ B
+             L.ptr(dB), N, 0, vb.ctypes.data_as(L._dp), L.ptr(dC), N, 0, 1, mode)
+    ref = Aeff @ B + (bv * C0 if beta else 0)
     err = abs(dC.cpu().numpy() - ref).max()
     assert err < 1e-12 * max(K, 16), err
