@@ -17,7 +17,14 @@
 namespace fisdf {
 
 static thread_local std::string g_last_error;
-void set_error(const std::string& msg) { g_last_error = msg; }
+// the context the calling thread is working on (set by the entry points' guards): a failure is
+// recorded in it too, so fisdf_last_error(ctx) reports that context's own last failure
+static thread_local fisdf_ctx* t_cur_ctx = nullptr;
+void set_ctx_error(fisdf_ctx* c, const std::string& msg);
+void set_error(const std::string& msg) {
+  g_last_error = msg;
+  if (t_cur_ctx) set_ctx_error(t_cur_ctx, msg);
+}
 
 LaunchEvents& launch_events() {
   static thread_local LaunchEvents ev;
@@ -121,7 +128,29 @@ struct fisdf_ctx {
   unsigned long long* spans = nullptr;
   int span_used = 0;
   static constexpr int kSpanCap = 16384;
+  std::string last_error;  // fisdf_last_error(ctx)
+  // fisdf_build: the resident result of the last composite build (W_q, W_s, X, ... on the device)
+  struct Build {
+    bool valid = false;
+    int nk = 0, nip = 0, nao = 0, ng0 = 0, nfit = 0, used_pivoted = 0, min_norm = 0;
+    int kmesh[3] = {0, 0, 0}, mesh[3] = {0, 0, 0};
+    double a[9] = {0};
+    std::vector<int> perm, fit_qs, partner, ranks;
+    std::vector<double> wt;
+    void *X = nullptr, *x4 = nullptr, *Wq = nullptr, *Ws = nullptr;
+  } bld;
+  // fisdf_set_allocator: device memory of the composite build's buffers from the caller (e.g. a
+  // framework's caching allocator), else library-owned grow-only buffers
+  fisdf_alloc_fn alloc_fn = nullptr;
+  fisdf_free_fn free_fn = nullptr;
+  void* alloc_user = nullptr;
+  std::map<int, std::pair<void*, size_t>> owned;  // role -> library-owned buffer
+  std::vector<void*> lent;                        // buffers from alloc_fn not yet returned
 };
+
+namespace fisdf {
+void set_ctx_error(fisdf_ctx* c, const std::string& msg) { c->last_error = msg; }
+}  // namespace fisdf
 
 namespace {
 
@@ -280,8 +309,16 @@ int get_phase(fisdf_ctx* c, const int kmesh[3], const double a[9], const cplx** 
 }
 
 int device_guard(fisdf_ctx* c) {
+  t_cur_ctx = c;
   FISDF_CHECK(c != nullptr, "null context");
   FISDF_HIP(hipSetDevice(c->device));
+  return 0;
+}
+
+// the entry points that touch no device state: failures still go to the context's own message
+int ctx_guard(fisdf_ctx* c) {
+  t_cur_ctx = c;
+  FISDF_CHECK(c != nullptr, "null context");
   return 0;
 }
 
@@ -553,7 +590,9 @@ extern "C" {
 
 int fisdf_abi_version(void) { return FISDF_ABI_VERSION; }
 
-const char* fisdf_last_error(void) { return g_last_error.c_str(); }
+const char* fisdf_last_error(const fisdf_ctx* c) {
+  return c ? c->last_error.c_str() : g_last_error.c_str();
+}
 
 int fisdf_create(int device, void* stream, fisdf_ctx** out) {
   FISDF_CHECK(out != nullptr, "out is null");
@@ -574,8 +613,14 @@ int fisdf_create(int device, void* stream, fisdf_ctx** out) {
 
 int fisdf_destroy(fisdf_ctx* c) {
   if (!c) return 0;
+  if (t_cur_ctx == c) t_cur_ctx = nullptr;
   FISDF_HIP(hipSetDevice(c->device));
   FISDF_HIP(hipStreamSynchronize(c->stream));
+  // buffers lent by the caller's allocator stay the caller's (fisdf_set_allocator)
+  c->lent.clear();
+  for (auto& kv : c->owned)
+    if (kv.second.first) (void)hipFree(kv.second.first);
+  c->owned.clear();
   for (auto& e : c->events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto& kv : c->phase_cache) (void)hipFree(kv.second);
   for (auto& kv : c->asym_cache) {
@@ -1323,6 +1368,7 @@ static int ensure_side(fisdf_ctx* c) {
 }
 
 int fisdf_set_factor_priority(fisdf_ctx* c, int high) {
+  FISDF_TRY(ctx_guard(c));
   FISDF_CHECK(c != nullptr && (high == 0 || high == 1), "set_factor_priority: 0 or 1");
   c->factor_hi = high;
   return 0;
@@ -1364,8 +1410,11 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   FISDF_HIP(hipMalloc(&c->f_Linv, sizeof(cplx) * (size_t)nk * nblk * nb * nb));
   FISDF_HIP(hipMalloc(&c->f_Q, sizeof(cplx) * nk * nn));
   FISDF_HIP(hipMalloc(&c->f_Li, sizeof(cplx) * nk * nn));
-  // split-K partials of the L^{-1} substitution for the whole batch (one launch per block row)
-  c->f_ksw_elems = std::max(1L, trsm_split_work_elems(nip, nk));
+  // split-K partials of the L^{-1} substitution: the whole batch in one launch per block row when
+  // that fits 16M elements (256 MB), else trsm_merged_batched runs sub-batches (a matrix's split
+  // depends on its shape only, so its arithmetic is unchanged)
+  c->f_ksw_elems = std::max({1L, trsm_split_work_elems(nip, 1),
+                             std::min(trsm_split_work_elems(nip, nk), 16L << 20)});
   FISDF_HIP(hipMalloc(&c->f_ksw, sizeof(cplx) * c->f_ksw_elems));
   FISDF_HIP(hipMalloc(&c->f_piv, sizeof(int) * (size_t)nk * nip));
   FISDF_HIP(hipMalloc(&c->f_rank_dev, sizeof(int) * nk));
@@ -1435,18 +1484,21 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
 }
 
 int fisdf_set_pivoted_fit(fisdf_ctx* c, int mode) {
+  FISDF_TRY(ctx_guard(c));
   FISDF_CHECK(c != nullptr && mode >= -1 && mode <= 1, "set_pivoted_fit: bad mode");
   c->force_pivoted = mode;
   return 0;
 }
 
 int fisdf_set_half_grid(fisdf_ctx* c, int mode) {
+  FISDF_TRY(ctx_guard(c));
   FISDF_CHECK(c != nullptr && mode >= -1 && mode <= 1, "set_half_grid: mode must be -1, 0 or 1");
   c->half_grid = mode;
   return 0;
 }
 
 int fisdf_set_fit_mode(fisdf_ctx* c, int mode) {
+  FISDF_TRY(ctx_guard(c));
   FISDF_CHECK(c != nullptr && mode >= FISDF_FIT_LSTSQ && mode <= FISDF_FIT_BASIC,
               "set_fit_mode: mode must be FISDF_FIT_LSTSQ, FISDF_FIT_SVD or FISDF_FIT_BASIC");
   c->fit_mode = mode;
@@ -1454,6 +1506,7 @@ int fisdf_set_fit_mode(fisdf_ctx* c, int mode) {
 }
 
 int fisdf_min_norm_info(fisdf_ctx* c, int* h_nslots) {
+  FISDF_TRY(ctx_guard(c));
   FISDF_CHECK(c != nullptr, "null context");
   int n = 0;
   for (char v : c->f_cod) n += v ? 1 : 0;
@@ -1462,24 +1515,28 @@ int fisdf_min_norm_info(fisdf_ctx* c, int* h_nslots) {
 }
 
 int fisdf_set_omega(fisdf_ctx* c, double omega) {
+  FISDF_TRY(ctx_guard(c));
   FISDF_CHECK(c != nullptr && std::isfinite(omega), "set_omega: omega must be finite");
   c->omega = omega;
   return 0;
 }
 
 int fisdf_set_time_reversal(fisdf_ctx* c, int on) {
+  FISDF_TRY(ctx_guard(c));
   FISDF_CHECK(c != nullptr && (on == 0 || on == 1), "set_time_reversal: on must be 0 or 1");
   c->time_reversal = on == 1;
   return 0;
 }
 
 int fisdf_set_fit_lanes(fisdf_ctx* c, int lanes) {
+  FISDF_TRY(ctx_guard(c));
   FISDF_CHECK(c != nullptr && lanes >= 0 && lanes <= 4, "set_fit_lanes: lanes must be 0..4");
   c->lanes = lanes;
   return 0;
 }
 
 int fisdf_set_fit_pipe(fisdf_ctx* c, int mode, int depth) {
+  FISDF_TRY(ctx_guard(c));
   FISDF_CHECK(c != nullptr && mode >= -1 && mode <= 1 && depth >= 0 && depth <= 64,
               "set_fit_pipe: mode must be -1..1, depth 0..64");
   c->pipe_mode = mode;
@@ -1521,6 +1578,7 @@ int fisdf_set_y_slices(fisdf_ctx* c, int j, const void* recv, int nparts, const 
 }
 
 int fisdf_fit_info(fisdf_ctx* c, int* h_lanes, int* h_pipe_depth) {
+  FISDF_TRY(ctx_guard(c));
   FISDF_CHECK(c != nullptr, "null context");
   if (h_lanes) *h_lanes = c->last_fit_lanes;
   if (h_pipe_depth) *h_pipe_depth = c->last_fit_pipe;
@@ -1534,6 +1592,7 @@ int fisdf_reserve_workspace(fisdf_ctx* c, size_t bytes) {
 }
 
 int fisdf_factor_info(fisdf_ctx* c, int* h_used_pivoted) {
+  FISDF_TRY(ctx_guard(c));
   FISDF_CHECK(c != nullptr, "null context");
   if (h_used_pivoted) *h_used_pivoted = c->f_used_pivoted ? 1 : 0;
   return 0;
@@ -1798,6 +1857,15 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   }
   c->last_fit_lanes = NL;
   c->last_fit_pipe = pipe ? D : 0;
+  // all-to-all pieces of a mesh whose first FFT pass cannot read plane slices in place (no
+  // register kernel, plane too large for the LDS plane kernel): each FFT-issuing stream (the FFT
+  // stream, or every lane) unpacks its q's piece into a (nip, ngrid) buffer of its own first
+  bool any_piece = false;
+  for (int lq = 0; lq < nq; ++lq) any_piece = any_piece || piece_of(lq) != nullptr;
+  const bool unpack = any_piece && !fft3d_reads_slices(mesh[0], mesh[1], mesh[2]);
+  size_t oP[4] = {0, 0, 0, 0};
+  if (unpack)
+    for (int l = 0; l < (pipe ? 1 : NL); ++l) oP[l] = cv.take(sizeof(cplx) * (size_t)nip * ngrid);
   size_t oG = cv.take(sizeof(cplx) * nq * rr);
   size_t oT = cv.take(sizeof(cplx) * nq * rr);
   size_t oS = cv.take(sizeof(cplx) * nq * rr);
@@ -1860,11 +1928,10 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   // sharded build: q read in place from their all-to-all pieces (fisdf_set_y_slices) through a
   // per-plane address table (plane-aligned slices)
   const PlaneRef* planes = nullptr;
-  bool any_piece = false;
-  for (int lq = 0; lq < nq; ++lq) any_piece = any_piece || piece_of(lq) != nullptr;
-  if (any_piece) FISDF_TRY(plane_table(c, mesh, nip, &planes));
+  if (any_piece && !unpack) FISDF_TRY(plane_table(c, mesh, nip, &planes));
   FISDF_CHECK(yT != nullptr || any_piece, "fit_coulomb: no y");
-  auto fft_q = [&](hipStream_t st, int lq, cplx* Yh) -> int {
+  // ub: the stream's unpack buffer (FFT stream 0, lane l -> l)
+  auto fft_q = [&](hipStream_t st, int lq, cplx* Yh, int ub) -> int {
     const int sl = s0 + lq;
     const int r = cod_of(sl) ? nip : c->f_rank[sl];
     double kq[3], kd[3];
@@ -1875,6 +1942,22 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     StageTimer tm(c, FISDF_ST_FFT, st);
     const cplx* pc = piece_of(lq);
     FISDF_CHECK(pc || yT, "fit_coulomb: q without y");
+    if (pc && unpack) {  // piece -> (nip, ngrid) rows, stream-ordered before the FFT reads them
+      cplx* yb = (cplx*)(b + oP[ub]);
+      const char* src = (const char*)pc;
+      for (size_t p = 0; p + 1 < c->y_slices.size(); p += 2) {
+        const long g0 = c->y_slices[p], ng = c->y_slices[p + 1];
+        FISDF_CHECK(g0 + ng <= ngrid, "fit_coulomb: y slice out of the mesh");
+        if (ng == 0) continue;
+        FISDF_HIP(hipMemcpy2DAsync(yb + g0, sizeof(cplx) * ngrid, src, sizeof(cplx) * ng,
+                                   sizeof(cplx) * ng, nip, hipMemcpyDeviceToDevice, st));
+        src += sizeof(cplx) * (size_t)ng * nip;
+      }
+      pc = nullptr;
+      FISDF_TRY(fft3d(st, yb, ngrid, c->f_piv + (long)sl * nip, Yh, ngrid, r, mesh[0], mesh[1],
+                      mesh[2], kd, wt, nullptr, nullptr));
+      return 0;
+    }
     FISDF_TRY(fft3d(st, pc ? pc : yT + (long)lq * nip * ngrid, ngrid, c->f_piv + (long)sl * nip, Yh,
                     ngrid, r, mesh[0], mesh[1], mesh[2], kd, wt, nullptr, pc ? planes : nullptr));
     return 0;
@@ -1886,7 +1969,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     if (lq >= nq || c->f_rank[s0 + lq] == 0) return 0;
     if (lq >= D) FISDF_HIP(hipStreamWaitEvent(fst, c->ev_free[lq % D], 0));
     if (ready) FISDF_HIP(hipStreamWaitEvent(fst, c->ev_ready[lq], 0));
-    FISDF_TRY(fft_q(fst, lq, slot_y(lq)));
+    FISDF_TRY(fft_q(fst, lq, slot_y(lq), 0));
     FISDF_HIP(hipEventRecord(c->ev_q[lq], fst));
     return 0;
   };
@@ -1915,7 +1998,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       FISDF_HIP(hipStreamWaitEvent(st, c->ev_q[lq], 0));
     } else {
       if (ready) FISDF_HIP(hipStreamWaitEvent(st, c->ev_ready[lq], 0));
-      FISDF_TRY(fft_q(st, lq, Yh));
+      FISDF_TRY(fft_q(st, lq, Yh, ln));
     }
     cplx* Uq = U;  // where L^{-1} Yh lands
     const long ncol = ncols_of(lq);  // grid columns fitted (half for a self-conjugate q)
@@ -2363,6 +2446,283 @@ static int get_k_block(fisdf_ctx* c, const void* Xv, const double* Ws_rows, long
 int fisdf_get_k(fisdf_ctx* c, const void* Xv, const void* Wsv, const void* dmsv, int nset, int nip,
                 int nao, const int kmesh[3], const double a[9], void* vkv) {
   return fisdf_get_k_rows(c, Xv, Wsv, dmsv, nset, nip, nao, kmesh, a, 0, nip, vkv);
+}
+
+// ---- composite entries --------------------------------------------------------
+}  // extern "C"
+
+namespace {
+
+enum BuildRole { BR_X = 0, BR_X4 = 1, BR_Y = 2, BR_WQ = 3, BR_WS = 4 };
+
+// a buffer of the composite build: the caller's allocator, or a library-owned grow-only buffer
+int build_alloc(fisdf_ctx* c, int role, size_t bytes, void** out) {
+  bytes = std::max<size_t>(bytes, 256);
+  if (c->alloc_fn) {
+    void* p = c->alloc_fn(bytes, c->alloc_user);
+    FISDF_CHECK(p != nullptr, "build: the caller's allocator returned NULL");
+    c->lent.push_back(p);
+    *out = p;
+    return 0;
+  }
+  auto& o = c->owned[role];
+  if (o.second < bytes) {
+    if (o.first) {
+      FISDF_HIP(hipStreamSynchronize(c->stream));
+      FISDF_HIP(hipFree(o.first));
+    }
+    o = {nullptr, 0};
+    FISDF_HIP(hipMalloc(&o.first, bytes));
+    o.second = bytes;
+  }
+  *out = o.first;
+  return 0;
+}
+
+// hand one lent buffer back (stream-ordered: its last use is enqueued on c->stream)
+void build_return(fisdf_ctx* c, void* p) {
+  if (!c->alloc_fn || !p) return;
+  auto it = std::find(c->lent.begin(), c->lent.end(), p);
+  if (it == c->lent.end()) return;
+  c->lent.erase(it);
+  if (c->free_fn) c->free_fn(p, c->alloc_user);
+}
+
+void build_return_all(fisdf_ctx* c) {
+  std::vector<void*> l;
+  l.swap(c->lent);
+  if (c->free_fn)
+    for (void* p : l) c->free_fn(p, c->alloc_user);
+  c->bld = fisdf_ctx::Build();
+}
+
+// time-reversal classes of the q-mesh (get_kpts order): partner[q] = index of -q, the fitted
+// representatives (smaller index of each pair) and their W_s weights (2 unless self-paired)
+void tr_classes(const int km[3], bool on, std::vector<int>& reps, std::vector<int>& partner,
+                std::vector<double>& wt) {
+  const int nk = km[0] * km[1] * km[2];
+  partner.resize(nk);
+  reps.clear();
+  wt.clear();
+  for (int q = 0; q < nk; ++q) {
+    const int i2 = q % km[2], i1 = (q / km[2]) % km[1], i0 = q / (km[1] * km[2]);
+    partner[q] = (((km[0] - i0) % km[0]) * km[1] + (km[1] - i1) % km[1]) * km[2] + (km[2] - i2) % km[2];
+  }
+  for (int q = 0; q < nk; ++q) {
+    if (!on) {  // every q fitted on its own (W_s weights 1)
+      partner[q] = q;
+      reps.push_back(q);
+      wt.push_back(1.0);
+    } else if (partner[q] >= q) {
+      reps.push_back(q);
+      wt.push_back(partner[q] == q ? 1.0 : 2.0);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+void fisdf_build_opts_default(fisdf_build_opts* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->nip_max = 0;
+  o->select_tol = -1.0;
+  o->perm = nullptr;
+  o->n_perm = 0;
+  o->fit_mode = FISDF_FIT_LSTSQ;
+  o->fit_tol = 1e-14;
+  o->pivoted_fit = -1;
+  o->half_grid = -1;
+  o->time_reversal = 1;
+  o->real_self_conjugate = 1;
+  o->omega = 0.0;
+}
+
+int fisdf_set_allocator(fisdf_ctx* c, fisdf_alloc_fn alloc, fisdf_free_fn release, void* user) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK((alloc == nullptr) == (release == nullptr), "set_allocator: give both functions or neither");
+  FISDF_TRY(fisdf_build_release(c));
+  c->alloc_fn = alloc;
+  c->free_fn = release;
+  c->alloc_user = user;
+  return 0;
+}
+
+int fisdf_build_release(fisdf_ctx* c) {
+  FISDF_TRY(device_guard(c));
+  if (c->f_pending) FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
+  build_return_all(c);
+  if (!c->owned.empty()) {
+    FISDF_HIP(hipStreamSynchronize(c->stream));
+    for (auto& kv : c->owned)
+      if (kv.second.first) FISDF_HIP(hipFree(kv.second.first));
+    c->owned.clear();
+  }
+  return 0;
+}
+
+// ISDF.build() (fftisdf.py:308-325 -> build(df_obj), :22-128) on one GPU: the same stage sequence
+// the Python mirror's k-shard-capable build runs (fisdf/isdf.py build(), unsharded branch)
+int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, const int kmesh[3],
+                const int mesh[3], const double a[9], const fisdf_build_opts* opts_in, int* h_nip) {
+  FISDF_TRY(device_guard(c));
+  fisdf_build_opts o;
+  fisdf_build_opts_default(&o);
+  if (opts_in) o = *opts_in;
+  FISDF_CHECK(x0 && f && kmesh && mesh && a && ng0 > 0 && nao > 0, "build: bad arguments");
+  FISDF_CHECK(kmesh[0] > 0 && kmesh[1] > 0 && kmesh[2] > 0 && mesh[0] > 0 && mesh[1] > 0 && mesh[2] > 0,
+              "build: bad k-mesh or mesh");
+  FISDF_CHECK(o.fit_mode >= FISDF_FIT_LSTSQ && o.fit_mode <= FISDF_FIT_BASIC, "build: bad fit_mode");
+  FISDF_CHECK(o.perm == nullptr || o.n_perm > 0, "build: perm given without n_perm");
+  // the previous build's buffers go back first (its factor chain may still read x4)
+  if (c->f_pending) FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
+  build_return_all(c);
+  fisdf_ctx::Build& B = c->bld;
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  const long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
+  FISDF_CHECK(ngrid < (1L << 31), "build: mesh too large");
+  // interpolation points (:33 -> :357-388), or the caller's
+  std::vector<int> perm;
+  if (o.perm) {
+    perm.assign(o.perm, o.perm + o.n_perm);
+  } else {
+    const int cap = o.nip_max > 0 ? std::min(o.nip_max, ng0) : ng0;
+    perm.assign(cap, 0);
+    int npiv = 0, full = 0;
+    FISDF_TRY(fisdf_select_points(c, x0, nk, ng0, nao, cap, o.select_tol, perm.data(), &npiv, &full));
+    perm.resize(std::min(cap, npiv));                                             // :383
+  }
+  const int nip = (int)perm.size();
+  FISDF_CHECK(nip > 0, "build: no interpolation points");
+  const long nn = (long)nip * nip;
+  void *X, *x4;
+  FISDF_TRY(build_alloc(c, BR_X, sizeof(cplx) * (size_t)nk * nip * nao, &X));
+  FISDF_TRY(fisdf_gather_points(c, x0, nk, ng0, nao, perm.data(), nip, X));        // :388
+  FISDF_TRY(build_alloc(c, BR_X4, sizeof(cplx) * (size_t)nk * nn, &x4));
+  FISDF_TRY(fisdf_build_x4(c, X, nip, nao, kmesh, a, x4));                         // :38-48
+  std::vector<int> qs, partner;
+  std::vector<double> wt;
+  tr_classes(kmesh, o.time_reversal != 0, qs, partner, wt);
+  const int nq = (int)qs.size();
+  // the factorisation (replaces zgelsy's QRCP, :108) on the side stream, overlapped with y
+  FISDF_TRY(fisdf_set_pivoted_fit(c, o.pivoted_fit));
+  FISDF_TRY(fisdf_set_fit_mode(c, o.fit_mode));
+  FISDF_TRY(fisdf_set_half_grid(c, o.half_grid));
+  FISDF_TRY(fisdf_set_factor_priority(c, 0));
+  FISDF_TRY(fisdf_factor_x4_mark(c));
+  FISDF_TRY(fisdf_set_time_reversal(c, o.time_reversal ? 1 : 0));
+  FISDF_TRY(fisdf_set_omega(c, o.omega));
+  void* yT;
+  FISDF_TRY(build_alloc(c, BR_Y, sizeof(cplx) * (size_t)nq * nip * ngrid, &yT));
+  FISDF_TRY(fisdf_build_y_qs(c, f, ngrid * nao, 0, (int)ngrid, (int)ngrid, X, nip, nao, kmesh, a,
+                             qs.data(), nq, yT));                                  // :67-87
+  FISDF_TRY(fisdf_factor_x4_async(c, x4, qs.data(), nq, nip, o.fit_tol,
+                                  o.real_self_conjugate ? kmesh : nullptr));
+  std::vector<int> ranks(nq, 0);
+  FISDF_TRY(fisdf_factor_x4_wait(c, ranks.data()));
+  int used = 0, ncod = 0;
+  FISDF_TRY(fisdf_factor_info(c, &used));
+  FISDF_TRY(fisdf_min_norm_info(c, &ncod));
+  void *Wq, *Ws;
+  FISDF_TRY(build_alloc(c, BR_WQ, sizeof(cplx) * (size_t)nq * nn, &Wq));
+  FISDF_TRY(fisdf_fit_coulomb_qs(c, qs.data(), nq, yT, nip, mesh, kmesh, a, Wq));   // :97-121
+  build_return(c, yT);  // y is dead once the fit is enqueued (stream-ordered)
+  FISDF_TRY(build_alloc(c, BR_WS, sizeof(double) * (size_t)nk * nn, &Ws));
+  FISDF_TRY(fisdf_build_ws_qs(c, Wq, qs.data(), wt.data(), nq, nip, kmesh, a, Ws)); // :204-207
+  B.valid = true;
+  B.nk = nk;
+  B.nip = nip;
+  B.nao = nao;
+  B.ng0 = ng0;
+  B.nfit = nq;
+  B.used_pivoted = used;
+  B.min_norm = ncod;
+  for (int i = 0; i < 3; ++i) B.kmesh[i] = kmesh[i], B.mesh[i] = mesh[i];
+  for (int i = 0; i < 9; ++i) B.a[i] = a[i];
+  B.perm = perm;
+  B.fit_qs = qs;
+  B.partner = partner;
+  B.ranks = ranks;
+  B.wt = wt;
+  B.X = X;
+  B.x4 = x4;
+  B.Wq = Wq;
+  B.Ws = Ws;
+  if (h_nip) *h_nip = nip;
+  return 0;
+}
+
+int fisdf_build_get(fisdf_ctx* c, fisdf_build_result* out) {
+  FISDF_TRY(ctx_guard(c));
+  FISDF_CHECK(out != nullptr, "build_get: out is null");
+  const fisdf_ctx::Build& B = c->bld;
+  FISDF_CHECK(B.valid, "build_get: no build (call fisdf_build first)");
+  out->nk = B.nk;
+  out->nip = B.nip;
+  out->nao = B.nao;
+  out->nfit = B.nfit;
+  out->used_pivoted_fit = B.used_pivoted;
+  out->min_norm_slots = B.min_norm;
+  out->perm = B.perm.data();
+  out->fit_qs = B.fit_qs.data();
+  out->ranks = B.ranks.data();
+  out->partner = B.partner.data();
+  out->d_X = B.X;
+  out->d_x4 = B.x4;
+  out->d_Wq = B.Wq;
+  out->d_Ws = B.Ws;
+  return 0;
+}
+
+int fisdf_get_x(fisdf_ctx* c, void* h_x) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(c->bld.valid && h_x, "get_x: no build or null output");
+  const auto& B = c->bld;
+  return fisdf_memcpy_dtoh(c, h_x, B.X, sizeof(cplx) * (size_t)B.nk * B.nip * B.nao);
+}
+
+int fisdf_get_w0(fisdf_ctx* c, void* h_w0) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(c->bld.valid && h_w0, "get_w0: no build or null output");
+  const auto& B = c->bld;  // q = 0 is always fitted (slot 0: the smallest representative)
+  return fisdf_memcpy_dtoh(c, h_w0, B.Wq, sizeof(cplx) * (size_t)B.nip * B.nip);
+}
+
+int fisdf_get_wq(fisdf_ctx* c, void* h_wq) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(c->bld.valid && h_wq, "get_wq: no build or null output");
+  const auto& B = c->bld;
+  const size_t nn = (size_t)B.nip * B.nip;
+  cplx* h = (cplx*)h_wq;
+  std::vector<int> slot(B.nk, -1);
+  for (int i = 0; i < B.nfit; ++i) slot[B.fit_qs[i]] = i;
+  for (int i = 0; i < B.nfit; ++i)
+    FISDF_HIP(hipMemcpyAsync(h + (size_t)B.fit_qs[i] * nn, (const cplx*)B.Wq + i * nn,
+                             sizeof(cplx) * nn, hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  for (int q = 0; q < B.nk; ++q) {  // W_{-q} = conj(W_q) (x4_s, y_s real: fftisdf.py:43,81)
+    if (slot[q] >= 0) continue;
+    const int p = B.partner[q];
+    FISDF_CHECK(p >= 0 && p < B.nk && slot[p] >= 0, "get_wq: q neither fitted nor a partner");
+    for (size_t e = 0; e < nn; ++e) h[(size_t)q * nn + e] = cconj(h[(size_t)p * nn + e]);
+  }
+  return 0;
+}
+
+// fftisdf.py:390-408: K (get_k_kpts, :173-228) enqueued before J (get_j_kpts, :133-171)
+int fisdf_get_jk(fisdf_ctx* c, const void* dms, int nset, int with_j, int with_k, void* vj, void* vk) {
+  FISDF_TRY(device_guard(c));
+  const auto& B = c->bld;
+  FISDF_CHECK(B.valid, "get_jk: no build (call fisdf_build first)");
+  FISDF_CHECK(dms && nset > 0, "get_jk: no density matrices");
+  FISDF_CHECK((!with_j || vj) && (!with_k || vk), "get_jk: missing output");
+  if (with_k)
+    FISDF_TRY(fisdf_get_k_rows(c, B.X, B.Ws, dms, nset, B.nip, B.nao, B.kmesh, B.a, 0, B.nip, vk));
+  if (with_j)
+    FISDF_TRY(fisdf_get_j_rows(c, B.X, B.Wq, dms, nset, B.nk, B.nip, B.nao, 0, B.nip, vj));
+  return 0;
 }
 
 }  // extern "C"

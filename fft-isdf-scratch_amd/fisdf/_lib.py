@@ -32,7 +32,7 @@ _SIGS = {
     "fisdf_abi_version": ([], _i),
     "fisdf_create": ([_i, _vp, C.POINTER(_vp)], _i),
     "fisdf_destroy": ([_vp], _i),
-    "fisdf_last_error": ([], C.c_char_p),
+    "fisdf_last_error": ([_vp], C.c_char_p),
     "fisdf_sync": ([_vp], _i),
     "fisdf_malloc": ([_vp, C.c_size_t, C.POINTER(_vp)], _i),
     "fisdf_free": ([_vp, _vp], _i),
@@ -95,7 +95,36 @@ _SIGS = {
     "fisdf_pivoted_cholesky": ([_vp, _vp, _i, _i, _i, _d, _ip, _ip], _i),
     "fisdf_cholesky": ([_vp, _vp, _i, _i, _d, _ip], _i),
     "fisdf_tri_inverse": ([_vp, _vp, _i, _i, _vp], _i),
+    # composite entries
+    "fisdf_build_opts_default": ([_vp], None),
+    "fisdf_build": ([_vp, _vp, _i, _vp, _i, _ip, _ip, _dp, _vp, _ip], _i),
+    "fisdf_build_get": ([_vp, _vp], _i),
+    "fisdf_build_release": ([_vp], _i),
+    "fisdf_get_x": ([_vp, _vp], _i),
+    "fisdf_get_w0": ([_vp, _vp], _i),
+    "fisdf_get_wq": ([_vp, _vp], _i),
+    "fisdf_get_jk": ([_vp, _vp, _i, _i, _i, _vp, _vp], _i),
+    "fisdf_set_allocator": ([_vp, _vp, _vp, _vp], _i),
 }
+
+
+class BuildOpts(C.Structure):
+    """struct fisdf_build_opts (include/fisdf.h)."""
+    _fields_ = [("nip_max", _i), ("select_tol", _d), ("perm", _ip), ("n_perm", _i),
+                ("fit_mode", _i), ("fit_tol", _d), ("pivoted_fit", _i), ("half_grid", _i),
+                ("time_reversal", _i), ("real_self_conjugate", _i), ("omega", _d)]
+
+
+class BuildResult(C.Structure):
+    """struct fisdf_build_result (include/fisdf.h)."""
+    _fields_ = [("nk", _i), ("nip", _i), ("nao", _i), ("nfit", _i), ("used_pivoted_fit", _i),
+                ("min_norm_slots", _i), ("perm", _ip), ("fit_qs", _ip), ("ranks", _ip),
+                ("partner", _ip), ("d_X", _vp), ("d_x4", _vp), ("d_Wq", _vp), ("d_Ws", _vp)]
+
+
+# fisdf_alloc_fn / fisdf_free_fn
+ALLOC_FN = C.CFUNCTYPE(_vp, C.c_size_t, _vp)
+FREE_FN = C.CFUNCTYPE(None, _vp, _vp)
 
 
 class FisdfError(RuntimeError):
@@ -122,9 +151,10 @@ def load(path: str = LIB_PATH):
     return lib
 
 
-def check(rc):
+def check(rc, ctx=None):
+    """Raise FisdfError with the failing context's message (fisdf_last_error(ctx))."""
     if rc != 0:
-        raise FisdfError(load().fisdf_last_error().decode())
+        raise FisdfError(load().fisdf_last_error(ctx).decode())
 
 
 def iarr(x):
@@ -152,7 +182,7 @@ class Context:
     def __init__(self, device: int = 0, stream=None):
         lib = load()
         out = _vp()
-        check(lib.fisdf_create(int(device), _vp(stream) if stream else None, C.byref(out)))
+        check(lib.fisdf_create(int(device), _vp(stream) if stream else None, C.byref(out)), None)
         self.lib = lib
         self.h = out
         self.device = device
@@ -169,7 +199,13 @@ class Context:
             pass
 
     def call(self, name, *args):
-        check(getattr(self.lib, name)(self.h, *args))
+        check(getattr(self.lib, name)(self.h, *args), self.h)
+
+    def build_result(self):
+        """The last fisdf_build's resident result (struct fisdf_build_result)."""
+        r = BuildResult()
+        self.call("fisdf_build_get", C.byref(r))
+        return r
 
     def timings(self):
         ms = (C.c_double * len(STAGES))()

@@ -479,10 +479,105 @@ ISDF = InterpolativeSeparableDensityFitting
 from ctypes import c_int as C_int, c_long as C_long, byref  # noqa: E402
 
 
+class _TorchBuffers:
+    """The composite build's device buffers (fisdf_set_allocator) taken from torch's caching
+    allocator on the context's stream, so X, x4, W_q, W_s become torch tensors the rest of the
+    mirror (get_jk, ERIs, the reference attributes) reads, and y returns to torch's cache as soon
+    as the fit is enqueued."""
+
+    def __init__(self, d):
+        self.d = d
+        self.live = {}
+        self.alloc_cb = _lib.ALLOC_FN(self._alloc)
+        self.free_cb = _lib.FREE_FN(self._free)
+        d.ctx.call("fisdf_set_allocator", self.alloc_cb, self.free_cb, None)
+
+    def _alloc(self, nbytes, user):
+        t = self.d.torch.empty(int(nbytes), dtype=self.d.torch.uint8, device=self.d.dev)
+        self.live[t.data_ptr()] = t
+        return t.data_ptr()
+
+    def _free(self, ptr, user):
+        self.live.pop(ptr, None)
+
+    def tensor(self, ptr, shape, dtype="c128"):
+        t = self.d.torch
+        dt, size = {"c128": (t.complex128, 16), "f64": (t.float64, 8)}[dtype]
+        n = int(np.prod(shape))
+        return self.live[ptr][:n * size].view(dt).reshape(tuple(int(x) for x in shape))
+
+
+def _build_one_gpu(df_obj):
+    """The 1-GPU build through the library's composite entry fisdf_build (include/fisdf.h;
+    fftisdf.py:22-128): selection (or the injected points), x4, y, factor + fit + FFT Coulomb of
+    the fitted q, W_s — one C call; the result is adopted as torch tensors."""
+    d = df_obj.device
+    cell = df_obj.cell
+    kmesh = np.asarray(df_obj._kmesh(), dtype=np.int32)
+    nk = int(np.prod(kmesh))
+    nao = cell.nao_nr()
+    km_c, km_p = _lib.iarr(kmesh)
+    a_c, a_p = _lib.darr(np.ascontiguousarray(cell.lattice_vectors(), dtype=np.float64).ravel())
+    mesh_c, mesh_p = _lib.iarr(df_obj.mesh)
+    if df_obj._ao_parent is None:
+        df_obj._ao_parent = df_obj._eval_ao(cell.gen_uniform_grids(df_obj.m0))
+    if df_obj._ao_grid is None:
+        df_obj._ao_grid = df_obj._eval_ao(df_obj.grids_coords())
+    x0, f = df_obj._ao_parent, df_obj._ao_grid
+    ng0 = x0.shape[1]
+    modes = {"lstsq": 0, "svd": 1, "basic": 2}
+    if df_obj.fit not in modes:
+        raise ValueError(f"ISDF.fit must be one of {sorted(modes)}, not {df_obj.fit!r}")
+    o = _lib.BuildOpts()
+    d.ctx.lib.fisdf_build_opts_default(byref(o))
+    st = df_obj._dev_state
+    if st is not None and "X" in st:            # points given (select_interpolation_points /
+        perm_c = np.ascontiguousarray(df_obj.perm, dtype=np.int32)   # set_interpolation_points)
+        o.perm, o.n_perm = perm_c.ctypes.data_as(_lib._ip), len(perm_c)
+    else:
+        cap = int(nao * df_obj.c0) if df_obj.nip_max is None else int(df_obj.nip_max)
+        o.nip_max = max(1, min(cap, ng0))                              # fftisdf.py:383
+    o.select_tol = float(df_obj.select_tol)
+    o.fit_mode = modes[df_obj.fit]
+    o.fit_tol = float(df_obj.fit_tol)
+    o.pivoted_fit = -1 if df_obj.pivoted_fit is None else int(bool(df_obj.pivoted_fit))
+    o.half_grid = -1 if df_obj.half_grid is None else int(bool(df_obj.half_grid))
+    o.time_reversal = int(bool(df_obj.time_reversal))
+    o.real_self_conjugate = int(bool(df_obj.real_self_conjugate))
+    o.omega = float(getattr(df_obj, "_fit_omega", 0.0))
+    if getattr(d, "bufs", None) is None:
+        d.bufs = _TorchBuffers(d)
+    nip_c = C_int()
+    d.ctx.call("fisdf_build", _lib.ptr(x0), ng0, _lib.ptr(f), nao, km_p, mesh_p, a_p, byref(o),
+               byref(nip_c))
+    r = d.ctx.build_result()
+    nip, nq = r.nip, r.nfit
+    b = d.bufs
+    Wq = b.tensor(r.d_Wq, (nq, nip, nip))
+    df_obj._dev_state = dict(X=b.tensor(r.d_X, (nk, nip, nao)), x4=b.tensor(r.d_x4, (nk, nip, nip)),
+                             Wq=Wq, W0=Wq[0], Ws=b.tensor(r.d_Ws, (nk, nip, nip), "f64"))
+    df_obj.perm = np.ctypeslib.as_array(r.perm, (nip,)).copy()
+    df_obj.fit_qs = np.ctypeslib.as_array(r.fit_qs, (nq,)).astype(np.int32)
+    df_obj.q_partner = np.ctypeslib.as_array(r.partner, (nk,)).astype(np.int32)
+    df_obj.my_qs = df_obj.fit_qs.copy()
+    df_obj.ranks = np.ctypeslib.as_array(r.ranks, (nq,)).copy()
+    df_obj.used_pivoted_fit = bool(r.used_pivoted_fit)
+    df_obj.min_norm_slots = int(r.min_norm_slots)
+    df_obj.nip = nip
+    return df_obj
+
+
 def build(df_obj):
-    """fftisdf.py:22-128 on the GPU.  Leaves X, W_q (own shard), W_0, W_s resident."""
+    """fftisdf.py:22-128 on the GPU.  Leaves X, W_q (own shard), W_0, W_s resident.  One GPU:
+    the library's composite fisdf_build; k-sharded: the stage entries with the collectives
+    between them."""
     t0 = time.perf_counter()
     d = df_obj.device
+    if not d.sharded(df_obj):
+        df_obj._omega_dfs = {}                   # range-separated states of an earlier build
+        _build_one_gpu(df_obj)
+        df_obj.timings["build"] = time.perf_counter() - t0
+        return df_obj
     torch = d.torch
     cell = df_obj.cell
     kmesh = np.asarray(df_obj._kmesh(), dtype=np.int32)

@@ -12,9 +12,15 @@
  *  - pointers named d_* are DEVICE pointers (hipMalloc'ed, or from fisdf_malloc);
  *    pointers named h_* are host pointers.  Work is enqueued on the context's stream
  *    and is asynchronous unless the function says "synchronous".
- *  - every function returns 0 on success or a negative code; fisdf_last_error()
- *    returns the message of the last failure on the calling thread.
- *  - one context per process/device; not thread-safe.
+ *  - every function returns 0 on success or a negative code; fisdf_last_error(ctx)
+ *    returns the message of that context's last failure (fisdf_last_error(NULL): the last
+ *    failure on the calling thread, e.g. of fisdf_create).
+ *  - a context is not thread-safe; several contexts (devices) may be driven from one thread.
+ *
+ * Two layers: the composite entries (fisdf_build / fisdf_get_jk / fisdf_get_wq, the reference's
+ * ISDF.build() and ISDF.get_jk(), fftisdf.py:308-325,390-408) drive the whole 1-GPU path; the
+ * stage entries below them are what the composite entries run, exported for k-sharded callers
+ * (which interleave collectives between the stages, fisdf/isdf.py) and for the tests.
  */
 #ifndef FISDF_H
 #define FISDF_H
@@ -25,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FISDF_ABI_VERSION 1
+#define FISDF_ABI_VERSION 2
 
 typedef struct fisdf_ctx fisdf_ctx;
 
@@ -50,7 +56,7 @@ enum {
 int fisdf_abi_version(void);
 int fisdf_create(int device, void* hip_stream /* NULL: default (null) stream */, fisdf_ctx** out);
 int fisdf_destroy(fisdf_ctx* ctx);
-const char* fisdf_last_error(void);
+const char* fisdf_last_error(const fisdf_ctx* ctx /* NULL: the calling thread's last failure */);
 int fisdf_sync(fisdf_ctx* ctx);
 int fisdf_malloc(fisdf_ctx* ctx, size_t bytes, void** d_ptr);
 int fisdf_free(fisdf_ctx* ctx, void* d_ptr);
@@ -61,6 +67,77 @@ int fisdf_timings(fisdf_ctx* ctx, double* h_ms /* FISDF_NSTAGES */, int* h_calls
 /* reality invariants, max |Im| seen since the last call: [0] x2_s (fftisdf.py:43),
  * [1] fx_s (fftisdf.py:81), [2] rho_s (fftisdf.py:216).  synchronous; resets. */
 int fisdf_max_imag(fisdf_ctx* ctx, double* h_out /* 3 */);
+
+/* ---- composite entries: the whole 1-GPU build and get_jk ----------------
+ * Replace InterpolativeSeparableDensityFitting.build() + get_jk() (fftisdf.py:308-325, 22-128,
+ * 390-408): selection (:357-388), x4 (:38-48), y (:67-87), per-q fit + FFT Coulomb (:97-121),
+ * W_s (:204-207) in one call, the results left resident on the device for fisdf_get_jk. */
+typedef struct fisdf_build_opts {
+  int nip_max;             /* cap on interpolation points, int(nao * c0) (fftisdf.py:383); <= 0: ng0 */
+  double select_tol;       /* dpstrf tolerance of the selection; <= 0: ng0 * eps * max diag */
+  const int* perm;         /* host, n_perm parent-grid indices: use these points, no selection */
+  int n_perm;              /*   (ISDF.set_interpolation_points / a refit on the same points)     */
+  int fit_mode;            /* FISDF_FIT_LSTSQ (gelsy semantics, default), _SVD, _BASIC */
+  double fit_tol;          /* relative pivot cut of the x4_q factorisation (1e-14) */
+  int pivoted_fit;         /* -1 default (fisdf_set_pivoted_fit), 0, 1 */
+  int half_grid;           /* -1 default (fisdf_set_half_grid), 0, 1 */
+  int time_reversal;       /* 1: fit one q of each (q, -q) pair, W_{-q} = conj(W_q) (default) */
+  int real_self_conjugate; /* 1: q with 2 k_q in the reciprocal lattice fitted in real arithmetic */
+  double omega;            /* Coulomb kernel (fisdf_set_omega); 0 = 1/r */
+} fisdf_build_opts;
+void fisdf_build_opts_default(fisdf_build_opts* opts);
+
+/* The build.  d_x0 (nk, ng0, nao) c128: Bloch AOs on the parent grid (:367-370); d_f (nk,
+ * ngrid, nao): Bloch AOs on the FFT grid (:72); kmesh, mesh, a: k-mesh, FFT mesh, lattice rows
+ * (bohr); opts may be NULL (defaults).  *h_nip = interpolation points.  Synchronous (returns
+ * with the device work enqueued; the host waits only where the stages read ranks back).
+ * Replaces the previous build's results; its buffers are released first. */
+int fisdf_build(fisdf_ctx* ctx, const void* d_x0, int ng0, const void* d_f, int nao,
+                const int kmesh[3], const int mesh[3], const double a[9],
+                const fisdf_build_opts* opts, int* h_nip);
+
+/* What the last build left resident.  Pointers stay valid until the next fisdf_build,
+ * fisdf_build_release or fisdf_destroy on the context. */
+typedef struct fisdf_build_result {
+  int nk, nip, nao, nfit;     /* k-points, interpolation points, AOs, fitted q */
+  int used_pivoted_fit;       /* 1: some x4_q needed the pivoted (rank-revealing) factorisation */
+  int min_norm_slots;         /* q fitted through the minimum-norm operator */
+  const int* perm;            /* host (nip): the interpolation points, parent-grid indices */
+  const int* fit_qs;          /* host (nfit): fitted q, ascending (W_q slot i <-> q = fit_qs[i]) */
+  const int* ranks;           /* host (nfit): numerical rank of each fitted x4_q (:122) */
+  const int* partner;         /* host (nk): index of -q; W_q = conj(W_{partner[q]}) if not fitted */
+  const void* d_X;            /* (nk, nip, nao) c128: x0 at the points (fftisdf.py:125, _x) */
+  const void* d_x4;           /* (nk, nip, nip) c128 */
+  const void* d_Wq;           /* (nfit, nip, nip) c128 */
+  const void* d_Ws;           /* (nk, nip, nip) float64: W_s = Re(...) (fftisdf.py:207) */
+} fisdf_build_result;
+int fisdf_build_get(fisdf_ctx* ctx, fisdf_build_result* out);
+int fisdf_build_release(fisdf_ctx* ctx);
+
+/* Host copies of the reference's attributes (fftisdf.py:125-128): h_x (nk, nip, nao) = _x,
+ * h_w0 (nip, nip) = _w0, h_wq (nk, nip, nip) = _wq (unfitted q filled as conj(W_{-q})).
+ * synchronous. */
+int fisdf_get_x(fisdf_ctx* ctx, void* h_x);
+int fisdf_get_w0(fisdf_ctx* ctx, void* h_w0);
+int fisdf_get_wq(fisdf_ctx* ctx, void* h_wq);
+
+/* get_jk of the last build (fftisdf.py:390-408 -> get_k_kpts :173-228, then get_j_kpts
+ * :133-171): d_dms (nset, nk, nao, nao) c128 device; d_vj / d_vk same shape (either may be NULL
+ * when with_j / with_k is 0).  J is complex: a Gamma-only caller takes .real (:169-170).
+ * asynchronous. */
+int fisdf_get_jk(fisdf_ctx* ctx, const void* d_dms, int nset, int with_j, int with_k, void* d_vj,
+                 void* d_vk);
+
+/* Device memory of the composite build's buffers (X, x4, y, W_q, W_s) from the caller, e.g. a
+ * framework's caching allocator; alloc(NULL-safe) returns a device pointer of >= bytes or NULL.
+ * The library returns each buffer through free_fn once it no longer uses it — the y buffer right
+ * after the fit is enqueued, so free_fn must be stream-ordered on the context's stream (like
+ * hipFreeAsync / a caching allocator bound to that stream); the rest at the next build or
+ * fisdf_build_release (not at fisdf_destroy: the caller owns what it allocated).  NULL: library-
+ * owned buffers, kept between builds of the same size (fisdf_build_release frees them). */
+typedef void* (*fisdf_alloc_fn)(size_t bytes, void* user);
+typedef void (*fisdf_free_fn)(void* d_ptr, void* user);
+int fisdf_set_allocator(fisdf_ctx* ctx, fisdf_alloc_fn alloc, fisdf_free_fn release, void* user);
 
 /* ---- input layer: Bloch AO values ------------------------
  * Replaces PySCF pbc_eval_gto('GTOval', coords, kpts) / KNumInt.block_loop as called at

@@ -28,7 +28,14 @@ def test_library_exports_header_symbols():
         assert hasattr(lib, s), s
     # and the ctypes signature table covers the whole header
     assert set(syms) == set(_lib._SIGS), set(syms) ^ set(_lib._SIGS)
-    assert lib.fisdf_abi_version() == 1
+    assert lib.fisdf_abi_version() == 2
+    # no GPU here: fisdf_create fails and its message is the thread's last error (ctx NULL)
+    import ctypes as C
+    import torch
+    if not torch.cuda.is_available():
+        out = C.c_void_p()
+        assert lib.fisdf_create(0, None, C.byref(out)) != 0
+        assert b"device" in lib.fisdf_last_error(None) or b"HIP" in lib.fisdf_last_error(None)
 
 
 def test_no_cpu_fallback():
