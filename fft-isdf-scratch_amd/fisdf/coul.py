@@ -8,6 +8,9 @@ The reference's k-point ISDF scripts expose one function, ``get_coul(df_obj, ...
   ``nip = min(rank, 600)``, ``zgelsy`` fit);
 * ``get_coul_pinv``  — ``fftdf-with-k.py:20-160`` (parent grid ``m0``, ``nip = min(nip, rank)``,
   ``pinv(x4_q)`` fit);
+* ``get_coul_svd``   — ``fftdf-with-k-svd.py:20-185`` (Gamma-only selection Gram ``(x x^T)**2``,
+  ``dpstrf`` with ``tol=1e-32``, ``nip = int(ng * cisdf)`` not capped by the rank, truncated SVD
+  pseudo-solve) without that script's defects (SURVEY.md Appendix B);
 * ``check_eri``      — the harness ``fftdf-with-k-lstsq.py:208-258`` (``q = kconserv_ria[k1,k2]``,
   ``k4 = kconserv[k1,k2,k3]``, fail above 1e-4).
 
@@ -29,6 +32,7 @@ log = logging.getLogger("fisdf")
 
 NIP_CAP_LSTSQ = 600          # fftdf-with-k-lstsq.py:71 (``min(rank, 600)``)
 SELECT_TOL_LSTSQ = 1e-32     # fftdf-with-k-lstsq.py:70 (``pivoted_cholesky(x4, tol=1e-32)``)
+SELECT_TOL_SVD = 1e-32       # fftdf-with-k-svd.py:53
 
 
 class _Grids:
@@ -154,6 +158,70 @@ def get_coul_pinv(df_obj, m0=None, nip=100, kmesh=None, verbose=5, blksize=16000
     pseudo-solve as the lstsq driver."""
     m0 = [15, 15, 15] if m0 is None else m0
     return _run(df_obj, kmesh, m0, nip, -1.0, device, comm)
+
+
+def dpstrf_permutation(pivots, n):
+    """The whole permutation LAPACK dpstrf returns when it stops after ``len(pivots)`` steps:
+    step j swaps the chosen index into position j (dpstrf / dpstf2 exchange rows and columns j
+    and pvt), so the indices past the stop keep the order those swaps left — the order
+    ``perm[:nip]`` of fftdf-with-k-svd.py:57 reads past the rank."""
+    p = np.arange(n)
+    pos = np.arange(n)                    # pos[v]: where index v sits
+    for j, v in enumerate(np.asarray(pivots, dtype=int)):
+        i, w = pos[v], p[j]
+        p[j], p[i] = v, w
+        pos[v], pos[w] = j, i
+    return p
+
+
+def get_coul_svd(df_obj, k0=10.0, kmesh=None, cisdf=0.6, verbose=5, blksize=16000, m0=None,
+                 device=None, comm=None):
+    """``get_coul`` of fftdf-with-k-svd.py:20-185 (the SVD fit) -> ``(coul_q, x_k)``.
+
+    Parent grid ``cutoff_to_mesh(a, k0)`` (:31-33, or ``m0``); selection on the Gamma-point AOs
+    only, ``x4 = (x x^T)**2`` (:49-50) — the GPU selection with one k-point — by the greedy
+    pivoted Cholesky with dpstrf's ``tol=1e-32`` (:52-53); ``nip = int(ng * cisdf)`` points
+    (:54), NOT capped by the rank: past the point where the factorisation stops, the points are
+    the rest of dpstrf's permutation in its swap order (``dpstrf_permutation``), as
+    ``perm[:nip]`` reads them (:57); ``x_k`` the Bloch AOs there (:58); the truncated SVD
+    pseudo-solve ``z = V_r S_r^-1 U_r^H y`` per q (:158-164) with a relative cut instead of the
+    script's fixed rank 300, and without its broadcasting / rotated-basis defects (SURVEY.md
+    Appendix B) — ``ISDF.fit = "svd"``, the minimum-norm factored operator of DESIGN.md §3.4 on
+    every q.  ``verbose``/``blksize`` are accepted for signature parity."""
+    from . import _lib
+    from ctypes import byref, c_int
+    cell = df_obj.cell
+    kmesh = [1, 1, 1] if kmesh is None else [int(k) for k in kmesh]
+    if m0 is None:
+        m0 = cutoff_to_mesh(cell.lattice_vectors(), k0)
+    m0 = [int(m) for m in m0]
+    ng = int(np.prod(m0))
+    _device_guard(ng * ng * 16, "parent-grid selection Gram")             # :37-44
+    nip = min(int(ng * cisdf), ng)                                        # :54
+    isdf = ISDF(cell, cell.get_kpts(kmesh), m0=m0, device=device, comm=comm)
+    isdf.mesh = tuple(int(m) for m in df_obj.mesh)
+    isdf.fit = "svd"
+    d = isdf.device
+    coords0 = cell.gen_uniform_grids(m0)
+    if isdf.ao_on_gpu and hasattr(cell, "shells"):
+        from .ao import eval_ao_kpts_gpu
+        xg = eval_ao_kpts_gpu(d, cell, coords0, (1, 1, 1))               # :49-50, Gamma AOs
+    else:
+        from .cell import eval_ao_kpts
+        xg = d.to_dev(eval_ao_kpts(cell, coords0, (1, 1, 1)))
+    nao = cell.nao_nr()
+    piv = np.zeros(nip, np.int32)
+    npiv, full = c_int(), c_int()
+    d.ctx.call("fisdf_select_points", _lib.ptr(xg), 1, ng, nao, nip, SELECT_TOL_SVD,
+               piv.ctypes.data_as(_lib._ip), byref(npiv), byref(full))        # :52-53
+    perm = dpstrf_permutation(piv[:npiv.value], ng)[:nip]                  # :57
+    isdf.set_interpolation_points(perm)
+    isdf.build()
+    log.info("get_coul_svd: m0 = %s, ng = %d, nip = %d (factorisation stopped after %d), "
+             "ranks = %s", m0, ng, nip, npiv.value, np.asarray(isdf.ranks).tolist())
+    isdf.select_rank = int(npiv.value)
+    df_obj._isdf = isdf
+    return isdf._wq, isdf._x
 
 
 def check_eri(df_obj, kmesh, coul_q=None, x_k=None, tol=1e-4, triples=None):

@@ -152,6 +152,18 @@ def select_interpolation_points(x0, nao, c0):
     return perm[:nip], rank, nip, x4
 
 
+def select_points_svd_script(x_gamma, ng, cisdf):
+    """fftdf-with-k-svd.py:49-57: Gamma-only Gram x4 = (x x^T)**2 of the parent-grid AOs
+    x_gamma (ng, nao), dpstrf with tol=1e-32, nip = int(ng * cisdf) — not capped by the rank, so
+    perm[:nip] runs into the part of dpstrf's permutation past its stop.  Returns
+    (perm[:nip], rank, x4)."""
+    x = np.asarray(x_gamma)
+    x4 = (lambda v: (v @ v.T) ** 2)(x)                                 # :50
+    chol, perm, rank = pivoted_cholesky(x4, tol=1e-32)                 # :53
+    nip = int(ng * cisdf)                                              # :54
+    return perm[:nip], rank, x4
+
+
 def build_x4(xip, phase):
     """fftisdf.py:38-48: x2_k, x2_s (real), x4_s = x2_s**2, x4_k = Phi^H x4_s."""
     nkpt, nip, nao = xip.shape

@@ -157,3 +157,79 @@ def test_get_coul_gamma_default_kmesh():
     err = abs(c - out["wq"]).max()
     print("Gamma coul_q vs oracle", err, "scale", abs(out["wq"]).max())
     assert err < 1e-8 * max(1.0, abs(out["wq"]).max())
+
+
+def test_dpstrf_permutation_tail():
+    """The permutation dpstrf returns past its stop is its swap order: completing the first
+    `rank` pivots by dpstrf_permutation reproduces LAPACK's whole piv (what
+    fftdf-with-k-svd.py:57's perm[:nip] reads when nip exceeds the rank)."""
+    from scipy.linalg import lapack
+    rng = np.random.default_rng(3)
+    for n, r in [(40, 7), (97, 30), (64, 64)]:
+        B = rng.standard_normal((n, r))
+        A = B @ B.T
+        c, piv, rank, info = lapack.dpstrf(np.array(A, order="F"), tol=1e-10, lower=False)
+        piv = piv - 1
+        assert coul.dpstrf_permutation(piv[:rank], n).tolist() == piv.tolist(), (n, r, rank)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nip", [36, 320])
+def test_get_coul_svd_vs_oracle_and_eri_harness(nip):
+    """fftdf-with-k-svd.py get_coul: Gamma-only selection Gram (x x^T)^2 with dpstrf tol=1e-32,
+    nip = int(ng * cisdf), the SVD pseudo-solve.  toy222 (nao = 8 real AOs: the Gamma Gram has
+    rank 36).  The GPU's pivots inside that rank are greedy-optimal to rounding (the toy crystal
+    has exact ties).  nip = 36: every x4_q full rank, the solution unique — J/K against the
+    oracle's SVD pseudo-solve on the same points < 1e-8 Ha.  nip = 320 (cisdf 0.44, the script's
+    regime: most points past the rank, x4_q rank-deficient, the answer defined only up to the
+    pseudo-solve's cut): the script's own ERI check loop against exact ERIs (its bar 1e-4), and
+    J/K against the exact FFT-grid J/K no worse than the oracle's."""
+    from oracle import exact_ref as E
+    from oracle import isdf_ref as R
+    from fisdf.cell import eval_ao_kpts
+    from test_gpu_selection import residual_along
+    cell, kmesh, m0, c0, x0, coords, chi, dm = _toy("toy222")
+    df = coul.FFTDF(cell, eri_ref=_eri_ref(cell, kmesh, chi, coords))
+    ng = int(np.prod(m0))
+    cisdf = (nip + 0.5) / ng
+    c, x = coul.get_coul_svd(df, kmesh=kmesh, cisdf=cisdf, m0=list(m0))
+    isdf = df._isdf
+    assert nip == int(ng * cisdf)
+    nk = int(np.prod(kmesh))
+    assert c.shape == (nk, nip, nip) and x.shape == (nk, nip, cell.nao_nr())
+    perm = isdf.perm
+    assert len(set(perm.tolist())) == nip and abs(x - x0[:, perm]).max() < 1e-12
+    xg = eval_ao_kpts(cell, cell.gen_uniform_grids(m0), (1, 1, 1))[0].real
+    perm_ref, rank_ref, x4g = R.select_points_svd_script(xg, ng, cisdf)
+    sv = np.linalg.eigvalsh(x4g)[::-1]
+    num_rank = int((sv > 1e-12 * sv[0]).sum())
+    before, _ = residual_along(x4g, perm[:num_rank])
+    tie_tol = ng * np.finfo(float).eps * np.diag(x4g).max()
+    gap = max(b.max() - b[perm[j]] for j, b in enumerate(before))
+    print(f"\nsvd script nip {nip}: ng {ng}, Gram numerical rank {num_rank}, GPU factorisation "
+          f"stopped after {isdf.select_rank}, dpstrf after {rank_ref}; largest greedy gap over "
+          f"the first {num_rank} GPU pivots {gap:.1e} (tie tolerance {tie_tol:.1e}); x4_q ranks "
+          f"{np.asarray(isdf.ranks).min()}-{np.asarray(isdf.ranks).max()}")
+    assert gap <= tie_tol
+    out = R.build(x0[:, perm], chi, coords, cell.a, kmesh, cell.mesh, solver="svd")
+    kpts = R.get_kpts(cell.a, kmesh)
+    phase = R.get_phase(cell.a, kpts, kmesh)
+    vj0 = R.get_j_kpts(x0[:, perm], out["w0"], dm)[0]
+    vk0 = R.get_k_kpts(x0[:, perm], out["wq"], dm, phase)[0]
+    vj, vk = isdf.get_jk(dm[0])
+    dj, dk = abs(vj - vj0).max(), abs(vk - vk0).max()
+    print(f"svd script nip {nip}: GPU vs SVD oracle on the same points |dJ| {dj:.2e} |dK| {dk:.2e}")
+    if nip <= num_rank:
+        assert dj < 1e-8 and dk < 1e-8
+        return
+    vje = E.exact_j(chi, dm, cell.a, cell.mesh)[0]
+    vke = E.exact_k(chi, dm, cell.a, cell.mesh, kpts, coords)[0]
+    ej, ek = abs(vj - vje).max(), abs(vk - vke).max()
+    ej0, ek0 = abs(vj0 - vje).max(), abs(vk0 - vke).max()
+    print(f"svd script nip {nip}: vs exact FFT-grid J/K: GPU {ej:.2e} / {ek:.2e}, oracle "
+          f"{ej0:.2e} / {ek0:.2e}")
+    assert ej <= 1.5 * ej0 + 1e-8 and ek <= 1.5 * ek0 + 1e-8
+    rng = np.random.default_rng(1)
+    triples = [tuple(int(t) for t in rng.integers(0, nk, 3)) for _ in range(4)] + [(0, 0, 0)]
+    worst = coul.check_eri(df, kmesh, c, x, tol=1e-4, triples=triples)
+    print(f"svd script nip {nip}: worst ISDF ERI error vs exact {worst:.2e} (the script's bar 1e-4)")
