@@ -517,9 +517,8 @@ int num_cus(int device) {
   return n;
 }
 
-// The fit's extra streams: aux[0] and aux[1] are MFMA lanes, aux[2] the pipelined FFT stream at
-// the device's LEAST priority, so the CU slots it leaves free go to the lanes first (C3 -0.45
-// ms/step over 4 interleaved pairs, profiles/r03_ab/gemm_pipe.log).  All three are created
+// The fit's extra streams: aux[0] and aux[1] are MFMA lanes, aux[2] the pipelined FFT stream (its
+// priority below).  All three are created
 // together and in this order: HIP maps a process's streams onto hardware queues by creation
 // order, and leaving aux[1] uncreated when unused measured +4.5 ms/step (even with 8 queues).
 int ensure_aux(fisdf_ctx* c) {
@@ -527,9 +526,22 @@ int ensure_aux(fisdf_ctx* c) {
   FISDF_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
   int least = 0, greatest = 0;
   FISDF_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  // The FFT stream's priority depends on the HIP runtime the process runs: on the ROCm 7.0
+  // runtime torch bundles the least priority is -0.45 ms/step (the lanes' MFMA kernels take the
+  // CU slots first, r03), but the 7.2 runtime honours it more strictly and starves the FFTs the
+  // lanes wait on: +4.2 ms/step (tools/capi_bench.py, profiles/r04/capi_vs_torch).  So: least
+  // below 7.2, the default priority from 7.2 on.  FISDF_FFT_PRIO: 0 least, 1 default, 2 greatest.
+  static const int fft_prio = [] {
+    const char* e = getenv("FISDF_FFT_PRIO");
+    if (e) return atoi(e);
+    int v = 0;
+    if (hipRuntimeGetVersion(&v) != hipSuccess) return 1;
+    return (v / 10000000 > 7 || (v / 10000000 == 7 && (v / 100000) % 100 >= 2)) ? 1 : 0;
+  }();
   for (int l = 0; l < 3; ++l) {
-    if (l == 2)
-      FISDF_HIP(hipStreamCreateWithPriority(&c->aux[l], hipStreamNonBlocking, least));
+    if (l == 2 && fft_prio != 1)
+      FISDF_HIP(hipStreamCreateWithPriority(&c->aux[l], hipStreamNonBlocking,
+                                            fft_prio == 2 ? greatest : least));
     else
       FISDF_HIP(hipStreamCreateWithFlags(&c->aux[l], hipStreamNonBlocking));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_join[l], hipEventDisableTiming));
@@ -1167,6 +1179,9 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
   // time reversal (fisdf_set_time_reversal): fx_k only for the representatives k <= -k, the
   // others are conj(fx_{-k}) inside kmesh_y — 36 of 64 k at 4x4x4
   const bool half = c->time_reversal;
+#ifdef FISDF_EXP_NOY  // timing experiment only (wrong results)
+  return 0;
+#endif
   if (half && nblk > 0) {
     // fused fx + k-mesh DFT where the k-mesh allows it: no fx round trip through HBM
     bool done = false;
@@ -1942,6 +1957,9 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     StageTimer tm(c, FISDF_ST_FFT, st);
     const cplx* pc = piece_of(lq);
     FISDF_CHECK(pc || yT, "fit_coulomb: q without y");
+#ifdef FISDF_EXP_NOFFT  // timing experiment only (wrong results)
+    return 0;
+#endif
     if (pc && unpack) {  // piece -> (nip, ngrid) rows, stream-ordered before the FFT reads them
       cplx* yb = (cplx*)(b + oP[ub]);
       const char* src = (const char*)pc;
@@ -2015,6 +2033,9 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
                         real_q ? GEMM_A_REAL : GEMM_FULL));
         Uq = U;
       } else if (r == nip) {  // one lower-triangular GEMM with L^{-1}
+#ifdef FISDF_EXP_NOREALTRSM  // timing experiment only (wrong results)
+        if (real_q) { Uq = U; } else
+#endif
         FISDF_TRY(zgemm(st, OP_N, OP_N, nip, (int)ncol, nip, ONE, c->f_Li + (long)sl * nn, nip, 0,
                         Yh, ngrid, 0, ZERO, U, ngrid, 0, 1, 1, nullptr, EPI_NONE, nullptr,
                         GEMM_A_LOWER | (real_q ? GEMM_A_REAL : GEMM_FULL)));

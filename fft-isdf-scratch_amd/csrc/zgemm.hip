@@ -778,6 +778,9 @@ int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cpl
     launch<OP_N, OP_C, true>(s, grid, n, n, K, cmk(alpha, 0), A, lda, 0, A, lda, 0, cmk(0, 0), C,
                              ldc, 0, ksplit, kchunk, work, EPI_NONE, nullptr, 0, ev.span);
   FISDF_HIP(hipGetLastError());
+#ifdef FISDF_EXP_NOREDUCE  // timing experiment only (wrong results): no split-K reduction
+  ksplit = 1;
+#endif
   if (ksplit > 1) {
     const int t32 = (n + 31) / 32;
     hipLaunchKernelGGL(herk_reduce_kernel, dim3(t32 * (t32 + 1) / 2), dim3(256), 0, s, n, ksplit,
