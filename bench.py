@@ -188,7 +188,7 @@ def emulate_ranks(args):
                _lib.ptr(X), nip, nao, km_p, a_p, qs.ctypes.data_as(_lib._ip), len(qs),
                _lib.ptr(yall))
     real_q = np.array([partner[q] == q for q in fit_qs])
-    chunks = kshard.balanced_chunks(np.where(real_q, 0.6, 1.0), N)
+    chunks = kshard.assign_q(np.where(real_q, 0.6, 1.0), N)
     slices = kshard.grid_slices(cell.mesh, N)
     per_rank = []
     for R in range(N) if args.emulate_only is None else [args.emulate_only]:
@@ -224,10 +224,10 @@ def emulate_ranks(args):
     # collective bytes of the worst rank (fp64): the chunked all-to-all of y (its q on the other
     # ranks' slices in, its slice of the others' q out) and the W_s reduce-scatter (real parts)
     R = worst["rank"]
-    a0, a1 = chunks[R]
+    nmine = len(chunks[R])
     ng_self = slices[R][1]
-    a2a_in = (a1 - a0) * nip * (ngrid - ng_self) * 16
-    a2a_out = (len(fit_qs) - (a1 - a0)) * nip * ng_self * 16
+    a2a_in = nmine * nip * (ngrid - ng_self) * 16
+    a2a_out = (len(fit_qs) - nmine) * nip * ng_self * 16
     ws_rs = (N - 1) / N * nk * nip * nip * 8
     out = {"metric": "per-rank compute time of an emulated k-sharded step", "config": args.config,
            "n_ranks": N, "steps": args.steps, "warmup": args.warmup,

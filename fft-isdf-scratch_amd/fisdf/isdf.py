@@ -597,16 +597,15 @@ def build(df_obj):
     x4 = d.empty((nk, nip, nip))
     d.ctx.call("fisdf_build_x4", _lib.ptr(X), nip, nao, km_p, a_p, _lib.ptr(x4))   # :38-48
 
-    # q to fit: time-reversal representatives (W_{-q} = conj(W_q)) or every q, sharded in
-    # contiguous chunks over the ranks
+    # q to fit: time-reversal representatives (W_{-q} = conj(W_q)) or every q, shared among the
+    # ranks by cost: a self-conjugate q fitted with real arithmetic on its half
+    # grid costs about 0.6 of a complex one; longest-first greedy (kshard.assign_q)
     fit_qs, partner, weight = _fit_qset(df_obj, kmesh)
-    # cost-balanced contiguous chunks: a self-conjugate q fitted with real arithmetic costs
-    # about 0.6 of a complex one (half-MFMA TRSM and HERK, same FFT)
     real_q = np.array([bool(df_obj.real_self_conjugate and partner[q] == q) for q in fit_qs])
-    chunks = kshard.balanced_chunks(np.where(real_q, 0.6, 1.0), d.size)
-    a0, a1 = chunks[d.rank]
-    my_qs = np.ascontiguousarray(fit_qs[a0:a1], dtype=np.int32)
-    my_wt = np.ascontiguousarray(weight[a0:a1], dtype=np.float64)
+    parts = kshard.assign_q(np.where(real_q, 0.6, 1.0), d.size)
+    mine = parts[d.rank]
+    my_qs = np.ascontiguousarray(fit_qs[mine], dtype=np.int32)
+    my_wt = np.ascontiguousarray(weight[mine], dtype=np.float64)
     nq = len(my_qs)
     qs_c = my_qs.ctypes.data_as(_lib._ip)
     if df_obj._ao_grid is None:
@@ -657,7 +656,7 @@ def build(df_obj):
         # the all-to-all, split per local q, runs on the collective stream while this rank
         # factorises its x4_q and fits its earlier q
         pieces = kshard.exchange_y_chunked(send, nip, slices, d.rank, d.size, d.comm,
-                                           [b - a for a, b in chunks])
+                                           parts)
 
     ranks = np.zeros(nq, np.int32)
     if nq:
@@ -706,7 +705,7 @@ def build(df_obj):
         Ws = kshard.reduce_scatter_rows(Wsb, chunk, nk * (i1 - i0) * nip, d.rank, d.size,
                                         d.comm, rows=(i0, i1)).reshape(nk, i1 - i0, nip)
         del Wsb
-        owner0 = next(r for r, (a, b) in enumerate(chunks) if b > a)     # fit_qs[0] == 0
+        owner0 = next(r for r, p in enumerate(parts) if 0 in p)          # fit_qs[0] == 0
         W0 = Wq[0].clone() if d.rank == owner0 else d.empty((nip, nip))
         kshard.broadcast_w0(W0, nk, d.comm, src_local=owner0)           # W_0 for get_j
     else:

@@ -47,14 +47,40 @@ class EmulatedGroup:
         self.ws_blocks = None
 
 
-def emulated_pieces(yall, chunks, slices, rank: int):
+def positions(part):
+    """A rank's share of the fitted q as ascending positions in the fit order: an index list
+    (assign_q) or a contiguous (a, b) chunk."""
+    if isinstance(part, tuple) and len(part) == 2:
+        return list(range(int(part[0]), int(part[1])))
+    return [int(i) for i in part]
+
+
+def emulated_pieces(yall, parts, slices, rank: int):
     """The all-to-all pieces rank `rank` receives, built from the full y of every fitted q
     (yall: (nq_all, nip, ngrid) in fit order): its j-th q on each slice p, concatenated in rank
-    order p — exactly the layout exchange_y_chunked hands to the unpack."""
+    order p — exactly the layout exchange_y_chunked hands to the fit."""
     import torch
-    a0, a1 = chunks[rank]
-    return [torch.cat([yall[a0 + j, :, g0:g0 + ng].reshape(-1) for g0, ng in slices])
-            for j in range(a1 - a0)]
+    return [torch.cat([yall[i, :, g0:g0 + ng].reshape(-1) for g0, ng in slices])
+            for i in positions(parts[rank])]
+
+
+def assign_q(costs, size: int):
+    """Share the fitted q (in fit order, with their relative fit costs) among `size` ranks:
+    longest-processing-time greedy (most expensive q first, each to the least loaded rank; ties to
+    the lower rank), each rank's positions ascending.  Unlike contiguous chunks a rank may own
+    q from anywhere in the list: at C3 x8 (28 complex q of cost 1, 8 self-conjugate of 0.6) the
+    largest share is 4.2 instead of the 5.0 of the best contiguous split.  The 1-GPU and N-rank
+    builds give the same W_q bit for bit whatever the assignment (a q's arithmetic never depends
+    on its companions)."""
+    import numpy as np
+    c = np.asarray(costs, dtype=float)
+    load = [0.0] * size
+    parts = [[] for _ in range(size)]
+    for i in sorted(range(len(c)), key=lambda i: (-c[i], i)):
+        r = min(range(size), key=lambda r: (load[r], r))
+        parts[r].append(i)
+        load[r] += c[i]
+    return [sorted(p) for p in parts]
 
 
 def _emulated(group):
@@ -90,37 +116,6 @@ def shard_list(items, rank: int, size: int):
     """Contiguous, balanced chunk of `items` owned by `rank`."""
     a, b = shard_range(len(items), rank, size)
     return items[a:b]
-
-
-def balanced_chunks(costs, size: int):
-    """Split items (in order) into `size` contiguous chunks minimising the largest chunk cost
-    (linear partition by binary search on the bound).  Returns [(a, b)] per rank."""
-    import numpy as np
-    c = np.asarray(costs, dtype=float)
-    n = len(c)
-    if size <= 1 or n == 0:
-        return [(0, n)] + [(n, n)] * (size - 1)
-
-    def split(bound):
-        out, a, acc = [], 0, 0.0
-        for i in range(n):
-            if acc + c[i] > bound + 1e-12 and i > a:
-                out.append((a, i))
-                a, acc = i, 0.0
-            acc += c[i]
-        out.append((a, n))
-        return out
-
-    lo, hi = float(c.max()), float(c.sum())
-    for _ in range(60):
-        mid = 0.5 * (lo + hi)
-        if len(split(mid)) <= size:
-            hi = mid
-        else:
-            lo = mid
-    out = split(hi)
-    out += [(n, n)] * (size - len(out))
-    return out
 
 
 def owner_of(q: int, nk: int, size: int) -> int:
@@ -173,19 +168,21 @@ def exchange_y(send, nk: int, nip: int, slices, rank: int, size: int, group=None
     return (recv, work) if async_op else recv
 
 
-def exchange_y_chunked(send, nip: int, slices, rank: int, size: int, group, counts):
+def exchange_y_chunked(send, nip: int, slices, rank: int, size: int, group, parts):
     """The all-to-all of exchange_y split per local q index j, so the fit of a rank's j-th q
     can start as soon as its own piece has arrived (the later pieces move over xGMI while
-    the earlier q are fitted).  `send` is (nq_all, nip, ng_rank) in rank-chunk order with
-    counts[r] q per rank.  Returns [(recv_j, work_j)] for j < counts[rank]; recv_j is
-    concat_p (nip, ng_p); call work_j.wait() (may be None) before reading recv_j."""
+    the earlier q are fitted).  `send` is (nq_all, nip, ng_rank) in fit order; parts[r] are
+    rank r's positions in it (assign_q, or contiguous (a, b) chunks).  Returns [(recv_j, work_j)]
+    for the rank's j-th q; recv_j is concat_p (nip, ng_p); call work_j.wait() (may be None)
+    before reading recv_j."""
     import torch
     import torch.distributed as dist
+    pos = [positions(p) for p in parts]
+    counts = [len(p) for p in pos]
     if _emulated(group):
         ngrid = sum(ng for _, ng in slices)
         return [(group.pieces[j] if group.pieces is not None else
                  send.new_empty(nip * ngrid), None) for j in range(counts[rank])]
-    starts = [sum(counts[:r]) for r in range(size)]
     ng_self = slices[rank][1]
     nmax = max(counts) if counts else 0
     out = []
@@ -199,7 +196,7 @@ def exchange_y_chunked(send, nip: int, slices, rank: int, size: int, group, coun
         rj = torch.empty(sum(out_splits), dtype=send.dtype, device=send.device)
         if host:
             dst = [r for r in range(size) if j < counts[r]]
-            idx = torch.tensor([starts[r] + j for r in dst], dtype=torch.long)
+            idx = torch.tensor([pos[r][j] for r in dst], dtype=torch.long)
             sj = hs.index_select(0, idx).reshape(-1) if len(dst) else hs.new_empty(0)
             hr = rj.cpu()
             dist.all_to_all_single(torch.view_as_real(hr), torch.view_as_real(sj),
@@ -208,10 +205,10 @@ def exchange_y_chunked(send, nip: int, slices, rank: int, size: int, group, coun
                 rj.copy_(hr)
             work = None
         else:
-            # the piece for rank r is send[starts[r] + j], a contiguous (nip, ng_self) block: the
+            # the piece for rank r is send[pos[r][j]], a contiguous (nip, ng_self) block: the
             # list form sends every piece from its place (no gather copy of the send buffer)
             empty = torch.view_as_real(send.new_empty(0))
-            ins = [torch.view_as_real(send[starts[r] + j].reshape(-1)) if j < counts[r] else empty
+            ins = [torch.view_as_real(send[pos[r][j]].reshape(-1)) if j < counts[r] else empty
                    for r in range(size)]
             outs, off = [], 0
             for n in out_splits:

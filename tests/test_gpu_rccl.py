@@ -75,7 +75,7 @@ def test_emulated_rank_reproduces_its_q(name, n):
                _lib.ptr(X), nip, nao, km_p, a_p, qs.ctypes.data_as(_lib._ip), len(qs),
                _lib.ptr(yall))
     real_q = np.array([partner[q] == q for q in fit_qs])
-    chunks = kshard.balanced_chunks(np.where(real_q, 0.6, 1.0), n)
+    chunks = kshard.assign_q(np.where(real_q, 0.6, 1.0), n)
     slices = kshard.grid_slices(cell.mesh, n)
     for R in range(n):
         df = ISDF(cell, cell.get_kpts(kmesh), m0=list(m0), c0=c0,

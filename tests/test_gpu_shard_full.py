@@ -73,7 +73,7 @@ def run_emulated(cfg, n, fit):
     nk, nip = int(np.prod(kmesh)), df1.nip
     yall, fit_qs, partner = _full_y(df1)
     real_q = np.array([partner[q] == q for q in fit_qs])
-    chunks = kshard.balanced_chunks(np.where(real_q, 0.6, 1.0), n)
+    chunks = kshard.assign_q(np.where(real_q, 0.6, 1.0), n)
     slices = kshard.grid_slices(cell.mesh, n)
     ws_sum = torch.zeros_like(ws1)
     vj_sum = np.zeros_like(vj1)

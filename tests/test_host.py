@@ -89,17 +89,24 @@ def test_time_reversal_reps():
         assert covered == set(range(nk))
 
 
-def test_balanced_chunks():
-    from fisdf.kshard import balanced_chunks
+def test_assign_q():
+    """Longest-first sharing of the fitted q: every q once, ascending per rank, and at C3 x 8 (28
+    complex q of cost 1, 8 self-conjugate of 0.6) the largest share is 4.2 (the best contiguous
+    split: 5.0)."""
+    from fisdf.kshard import assign_q, positions
     for costs, size in [([1.0] * 36, 8), ([0.6] * 8 + [1.0] * 28, 8), ([1.0] * 3, 8),
-                        ([0.6, 1.0, 1.0, 0.6, 1.0], 2), ([], 3)]:
-        ch = balanced_chunks(costs, size)
-        assert len(ch) == size
-        assert ch[0][0] == 0 and ch[-1][1] == len(costs)
-        assert all(a <= b for a, b in ch) and all(ch[i][1] == ch[i + 1][0] for i in range(size - 1))
+                        ([0.6, 1.0, 1.0, 0.6, 1.0], 2), ([], 3), ([1.0] * 5, 1)]:
+        parts = assign_q(costs, size)
+        assert len(parts) == size
+        flat = sorted(i for p in parts for i in p)
+        assert flat == list(range(len(costs)))
+        assert all(p == sorted(p) for p in parts)
         if costs:
-            worst = max(sum(costs[a:b]) for a, b in ch)
-            assert worst <= max(max(costs), sum(costs) / size) + max(costs) + 1e-9
+            worst = max(sum(costs[i] for i in p) for p in parts)
+            assert worst <= sum(costs) / size + max(costs) + 1e-9
+    c3 = [1.0, 1.0, 0.6] + [1.0] * 25 + [0.6] * 8   # any order of 28 complex + 8 real
+    assert abs(max(sum(c3[i] for i in p) for p in assign_q(c3, 8)) - 4.2) < 1e-9
+    assert positions((2, 5)) == [2, 3, 4] and positions([7, 1]) == [7, 1]
 
 
 def test_shard_ranges():
@@ -224,15 +231,15 @@ def _worker_y(rank, size, port, result):
     kshard.allreduce_sum(t, None)
     full = sum(x0[q].conj() @ x0[q].T for q in range(nk))
     err_g = abs(t.numpy() - full).max() / abs(full).max()
-    # chunked exchange of the time-reversal representatives over cost-balanced chunks
+    # chunked exchange of the time-reversal representatives, shared by cost (assign_q: a rank's
+    # q need not be contiguous in the send buffer)
     reps, partner, _ = kshard.time_reversal_reps(kmesh)
     costs = [0.6 if partner[q] == q else 1.0 for q in reps]
-    chunks = kshard.balanced_chunks(costs, size)
-    counts = [b - a for a, b in chunks]
+    parts = kshard.assign_q(costs, size)
     send = torch.from_numpy(np.ascontiguousarray(yb[reps]))
-    pieces = kshard.exchange_y_chunked(send, nip, slices, rank, size, None, counts)
-    a0, a1 = chunks[rank]
-    assert len(pieces) == a1 - a0
+    pieces = kshard.exchange_y_chunked(send, nip, slices, rank, size, None, parts)
+    mine = parts[rank]
+    assert len(pieces) == len(mine)
     err_c = 0.0
     for j, (rj, work) in enumerate(pieces):
         if work is not None:
@@ -243,7 +250,7 @@ def _worker_y(rank, size, port, result):
         for (p0, npg) in slices:
             yq[:, p0:p0 + npg] = rj[off:off + nip * npg].reshape(nip, npg)
             off += nip * npg
-        err_c = max(err_c, abs(yq - o["y"][reps[a0 + j]].T).max() / abs(o["y"]).max())
+        err_c = max(err_c, abs(yq - o["y"][reps[mine[j]]].T).max() / abs(o["y"]).max())
     # real-part all-reduce of W_s-like data (imaginary part zero)
     w = torch.from_numpy((np.arange(12.0) * (rank + 1)).astype(complex))
     kshard.allreduce_real_part(w, None)
