@@ -78,6 +78,21 @@ struct fisdf_ctx {
   int fit_mode = 0;
   cplx* f_M = nullptr;          // (nk, nip, nip) minimum-norm operators A^+ (rows < rank)
   std::vector<char> f_cod;      // slot fitted through its minimum-norm operator
+  std::vector<char> f_pslot;    // slot factored by the pivoted (rank-revealing) path
+  // the fit's pipelined-FFT ring (Yhat slots), kept outside the arena so the FFTs of the first
+  // slots can be enqueued before the factor's verdict (fisdf_fit_coulomb_qs)
+  cplx* f_ring = nullptr;
+  size_t f_ring_bytes = 0;
+  hipEvent_t ev_spec = nullptr;
+  // grow-only temporaries instead of the stream-ordered pool (hipMallocAsync): on the HIP 7.2
+  // runtime a block freed on one stream was handed to another stream's allocation while the
+  // first still used it (torch-free C-ABI build: the pivoted factor's ranks corrupted by the
+  // Coulomb weights computed beside it on the FFT stream).  ws_main: the main stream's;
+  // ws_side_a / ws_side_b: the factorisation's (side stream)
+  struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+  } ws_main, ws_side_a, ws_side_b;
   int* f_nip_dev = nullptr;     // device copy of nip (scatter of a full W_PP)
   int lanes = 0;           // fisdf_set_fit_lanes; 0: environment FISDF_FIT_LANES / default
   bool time_reversal = false;  // fisdf_set_time_reversal: fx_{-k} = conj(fx_k) in build_y
@@ -153,6 +168,23 @@ void set_ctx_error(fisdf_ctx* c, const std::string& msg) { c->last_error = msg; 
 }  // namespace fisdf
 
 namespace {
+
+// a grow-only temporary (growth waits for the device: the old block may be in use on any stream)
+static int devbuf_get(fisdf_ctx::DevBuf& w, size_t bytes, void** out) {
+  bytes = std::max<size_t>(bytes, 256);
+  if (bytes > w.n) {
+    if (w.p) {
+      FISDF_HIP(hipDeviceSynchronize());
+      FISDF_HIP(hipFree(w.p));
+    }
+    w.p = nullptr;
+    w.n = 0;
+    FISDF_HIP(hipMalloc(&w.p, bytes));
+    w.n = bytes;
+  }
+  *out = w.p;
+  return 0;
+}
 
 int arena_get(fisdf_ctx* c, size_t bytes, void** out) {
   bytes = std::max<size_t>(bytes, 256);
@@ -373,11 +405,10 @@ int select_gram(fisdf_ctx* c, const cplx* x0, int nk, int q0, int q1, int ng0, i
   int ks = 1;
   const long tiles = (long)((ng0 + 63) / 64) * ((ng0 + 63) / 64 + 1) / 2;
   while (tiles * ks < 512 && K / (ks * 2) >= 256) ks *= 2;
-  cplx* work = nullptr;
-  if (ks > 1) FISDF_HIP(hipMallocAsync((void**)&work, sizeof(cplx) * (size_t)ks * ng0 * ng0, c->stream));
+  void* work = nullptr;
+  if (ks > 1) FISDF_TRY(devbuf_get(c->ws_main, sizeof(cplx) * (size_t)ks * ng0 * ng0, &work));
   // only Re(x2) enters the selection (fftisdf.py:379): real-part HERK, imaginary part zero
-  FISDF_TRY(herk(c->stream, ng0, K, 1.0, tmp, K, x2, ng0, ks, work, GEMM_RE_ONLY));
-  if (work) FISDF_HIP(hipFreeAsync(work, c->stream));
+  FISDF_TRY(herk(c->stream, ng0, K, 1.0, tmp, K, x2, ng0, ks, (cplx*)work, GEMM_RE_ONLY));
   (void)nk;
   return 0;
 }
@@ -420,13 +451,15 @@ int get_weight(fisdf_ctx* c, hipStream_t st, const int mesh[3], const int kmesh[
     if (!half) {
       FISDF_TRY(coulg_weight(st, mesh, g, kq, scale, 1, w, c->omega));
     } else {
+      // a cache fill: plain allocations (no stream-ordered pool memory shared with other streams)
       double* cw = nullptr;
-      FISDF_HIP(hipMallocAsync((void**)&cw, sizeof(double) * ng, st));
+      FISDF_HIP(hipMalloc((void**)&cw, sizeof(double) * ng));
       FISDF_TRY(coulg_weight(st, mesh, g, kq, scale, 0, cw, c->omega));
       int m[3];
       self_conjugate_m(kmesh, q, m);
       FISDF_TRY(half_weight(st, w, cw, mesh, m));
-      FISDF_HIP(hipFreeAsync(cw, st));
+      FISDF_HIP(hipStreamSynchronize(st));
+      FISDF_HIP(hipFree(cw));
     }
     FISDF_HIP(hipStreamSynchronize(st));
     it = c->wt_cache.emplace(key, w).first;
@@ -452,14 +485,14 @@ int get_asym_half(fisdf_ctx* c, hipStream_t st, const int mesh[3], const int kme
     double* cw = nullptr;
     FISDF_HIP(hipMalloc(&as.idx, sizeof(int) * (ngrid + 1)));
     FISDF_HIP(hipMalloc(&as.f, sizeof(double) * ngrid));
-    FISDF_HIP(hipMallocAsync((void**)&cw, sizeof(double) * ngrid, st));
+    FISDF_HIP(hipMalloc((void**)&cw, sizeof(double) * ngrid));  // a cache fill (see get_weight)
     FISDF_TRY(coulg_weight(st, mesh, g, kq, scale, 0, cw, c->omega));
     int m[3];
     self_conjugate_m(kmesh, q, m);
     FISDF_TRY(asym_half(st, cw, mesh, m, as.idx, as.f, as.idx + ngrid));
-    FISDF_HIP(hipFreeAsync(cw, st));
     FISDF_HIP(hipMemcpyAsync(&as.n, as.idx + ngrid, sizeof(int), hipMemcpyDeviceToHost, st));
     FISDF_HIP(hipStreamSynchronize(st));
+    FISDF_HIP(hipFree(cw));
     it = c->asym_cache.emplace(key, as).first;
   }
   *out = &it->second;
@@ -643,6 +676,10 @@ int fisdf_destroy(fisdf_ctx* c) {
   if (c->f_pending) (void)hipEventSynchronize(c->ev_fac);
   free_factors(c);
   if (c->f_scratch) (void)hipFree(c->f_scratch);
+  if (c->f_ring) (void)hipFree(c->f_ring);
+  for (auto* w : {&c->ws_main, &c->ws_side_a, &c->ws_side_b})
+    if (w->p) (void)hipFree(w->p);
+  if (c->ev_spec) (void)hipEventDestroy(c->ev_spec);
   if (c->side) {
     (void)hipStreamSynchronize(c->side);
     (void)hipStreamDestroy(c->side);
@@ -840,9 +877,11 @@ int fisdf_min_norm_operator(fisdf_ctx* c, const void* A, int n, double tol_rel, 
   void* base;
   FISDF_TRY(arena_get(c, cv.off, &base));
   char* b = (char*)base;
+  void* trail = nullptr;
+  FISDF_TRY(devbuf_get(c->ws_main, sizeof(cplx) * pchol_trail_elems(n, 1), &trail));
   FISDF_TRY(pchol(c->stream, (const cplx*)A, n, (long)n * n, n, 1, n, tol_rel, 0.0, (cplx*)(b + oL),
                   (int*)(b + oP), (int*)(b + oR), (double*)(b + oD), (int*)(b + oF),
-                  (double*)(b + oW)));
+                  (double*)(b + oW), (cplx*)trail));
   int r = 0;
   FISDF_HIP(hipMemcpyAsync(&r, b + oR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   FISDF_HIP(hipStreamSynchronize(c->stream));
@@ -872,9 +911,11 @@ int fisdf_pivoted_cholesky(fisdf_ctx* c, const void* A, int n, int batch, int rm
   void* base;
   FISDF_TRY(arena_get(c, cv.off, &base));
   char* b = (char*)base;
+  void* trail = nullptr;
+  FISDF_TRY(devbuf_get(c->ws_main, sizeof(cplx) * pchol_trail_elems(n, batch), &trail));
   FISDF_TRY(pchol(c->stream, (const cplx*)A, n, (long)n * n, n, batch, rmax, tol_rel, 0.0,
                   (cplx*)(b + oL), (int*)(b + oP), (int*)(b + oR), (double*)(b + oD),
-                  (int*)(b + oF), (double*)(b + oW)));
+                  (int*)(b + oF), (double*)(b + oW), (cplx*)trail));
   FISDF_HIP(hipMemcpyAsync(h_piv, b + oP, sizeof(int) * (size_t)batch * rmax,
                            hipMemcpyDeviceToHost, c->stream));
   FISDF_HIP(hipMemcpyAsync(h_rank, b + oR, sizeof(int) * batch, hipMemcpyDeviceToHost, c->stream));
@@ -942,7 +983,10 @@ static int select_pivots_dev(fisdf_ctx* c, const cplx* X2, double scale, int ng0
                                 flags, &handled, pass == 0, &coop_err));
     if (!handled) {
       FISDF_TRY(square_scale(c->stream, X2, scale, X4, (long)ng0 * ng0));
-      FISDF_TRY(pchol(c->stream, X4, ng0, 0, ng0, 1, nip_max, tol, 0.0, L, piv, rank, d, flags, w));
+      void* trail = nullptr;
+      FISDF_TRY(devbuf_get(c->ws_main, sizeof(cplx) * pchol_trail_elems(ng0, 1), &trail));
+      FISDF_TRY(pchol(c->stream, X4, ng0, 0, ng0, 1, nip_max, tol, 0.0, L, piv, rank, d, flags, w,
+                      (cplx*)trail));
     }
     int* hp = c->sel_pinned;
     hp[0] = 0;
@@ -1310,8 +1354,11 @@ int factor_pivoted(fisdf_ctx* c, hipStream_t s) {
   size_t oD = cv.take(sizeof(double) * (size_t)nk * nip);
   size_t oF = cv.take(sizeof(int) * nk);
   size_t oW = cv.take(sizeof(double) * (size_t)nk * (1 + nip));
+  void* trail = nullptr;
+  FISDF_TRY(devbuf_get(c->ws_side_b, sizeof(cplx) * pchol_trail_elems(nip, nk), &trail));
   FISDF_TRY(pchol(s, c->f_x4s, nip, nn, nip, nk, nip, c->f_tol, 0.0, c->f_L, c->f_piv,
-                  (int*)(b + oR), (double*)(b + oD), (int*)(b + oF), (double*)(b + oW)));
+                  (int*)(b + oR), (double*)(b + oD), (int*)(b + oF), (double*)(b + oW),
+                  (cplx*)trail));
   c->f_used_pivoted = true;
   return factor_finish(c, s, (const int*)(b + oR), true);
 }
@@ -1329,16 +1376,18 @@ int factor_pivoted_slots(fisdf_ctx* c, hipStream_t s, const std::vector<int>& sl
   size_t oF = cv.take(sizeof(int) * nk);
   size_t oW = cv.take(sizeof(double) * (size_t)nk * (1 + nip));
   size_t oU = cv.take(sizeof(int) * nk);  // the unpivoted path's per-slot ranks
-  cplx *A = nullptr, *L = nullptr;
-  int* P = nullptr;
-  FISDF_HIP(hipMallocAsync((void**)&A, sizeof(cplx) * nf * nn, s));
-  FISDF_HIP(hipMallocAsync((void**)&L, sizeof(cplx) * nf * nn, s));
-  FISDF_HIP(hipMallocAsync((void**)&P, sizeof(int) * (size_t)nf * nip, s));
+  void* wa = nullptr;
+  FISDF_TRY(devbuf_get(c->ws_side_a, sizeof(cplx) * 2 * nf * nn + sizeof(int) * (size_t)nf * nip, &wa));
+  cplx* A = (cplx*)wa;
+  cplx* L = A + nf * nn;
+  int* P = (int*)(L + nf * nn);
+  void* trail = nullptr;
+  FISDF_TRY(devbuf_get(c->ws_side_b, sizeof(cplx) * pchol_trail_elems(nip, nf), &trail));
   for (int j = 0; j < nf; ++j)
     FISDF_HIP(hipMemcpyAsync(A + j * nn, c->f_x4s + slots[j] * nn, sizeof(cplx) * nn,
                              hipMemcpyDeviceToDevice, s));
   FISDF_TRY(pchol(s, A, nip, nn, nip, nf, nip, c->f_tol, 0.0, L, P, (int*)(b + oR),
-                  (double*)(b + oD), (int*)(b + oF), (double*)(b + oW)));
+                  (double*)(b + oD), (int*)(b + oF), (double*)(b + oW), (cplx*)trail));
   for (int j = 0; j < nf; ++j) {
     const int i = slots[j];
     FISDF_HIP(hipMemcpyAsync(c->f_L + i * nn, L + j * nn, sizeof(cplx) * nn, hipMemcpyDeviceToDevice, s));
@@ -1347,9 +1396,6 @@ int factor_pivoted_slots(fisdf_ctx* c, hipStream_t s, const std::vector<int>& sl
     FISDF_HIP(hipMemcpyAsync((int*)(b + oU) + i, (int*)(b + oR) + j, sizeof(int),
                              hipMemcpyDeviceToDevice, s));
   }
-  FISDF_HIP(hipFreeAsync(A, s));
-  FISDF_HIP(hipFreeAsync(L, s));
-  FISDF_HIP(hipFreeAsync(P, s));
   c->f_used_pivoted = true;
   return factor_finish(c, s, (const int*)(b + oU), true);
 }
@@ -1455,6 +1501,7 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   char* b = (char*)c->f_scratch;
   c->f_qs.assign(h_qs, h_qs + nq);
   c->f_real.assign(nq, 0);
+  c->f_pslot.assign(nq, 0);
   for (int i = 0; kmesh && i < nq; ++i) c->f_real[i] = self_conjugate(kmesh, h_qs[i]) ? 1 : 0;
   c->f_nk = nk;
   c->f_nip = nip;
@@ -1482,6 +1529,7 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   FISDF_TRY(stage_x4(s, (const cplx*)x4all, c->f_qr_dev, nq, nn, c->f_x4s, pivoted ? nullptr : c->f_L));
   if (pivoted) {
     FISDF_TRY(factor_pivoted(c, s));
+    c->f_pslot.assign(nq, 1);
     c->f_check_fail = false;
   } else {
     // full-rank fast path: unpivoted blocked Cholesky (all pivots > tol_rel * max diag is the
@@ -1636,8 +1684,9 @@ static int build_min_norm(fisdf_ctx* c, bool* built) {
   FISDF_HIP(hipMemcpy(c->f_nip_dev, &nip, sizeof(int), hipMemcpyHostToDevice));
   hipStream_t s = c->side;
   const size_t wb = (min_norm_work_bytes(nip, nip) + 255) / 256 * 256;
-  char* work = nullptr;
-  FISDF_HIP(hipMallocAsync((void**)&work, wb + sizeof(int) * 3 * (size_t)nk, s));
+  void* wv = nullptr;
+  FISDF_TRY(devbuf_get(c->ws_side_b, wb + sizeof(int) * 3 * (size_t)nk, &wv));
+  char* work = (char*)wv;
   int* fail = (int*)(work + wb);
   for (int q = 0; q < nk; ++q)
     if (c->f_cod[q])
@@ -1645,7 +1694,6 @@ static int build_min_norm(fisdf_ctx* c, bool* built) {
                                   c->f_rank[q], c->f_M + q * nn, nip, work, fail + 3 * q));
   std::vector<int> hf(3 * (size_t)nk, 0);
   FISDF_HIP(hipMemcpyAsync(hf.data(), fail, sizeof(int) * 3 * nk, hipMemcpyDeviceToHost, s));
-  FISDF_HIP(hipFreeAsync(work, s));
   FISDF_HIP(hipEventRecord(c->ev_fac, s));
   FISDF_HIP(hipEventSynchronize(c->ev_fac));
   for (int q = 0; q < nk; ++q)
@@ -1668,6 +1716,7 @@ int fisdf_factor_x4_wait(fisdf_ctx* c, int* h_ranks) {
         if (c->f_fail_pinned[q] != 0) failed.push_back(q);
       c->f_check_fail = false;
       if (!failed.empty()) {  // not numerically full rank at tol: rank-revealing factorisation
+        for (int q : failed) c->f_pslot[q] = 1;
         FISDF_TRY(factor_pivoted_slots(c, c->side, failed));
         FISDF_HIP(hipEventRecord(c->ev_fac, c->side));
         FISDF_HIP(hipEventSynchronize(c->ev_fac));
@@ -1765,7 +1814,6 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   auto piece_of = [&](int lq) -> const cplx* {
     return lq < (int)c->y_piece.size() ? c->y_piece[lq] : nullptr;
   };
-  FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
   const long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
   const long nn = (long)nip * nip;
   const int nb = c->f_nb;
@@ -1775,6 +1823,114 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   const double vol = cell_volume(a);
   const cplx* yT = (const cplx*)yTv;
   cplx* Wq = (cplx*)Wqv;
+  // what does not depend on the factor's verdict: the lanes, the pipelined-FFT ring, the pieces
+  // q are processed on NL "lanes" (the main stream and aux streams), each with its own
+  // workspaces, so one q's HBM-bound FFT and memory-stalled HERK overlap another q's
+  // MFMA-bound TRSM on the same CUs
+  int NL = std::min(nq, c->lanes > 0 ? c->lanes : env_fit_lanes());
+  // Pipelined FFTs (default with >= 2 lanes; fisdf_set_fit_pipe / FISDF_FIT_PIPE=0 turn it
+  // off): the HBM-bound FFTs run on their own stream into a ring of D Yhat slots, ahead of the
+  // MFMA lanes, which wait per q on its event — the FFTs then overlap TRSM/HERK work instead of
+  // meeting another lane's FFT.  A slot is reused once the lane that read it records its
+  // `free` event, so the working set is D x nip x ngrid (D = lanes + 2 by default) whatever
+  // nq is.  With a single MFMA lane it is slower (C3 107.8 vs 100.9 ms/step), so one lane
+  // keeps the FFT in-lane.
+  const int pipe_mode = c->pipe_mode >= 0 ? c->pipe_mode : env_fit_pipe();
+  bool pipe = pipe_mode != 0 && nq > 1 && NL > 1;
+  // sharded build (fisdf_mark_y_ready): y of the call's j-th q lands at ev_ready[j] on the main
+  // stream (all-to-all piece + unpack); the lanes then run on the aux streams only and each q
+  // starts as soon as its own piece is there, one call for the whole shard
+  int nready = 0;
+  for (int lq = 0; lq < nq; ++lq)
+    nready += (lq < (int)c->ready_marked.size() && c->ready_marked[lq]) ? 1 : 0;
+  FISDF_CHECK(nready == 0 || nready == nq, "fit_coulomb: mark every q of the call ready, or none");
+  const bool ready = nready > 0;
+  if (pipe) NL = std::min(NL, ready ? 2 : 3);  // aux[2] is the FFT stream
+  if (ready) NL = std::min(NL, 3);
+  int D = pipe ? std::min(nq, c->pipe_depth > 0 ? c->pipe_depth : default_pipe_depth(NL)) : 0;
+  if (pipe) {
+    // the ring outside the arena (nip rows per slot, whatever the ranks turn out to be); without
+    // the memory for it, the in-lane FFT
+    const size_t rb = sizeof(cplx) * (size_t)D * nip * ngrid;
+    if (rb > c->f_ring_bytes) {
+      if (c->f_ring) FISDF_HIP(hipFree(c->f_ring));
+      c->f_ring = nullptr;
+      c->f_ring_bytes = 0;
+      if (hipMalloc(&c->f_ring, rb) == hipSuccess) {
+        c->f_ring_bytes = rb;
+      } else {
+        (void)hipGetLastError();
+        c->f_ring = nullptr;
+        pipe = false;
+        D = 0;
+      }
+    }
+  }
+  if (pipe) {
+    while ((int)c->ev_q.size() < nq) {
+      hipEvent_t e;
+      FISDF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c->ev_q.push_back(e);
+    }
+    while ((int)c->ev_free.size() < D) {
+      hipEvent_t e;
+      FISDF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c->ev_free.push_back(e);
+    }
+  }
+  bool any_piece = false;
+  for (int lq = 0; lq < nq; ++lq) any_piece = any_piece || piece_of(lq) != nullptr;
+  // all-to-all pieces of a mesh whose first FFT pass cannot read plane slices in place (no
+  // register kernel, plane too large for the LDS plane kernel): each FFT-issuing stream (the FFT
+  // stream, or every lane) unpacks its q's piece into a (nip, ngrid) buffer of its own first
+  const bool unpack = any_piece && !fft3d_reads_slices(mesh[0], mesh[1], mesh[2]);
+  const PlaneRef* planes = nullptr;
+  if (any_piece && !unpack) FISDF_TRY(plane_table(c, mesh, nip, &planes));
+  FISDF_CHECK(yT != nullptr || any_piece, "fit_coulomb: no y");
+  // sqrt(coulG(k_q+G) vol/N^2)  (:114-115 and the Parseval 1/N of :118), cached per q
+  const double wscale = vol / ((double)ngrid * ngrid);
+  static const int half_env = [] {
+    const char* e = getenv("FISDF_HALF_G");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  const bool half_on = (c->half_grid >= 0 ? c->half_grid : half_env) != 0;
+  auto half_of = [&](int sl) { return half_on && c->f_real[sl] != 0; };
+  auto weight_q = [&](hipStream_t st, int lq, const double** w) {
+    return get_weight(c, st, mesh, kmesh, a, h_qs[lq], wscale, half_of(s0 + lq), w);
+  };
+  auto slot_y = [&](int lq) { return c->f_ring + (long)(lq % D) * nip * ngrid; };
+  // Speculative FFTs (k-sharded builds, where the factor chain is on the critical path): while the
+  // factorisation is still running on the side stream with its unpivoted full-rank fast path
+  // pending, the ring's first D q are transformed assuming that verdict (all nip rows, pivot order
+  // = identity); after the verdict a q the assumption missed is transformed again
+  std::vector<char> spec(nq, 0);
+  static const bool spec_on = [] {
+    const char* e = getenv("FISDF_FIT_SPEC");
+    return !(e && e[0] == '0');
+  }();
+  if (spec_on && pipe && !unpack && c->f_pending && c->f_check_fail && c->fit_mode != FISDF_FIT_SVD) {
+    FISDF_TRY(ensure_aux(c));
+    if (!c->ev_spec) FISDF_HIP(hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming));
+    hipStream_t fs = c->aux[2];
+    FISDF_HIP(hipEventRecord(c->ev_spec, c->stream));  // after the y build / the pieces' marks
+    FISDF_HIP(hipStreamWaitEvent(fs, c->ev_spec, 0));
+    for (int lq = 0; lq < D; ++lq) {
+      double kq[3], kd[3];
+      kpoint(kmesh, g, h_qs[lq], kq);
+      for (int i = 0; i < 3; ++i) kd[i] = g.a[i][0] * kq[0] + g.a[i][1] * kq[1] + g.a[i][2] * kq[2];
+      const double* wt = nullptr;
+      FISDF_TRY(weight_q(fs, lq, &wt));
+      if (ready) FISDF_HIP(hipStreamWaitEvent(fs, c->ev_ready[lq], 0));
+      StageTimer tm(c, FISDF_ST_FFT, fs);
+      const cplx* pc = piece_of(lq);
+      FISDF_TRY(fft3d(fs, pc ? pc : yT + (long)lq * nip * ngrid, ngrid, nullptr, slot_y(lq), ngrid, nip,
+                      mesh[0], mesh[1], mesh[2], kd, wt, nullptr, pc ? planes : nullptr));
+      FISDF_HIP(hipEventRecord(c->ev_q[lq], fs));
+      spec[lq] = 1;
+    }
+    if (getenv("FISDF_DBG_SPEC_SYNC")) FISDF_HIP(hipStreamSynchronize(fs));
+  }
+  FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
   int rmax = 0;
   for (int lq = 0; lq < nq; ++lq) rmax = std::max(rmax, c->f_rank[s0 + lq]);
   // minimum-norm slots transform all nip rows of y (the operator A^+ mixes every row)
@@ -1792,13 +1948,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   int ks = 1;
   for (int lq = 0; lq < nq; ++lq) ks = std::max(ks, ks_of(c->f_rank[s0 + lq], ngrid));
   // a self-conjugate q is fitted on the prefix planes of its Hermitian G pairs (about half the
-  // grid): Re W = sum over one member of each pair with the pair's combined weight
-  static const int half_env = [] {
-    const char* e = getenv("FISDF_HALF_G");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  const bool half_on = (c->half_grid >= 0 ? c->half_grid : half_env) != 0;
-  auto half_of = [&](int sl) { return half_on && c->f_real[sl] != 0; };
+  // grid): Re W = sum over one member of each pair with the pair's combined weight (half_of)
   auto ncols_of = [&](int lq) -> long {
     if (!half_of(s0 + lq)) return ngrid;
     int m[3];
@@ -1807,77 +1957,16 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   };
   const long rr = (long)rmax * rmax;
   const long sLi = (long)nblk * nb * nb;
-  // q are processed on NL "lanes" (the main stream and aux streams), each with its own
-  // workspaces, so one q's HBM-bound FFT and memory-stalled HERK overlap another q's
-  // MFMA-bound TRSM on the same CUs
-  int NL = std::min(nq, c->lanes > 0 ? c->lanes : env_fit_lanes());
-  // Pipelined FFTs (default with >= 2 lanes; fisdf_set_fit_pipe / FISDF_FIT_PIPE=0 turn it
-  // off): the HBM-bound FFTs run on their own stream into a ring of D Yhat slots, ahead of the
-  // MFMA lanes, which wait per q on its event — the FFTs then overlap TRSM/HERK work instead of
-  // meeting another lane's FFT.  A slot is reused once the lane that read it records its
-  // `free` event, so the working set is D x rmax x ngrid (D = lanes + 2 by default) whatever
-  // nq is.  With a single MFMA lane it is slower (C3 107.8 vs 100.9 ms/step), so one lane
-  // keeps the FFT in-lane.
-  const int pipe_mode = c->pipe_mode >= 0 ? c->pipe_mode : env_fit_pipe();
-  bool pipe = pipe_mode != 0 && nq > 1 && NL > 1;
-  // sharded build (fisdf_mark_y_ready): y of the call's j-th q lands at ev_ready[j] on the main
-  // stream (all-to-all piece + unpack); the lanes then run on the aux streams only and each q
-  // starts as soon as its own piece is there, one call for the whole shard
-  int nready = 0;
-  for (int lq = 0; lq < nq; ++lq)
-    nready += (lq < (int)c->ready_marked.size() && c->ready_marked[lq]) ? 1 : 0;
-  FISDF_CHECK(nready == 0 || nready == nq, "fit_coulomb: mark every q of the call ready, or none");
-  const bool ready = nready > 0;
-  if (pipe) NL = std::min(NL, ready ? 2 : 3);  // aux[2] is the FFT stream
-  if (ready) NL = std::min(NL, 3);
-  int D = pipe ? std::min(nq, c->pipe_depth > 0 ? c->pipe_depth : default_pipe_depth(NL)) : 0;
   Carver cv;
   size_t oY[4], oU[4], oK[4], oTc[4];
-  size_t oYall = 0;
-  auto carve = [&]() {
-    cv = Carver();
-    for (int l = 0; l < NL; ++l) {
-      if (!pipe) oY[l] = cv.take(sizeof(cplx) * rfmax * ngrid);
-      oU[l] = cv.take(sizeof(cplx) * rmax * ngrid);
-      oK[l] = cv.take(sizeof(cplx) * (size_t)ks * rmax * rmax);
-      oTc[l] = cv.take(sizeof(cplx) * rr);
-    }
-    if (pipe) {
-      oYall = cv.take(sizeof(cplx) * (size_t)D * rfmax * ngrid);
-    }
-  };
-  carve();
-  if (pipe && cv.off > c->arena_size) {
-    // the ring's extra slots only if the device has room for them; else the in-lane FFT
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
-    const size_t extra = (size_t)D * rfmax * ngrid * sizeof(cplx);
-    if (free_b + c->arena_size < cv.off + extra / 8) {
-      pipe = false;
-      D = 0;
-      carve();
-    }
-  }
-  if (pipe) {
-    while ((int)c->ev_q.size() < nq) {
-      hipEvent_t e;
-      FISDF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      c->ev_q.push_back(e);
-    }
-    while ((int)c->ev_free.size() < D) {
-      hipEvent_t e;
-      FISDF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      c->ev_free.push_back(e);
-    }
+  for (int l = 0; l < NL; ++l) {
+    if (!pipe) oY[l] = cv.take(sizeof(cplx) * rfmax * ngrid);
+    oU[l] = cv.take(sizeof(cplx) * rmax * ngrid);
+    oK[l] = cv.take(sizeof(cplx) * (size_t)ks * rmax * rmax);
+    oTc[l] = cv.take(sizeof(cplx) * rr);
   }
   c->last_fit_lanes = NL;
   c->last_fit_pipe = pipe ? D : 0;
-  // all-to-all pieces of a mesh whose first FFT pass cannot read plane slices in place (no
-  // register kernel, plane too large for the LDS plane kernel): each FFT-issuing stream (the FFT
-  // stream, or every lane) unpacks its q's piece into a (nip, ngrid) buffer of its own first
-  bool any_piece = false;
-  for (int lq = 0; lq < nq; ++lq) any_piece = any_piece || piece_of(lq) != nullptr;
-  const bool unpack = any_piece && !fft3d_reads_slices(mesh[0], mesh[1], mesh[2]);
   size_t oP[4] = {0, 0, 0, 0};
   if (unpack)
     for (int l = 0; l < (pipe ? 1 : NL); ++l) oP[l] = cv.take(sizeof(cplx) * (size_t)nip * ngrid);
@@ -1934,17 +2023,9 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   } else {
     FISDF_HIP(hipMemsetAsync(G, 0, sizeof(cplx) * nq * rr, c->stream));
   }
-  // Yhat_q = FFT(y_q[:, piv] * f_q) * w_q   (:99, :113-115, :118; rows in pivot order)
-  // sqrt(coulG(k_q+G) vol/N^2)  (:114-115 and the Parseval 1/N of :118), cached per q
-  const double wscale = vol / ((double)ngrid * ngrid);
-  auto weight_q = [&](hipStream_t st, int lq, const double** w) {
-    return get_weight(c, st, mesh, kmesh, a, h_qs[lq], wscale, half_of(s0 + lq), w);
-  };
-  // sharded build: q read in place from their all-to-all pieces (fisdf_set_y_slices) through a
+  // Yhat_q = FFT(y_q[:, piv] * f_q) * w_q   (:99, :113-115, :118; rows in pivot order); the
+  // sharded build reads q in place from their all-to-all pieces (fisdf_set_y_slices) through a
   // per-plane address table (plane-aligned slices)
-  const PlaneRef* planes = nullptr;
-  if (any_piece && !unpack) FISDF_TRY(plane_table(c, mesh, nip, &planes));
-  FISDF_CHECK(yT != nullptr || any_piece, "fit_coulomb: no y");
   // ub: the stream's unpack buffer (FFT stream 0, lane l -> l)
   auto fft_q = [&](hipStream_t st, int lq, cplx* Yh, int ub) -> int {
     const int sl = s0 + lq;
@@ -1980,11 +2061,12 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
                     ngrid, r, mesh[0], mesh[1], mesh[2], kd, wt, nullptr, pc ? planes : nullptr));
     return 0;
   };
-  // ring slot of q lq (pipelined mode)
-  auto slot_y = [&](int lq) { return (cplx*)(b + oYall) + (long)(lq % D) * rfmax * ngrid; };
   // FFT of q lq into its ring slot, after the lane that read the slot's previous q is done
   auto enqueue_fft = [&](int lq) -> int {
     if (lq >= nq || c->f_rank[s0 + lq] == 0) return 0;
+    const int sl = s0 + lq;
+    if (lq < D && spec[lq] && c->f_rank[sl] == nip && !cod_of(sl) && !c->f_pslot[sl])
+      return 0;  // the speculative FFT (all rows, identity order) is this q's transform
     if (lq >= D) FISDF_HIP(hipStreamWaitEvent(fst, c->ev_free[lq % D], 0));
     if (ready) FISDF_HIP(hipStreamWaitEvent(fst, c->ev_ready[lq], 0));
     FISDF_TRY(fft_q(fst, lq, slot_y(lq), 0));
@@ -2641,14 +2723,15 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
                              qs.data(), nq, yT));                                  // :67-87
   FISDF_TRY(fisdf_factor_x4_async(c, x4, qs.data(), nq, nip, o.fit_tol,
                                   o.real_self_conjugate ? kmesh : nullptr));
+  void *Wq, *Ws;
+  FISDF_TRY(build_alloc(c, BR_WQ, sizeof(cplx) * (size_t)nq * nn, &Wq));
+  // the fit waits for the factor's verdict itself, after enqueueing its first FFTs
+  FISDF_TRY(fisdf_fit_coulomb_qs(c, qs.data(), nq, yT, nip, mesh, kmesh, a, Wq));   // :97-121
   std::vector<int> ranks(nq, 0);
   FISDF_TRY(fisdf_factor_x4_wait(c, ranks.data()));
   int used = 0, ncod = 0;
   FISDF_TRY(fisdf_factor_info(c, &used));
   FISDF_TRY(fisdf_min_norm_info(c, &ncod));
-  void *Wq, *Ws;
-  FISDF_TRY(build_alloc(c, BR_WQ, sizeof(cplx) * (size_t)nq * nn, &Wq));
-  FISDF_TRY(fisdf_fit_coulomb_qs(c, qs.data(), nq, yT, nip, mesh, kmesh, a, Wq));   // :97-121
   build_return(c, yT);  // y is dead once the fit is enqueued (stream-ordered)
   FISDF_TRY(build_alloc(c, BR_WS, sizeof(double) * (size_t)nk * nn, &Ws));
   FISDF_TRY(fisdf_build_ws_qs(c, Wq, qs.data(), wt.data(), nq, nip, kmesh, a, Ws)); // :204-207

@@ -112,10 +112,12 @@ int herk_batched(hipStream_t s, int n, int K, double alpha, const cplx* A, long 
                  double beta, cplx* C, long ldc, long sC, int batch);
 
 // batched pivoted Cholesky of Hermitian PSD matrices (fftisdf.py:381-382, A4 factorisation)
+// trail: pchol_trail_elems(n, batch) complex elements (the blocked path's trailing copy)
 int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int rmax,
           double tol_rel, double tol_abs, cplx* L /*batch, n, rmax*/, int* piv /*batch, rmax*/,
           int* rank /*batch, device*/, double* d /*batch,n*/, int* flags /*batch*/,
-          double* work /*batch*(1+rmax)*/);
+          double* work /*batch*(1+rmax)*/, cplx* trail);
+size_t pchol_trail_elems(int n, int batch);
 
 // unpivoted blocked Cholesky (full-rank fast path); see pchol.hip
 int chol_unpivoted(hipStream_t s, cplx* W, int n, int batch, double tol_rel, int* piv, int* rank,

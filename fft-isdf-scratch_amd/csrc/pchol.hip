@@ -800,9 +800,11 @@ __global__ void chol_finish_kernel(int n, int* __restrict__ piv, int* __restrict
 }  // namespace
 
 // pivot values are kept in `dmax0 + batch` (caller allocates 2*batch + batch*rmax doubles: see api)
+size_t pchol_trail_elems(int n, int batch) { return n <= PB_THREADS ? (size_t)n * n * batch : 0; }
+
 int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int rmax,
           double tol_rel, double tol_abs, cplx* L, int* piv, int* rank, double* d, int* flags,
-          double* work) {
+          double* work, cplx* trail) {
   FISDF_CHECK(n > 0 && batch > 0 && rmax > 0 && rmax <= n, "pchol: bad sizes");
   FISDF_CHECK(batch < 65536, "pchol: batch too large");
   double* thr = work;                  // batch
@@ -815,8 +817,8 @@ int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int
     // blocked: trailing copy W of A, panels of NB pivots, batched ZGEMM trailing updates
     constexpr int NB = 32;
     const long nn = (long)n * n;
-    cplx* W = nullptr;
-    FISDF_HIP(hipMallocAsync((void**)&W, sizeof(cplx) * nn * batch, s));
+    cplx* W = trail;  // the caller's (pchol_trail_elems): no stream-ordered pool memory
+    FISDF_CHECK(W != nullptr, "pchol: trailing-update workspace missing");
     FISDF_HIP(hipMemcpy2DAsync(W, sizeof(cplx) * n, A, sizeof(cplx) * lda, sizeof(cplx) * n,
                                (size_t)n * batch, hipMemcpyDeviceToDevice, s));
     if (sA != (long)n * lda) {  // batch stride differs from a packed copy: copy per matrix
@@ -834,7 +836,6 @@ int pchol(hipStream_t s, const cplx* A, long lda, long sA, int n, int batch, int
         FISDF_TRY(zgemm(s, OP_N, OP_C, n, n, kc, mone, L + j0, rmax, (long)n * rmax, L + j0, rmax,
                         (long)n * rmax, one, W, n, nn, batch));
     }
-    FISDF_HIP(hipFreeAsync(W, s));
     return 0;
   }
   const int rows_per_block = 4;

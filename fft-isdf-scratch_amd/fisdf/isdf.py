@@ -658,14 +658,8 @@ def build(df_obj):
         pieces = kshard.exchange_y_chunked(send, nip, slices, d.rank, d.size, d.comm,
                                            parts)
 
-    ranks = np.zeros(nq, np.int32)
-    if nq:
-        d.ctx.call("fisdf_factor_x4_wait", ranks.ctypes.data_as(_lib._ip))
-        used = C_int()
-        d.ctx.call("fisdf_factor_info", byref(used))
-        df_obj.used_pivoted_fit = bool(used.value)
-        d.ctx.call("fisdf_min_norm_info", byref(used))
-        df_obj.min_norm_slots = int(used.value)
+    # the factor's verdict (ranks, which q the rank-revealing path redid) is read after the fit
+    # call: the fit enqueues its first FFTs before it waits for the verdict itself
     Wq = d.empty((nq, nip, nip))
     if not sharded:
         if nq:
@@ -688,6 +682,14 @@ def build(df_obj):
         del send, pieces
         yT = None
     del yT
+    ranks = np.zeros(nq, np.int32)
+    if nq:
+        d.ctx.call("fisdf_factor_x4_wait", ranks.ctypes.data_as(_lib._ip))
+        used = C_int()
+        d.ctx.call("fisdf_factor_info", byref(used))
+        df_obj.used_pivoted_fit = bool(used.value)
+        d.ctx.call("fisdf_min_norm_info", byref(used))
+        df_obj.min_norm_slots = int(used.value)
 
     if sharded:
         # W_s = sqrt(nk) Re(sum_q Phi[R,q] W_q) (:204-207) mixes every rank's q; get_k on rank r
