@@ -78,12 +78,9 @@ struct fisdf_ctx {
   int fit_mode = 0;
   cplx* f_M = nullptr;          // (nk, nip, nip) minimum-norm operators A^+ (rows < rank)
   std::vector<char> f_cod;      // slot fitted through its minimum-norm operator
-  std::vector<char> f_pslot;    // slot factored by the pivoted (rank-revealing) path
-  // the fit's pipelined-FFT ring (Yhat slots), kept outside the arena so the FFTs of the first
-  // slots can be enqueued before the factor's verdict (fisdf_fit_coulomb_qs)
+  // the fit's pipelined-FFT ring (Yhat slots, nip rows each), a grow-only buffer of its own
   cplx* f_ring = nullptr;
   size_t f_ring_bytes = 0;
-  hipEvent_t ev_spec = nullptr;
   // grow-only temporaries instead of the stream-ordered pool (hipMallocAsync): on the HIP 7.2
   // runtime a block freed on one stream was handed to another stream's allocation while the
   // first still used it (torch-free C-ABI build: the pivoted factor's ranks corrupted by the
@@ -679,7 +676,6 @@ int fisdf_destroy(fisdf_ctx* c) {
   if (c->f_ring) (void)hipFree(c->f_ring);
   for (auto* w : {&c->ws_main, &c->ws_side_a, &c->ws_side_b})
     if (w->p) (void)hipFree(w->p);
-  if (c->ev_spec) (void)hipEventDestroy(c->ev_spec);
   if (c->side) {
     (void)hipStreamSynchronize(c->side);
     (void)hipStreamDestroy(c->side);
@@ -1501,7 +1497,6 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   char* b = (char*)c->f_scratch;
   c->f_qs.assign(h_qs, h_qs + nq);
   c->f_real.assign(nq, 0);
-  c->f_pslot.assign(nq, 0);
   for (int i = 0; kmesh && i < nq; ++i) c->f_real[i] = self_conjugate(kmesh, h_qs[i]) ? 1 : 0;
   c->f_nk = nk;
   c->f_nip = nip;
@@ -1529,7 +1524,6 @@ int fisdf_factor_x4_async(fisdf_ctx* c, const void* x4all, const int* h_qs, int 
   FISDF_TRY(stage_x4(s, (const cplx*)x4all, c->f_qr_dev, nq, nn, c->f_x4s, pivoted ? nullptr : c->f_L));
   if (pivoted) {
     FISDF_TRY(factor_pivoted(c, s));
-    c->f_pslot.assign(nq, 1);
     c->f_check_fail = false;
   } else {
     // full-rank fast path: unpivoted blocked Cholesky (all pivots > tol_rel * max diag is the
@@ -1716,7 +1710,6 @@ int fisdf_factor_x4_wait(fisdf_ctx* c, int* h_ranks) {
         if (c->f_fail_pinned[q] != 0) failed.push_back(q);
       c->f_check_fail = false;
       if (!failed.empty()) {  // not numerically full rank at tol: rank-revealing factorisation
-        for (int q : failed) c->f_pslot[q] = 1;
         FISDF_TRY(factor_pivoted_slots(c, c->side, failed));
         FISDF_HIP(hipEventRecord(c->ev_fac, c->side));
         FISDF_HIP(hipEventSynchronize(c->ev_fac));
@@ -1823,7 +1816,6 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   const double vol = cell_volume(a);
   const cplx* yT = (const cplx*)yTv;
   cplx* Wq = (cplx*)Wqv;
-  // what does not depend on the factor's verdict: the lanes, the pipelined-FFT ring, the pieces
   // q are processed on NL "lanes" (the main stream and aux streams), each with its own
   // workspaces, so one q's HBM-bound FFT and memory-stalled HERK overlap another q's
   // MFMA-bound TRSM on the same CUs
@@ -1899,37 +1891,6 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     return get_weight(c, st, mesh, kmesh, a, h_qs[lq], wscale, half_of(s0 + lq), w);
   };
   auto slot_y = [&](int lq) { return c->f_ring + (long)(lq % D) * nip * ngrid; };
-  // Speculative FFTs (k-sharded builds, where the factor chain is on the critical path): while the
-  // factorisation is still running on the side stream with its unpivoted full-rank fast path
-  // pending, the ring's first D q are transformed assuming that verdict (all nip rows, pivot order
-  // = identity); after the verdict a q the assumption missed is transformed again
-  std::vector<char> spec(nq, 0);
-  static const bool spec_on = [] {
-    const char* e = getenv("FISDF_FIT_SPEC");
-    return !(e && e[0] == '0');
-  }();
-  if (spec_on && pipe && !unpack && c->f_pending && c->f_check_fail && c->fit_mode != FISDF_FIT_SVD) {
-    FISDF_TRY(ensure_aux(c));
-    if (!c->ev_spec) FISDF_HIP(hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming));
-    hipStream_t fs = c->aux[2];
-    FISDF_HIP(hipEventRecord(c->ev_spec, c->stream));  // after the y build / the pieces' marks
-    FISDF_HIP(hipStreamWaitEvent(fs, c->ev_spec, 0));
-    for (int lq = 0; lq < D; ++lq) {
-      double kq[3], kd[3];
-      kpoint(kmesh, g, h_qs[lq], kq);
-      for (int i = 0; i < 3; ++i) kd[i] = g.a[i][0] * kq[0] + g.a[i][1] * kq[1] + g.a[i][2] * kq[2];
-      const double* wt = nullptr;
-      FISDF_TRY(weight_q(fs, lq, &wt));
-      if (ready) FISDF_HIP(hipStreamWaitEvent(fs, c->ev_ready[lq], 0));
-      StageTimer tm(c, FISDF_ST_FFT, fs);
-      const cplx* pc = piece_of(lq);
-      FISDF_TRY(fft3d(fs, pc ? pc : yT + (long)lq * nip * ngrid, ngrid, nullptr, slot_y(lq), ngrid, nip,
-                      mesh[0], mesh[1], mesh[2], kd, wt, nullptr, pc ? planes : nullptr));
-      FISDF_HIP(hipEventRecord(c->ev_q[lq], fs));
-      spec[lq] = 1;
-    }
-    if (getenv("FISDF_DBG_SPEC_SYNC")) FISDF_HIP(hipStreamSynchronize(fs));
-  }
   FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
   int rmax = 0;
   for (int lq = 0; lq < nq; ++lq) rmax = std::max(rmax, c->f_rank[s0 + lq]);
@@ -2064,9 +2025,6 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   // FFT of q lq into its ring slot, after the lane that read the slot's previous q is done
   auto enqueue_fft = [&](int lq) -> int {
     if (lq >= nq || c->f_rank[s0 + lq] == 0) return 0;
-    const int sl = s0 + lq;
-    if (lq < D && spec[lq] && c->f_rank[sl] == nip && !cod_of(sl) && !c->f_pslot[sl])
-      return 0;  // the speculative FFT (all rows, identity order) is this q's transform
     if (lq >= D) FISDF_HIP(hipStreamWaitEvent(fst, c->ev_free[lq % D], 0));
     if (ready) FISDF_HIP(hipStreamWaitEvent(fst, c->ev_ready[lq], 0));
     FISDF_TRY(fft_q(fst, lq, slot_y(lq), 0));
@@ -2725,7 +2683,7 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
                                   o.real_self_conjugate ? kmesh : nullptr));
   void *Wq, *Ws;
   FISDF_TRY(build_alloc(c, BR_WQ, sizeof(cplx) * (size_t)nq * nn, &Wq));
-  // the fit waits for the factor's verdict itself, after enqueueing its first FFTs
+  // the fit waits for the factor's verdict itself
   FISDF_TRY(fisdf_fit_coulomb_qs(c, qs.data(), nq, yT, nip, mesh, kmesh, a, Wq));   // :97-121
   std::vector<int> ranks(nq, 0);
   FISDF_TRY(fisdf_factor_x4_wait(c, ranks.data()));

@@ -659,7 +659,7 @@ def build(df_obj):
                                            parts)
 
     # the factor's verdict (ranks, which q the rank-revealing path redid) is read after the fit
-    # call: the fit enqueues its first FFTs before it waits for the verdict itself
+    # call, which waits for it itself
     Wq = d.empty((nq, nip, nip))
     if not sharded:
         if nq:
