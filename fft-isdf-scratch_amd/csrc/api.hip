@@ -1162,6 +1162,15 @@ int fisdf_gather_points(fisdf_ctx* c, const void* x0, int nk, int ng0, int nao, 
 }
 
 // ---- A2 ---------------------------------------------------------------------
+// FISDF_X4_DFT=0: the x4 build through the two dense Phi GEMMs (A/B on one box)
+static bool x4_dft_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FISDF_X4_DFT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int fisdf_build_x4(fisdf_ctx* c, const void* Xv, int nip, int nao, const int kmesh[3],
                    const double a[9], void* x4v) {
   FISDF_TRY(device_guard(c));
@@ -1176,6 +1185,34 @@ int fisdf_build_x4(fisdf_ctx* c, const void* Xv, int nip, int nao, const int kme
     // epilogue with the reality monitor of :43 (the two Phi GEMMs would run with M = 1)
     FISDF_TRY(zgemm(c->stream, OP_R, OP_T, nip, nip, nao, ONE, X, nao, 0, X, nao, 0, ZERO,
                     (cplx*)x4v, nip, 0, 1, 1, nullptr, EPI_CSQUARE, c->maximag + 0));
+    return 0;
+  }
+  if (x4_dft_enabled() && kmesh_y_reg_applies(kmesh, nn)) {
+    // the k-mesh DFT pair of :41-46 per (I, J) column in registers (the y build's kmesh_y with
+    // conj output: x4_k = Phi^H x4_s, x4_s real) instead of two dense nk x nk Phi GEMMs; under
+    // time reversal (X_{-k} = conj(X_k), so x2_{-k} = conj(x2_k)) x2_k only for the
+    // representatives k <= -k
+    const bool half = c->time_reversal;
+    const int nks = half ? kmesh_half_count(kmesh) : nk;
+    void* base;
+    FISDF_TRY(arena_get(c, sizeof(cplx) * (size_t)nks * nn, &base));
+    cplx* X2k = (cplx*)base;
+    std::vector<int> runs = {0, nk};
+    if (half) FISDF_TRY(kmesh_rep_runs(kmesh, &runs));
+    // x2_k = X_k^* X_k^T  (:38), one batched GEMM per run of stored k
+    for (size_t r = 0, slot = 0; r < runs.size(); r += 2) {
+      const int k0 = runs[r], nb = runs[r + 1] - runs[r];
+      FISDF_TRY(zgemm(c->stream, OP_R, OP_T, nip, nip, nao, ONE, X + (long)k0 * nip * nao, nao,
+                      (long)nip * nao, X + (long)k0 * nip * nao, nao, (long)nip * nao, ZERO,
+                      X2k + (long)slot * nn, nip, nn, nb));
+      slot += nb;
+    }
+    // x2_s = Phi x2_k (:41, real: max|Im| monitored, :43), x4_s = x2_s^2 (:45),
+    // x4_k = Phi^H x4_s (:46) for every k
+    std::vector<int> all(nk);
+    for (int q = 0; q < nk; ++q) all[q] = q;
+    FISDF_TRY(kmesh_y(c->stream, X2k, nn, kmesh, all.data(), nullptr, nk, nip, (cplx*)x4v, nn, nip,
+                      0, half, c->maximag + 0, true));
     return 0;
   }
   Carver cv;
@@ -2662,6 +2699,9 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
   FISDF_TRY(build_alloc(c, BR_X, sizeof(cplx) * (size_t)nk * nip * nao, &X));
   FISDF_TRY(fisdf_gather_points(c, x0, nk, ng0, nao, perm.data(), nip, X));        // :388
   FISDF_TRY(build_alloc(c, BR_X4, sizeof(cplx) * (size_t)nk * nn, &x4));
+  // time reversal (X_{-k} = conj(X_k)) before x4: its x2_k and the y build's fx_k are then
+  // formed for the representatives k <= -k only
+  FISDF_TRY(fisdf_set_time_reversal(c, o.time_reversal ? 1 : 0));
   FISDF_TRY(fisdf_build_x4(c, X, nip, nao, kmesh, a, x4));                         // :38-48
   std::vector<int> qs, partner;
   std::vector<double> wt;
@@ -2673,7 +2713,6 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
   FISDF_TRY(fisdf_set_half_grid(c, o.half_grid));
   FISDF_TRY(fisdf_set_factor_priority(c, 0));
   FISDF_TRY(fisdf_factor_x4_mark(c));
-  FISDF_TRY(fisdf_set_time_reversal(c, o.time_reversal ? 1 : 0));
   FISDF_TRY(fisdf_set_omega(c, o.omega));
   void* yT;
   FISDF_TRY(build_alloc(c, BR_Y, sizeof(cplx) * (size_t)nq * nip * ngrid, &yT));

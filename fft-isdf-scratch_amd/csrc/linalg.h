@@ -95,8 +95,12 @@ int eval_ao(hipStream_t s, const double* d_coords, int ng, int natm, const doubl
             const double* h_coefs, int nT, const int* h_tn, const int kmesh[3], const double a[9],
             double rcut, double* F, void* scratch, size_t scratch_size, cplx* chi, int* h_nao,
             int nkb = 0, const double* h_kband = nullptr);
+// conj_out: store conj(y_q) — the x4 build's Phi^H x4_s (fftisdf.py:46; x4_s real) where the y
+// build has Phi^T y_s (:84)
 int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const int* h_qs,
             const int* d_qs, int nq, int m, cplx* yT, long qs, long Is, long goff, bool half,
-            unsigned long long* mon);
+            unsigned long long* mon, bool conj_out = false);
+// whether kmesh_y runs its register kernel for this k-mesh and column count (no device q-list)
+bool kmesh_y_reg_applies(const int kmesh[3], long ncol);
 
 }  // namespace fisdf

@@ -451,7 +451,7 @@ __device__ __forceinline__ void reg_axis_dft(cplx* v, const cplx* tw) {
 template <int N0, int N1, int N2, bool HALF>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void kmesh_y_reg_kernel(
     const cplx* __restrict__ FX, int ncol, unsigned long long qmask, int m, cplx* __restrict__ yT,
-    long qs, long Is, long goff, unsigned long long* __restrict__ mon) {
+    long qs, long Is, long goff, unsigned long long* __restrict__ mon, double csign) {
   constexpr int NK = N0 * N1 * N2;
   cplx tw0[N0], tw1[N1], tw2[N2];
 #pragma unroll
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 #pragma unroll
     for (int k = 0; k < NK; ++k)
       if ((qmask >> k) & 1ull)  // slot of q = k in the ascending q-list
-        out[(long)__popcll(qmask & ((1ull << k) - 1ull)) * qs] = cmk(v[k].x * sc, v[k].y * sc);
+        out[(long)__popcll(qmask & ((1ull << k) - 1ull)) * qs] = cmk(v[k].x * sc, csign * v[k].y * sc);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mi = fmax(mi, __shfl_xor(mi, o, 64));
@@ -1422,9 +1422,21 @@ int kmesh_rep_runs(const int kmesh[3], std::vector<int>* runs) {
   return 0;
 }
 
+#define FISDF_KM_REG_MESHES(X)                                                                 \
+  X(1, 1, 1) X(1, 1, 2) X(2, 2, 2) X(3, 3, 1) X(3, 3, 3) X(4, 4, 4) X(2, 2, 1) X(1, 2, 2)       \
+  X(4, 4, 1) X(2, 2, 4)
+
+bool kmesh_y_reg_applies(const int kmesh[3], long ncol) {
+  bool on = false;
+#define FISDF_KM_HAS(a, b, c) on = on || (kmesh[0] == a && kmesh[1] == b && kmesh[2] == c);
+  FISDF_KM_REG_MESHES(FISDF_KM_HAS)
+#undef FISDF_KM_HAS
+  return on && ncol < (1L << 31);
+}
+
 int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const int* h_qs,
             const int* d_qs, int nq, int m, cplx* yT, long qs, long Is, long goff,
-            bool half, unsigned long long* mon) {
+            bool half, unsigned long long* mon, bool conj_out) {
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
   for (int i = 0; i < nq; ++i)
     FISDF_CHECK(h_qs[i] >= 0 && h_qs[i] < nk && (i == 0 || h_qs[i] > h_qs[i - 1]),
@@ -1436,21 +1448,22 @@ int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const 
     unsigned long long qmask = 0;
     for (int i = 0; i < nq; ++i) qmask |= 1ull << h_qs[i];
     const unsigned grid = (unsigned)std::max<long>(1, std::min<long>((ncol + 63) / 64, 32768));
+    const double csign = conj_out ? -1.0 : 1.0;
 #define FISDF_KM(a, b, c)                                                                      \
   if (kmesh[0] == a && kmesh[1] == b && kmesh[2] == c) {                                       \
     if (half)                                                                                  \
       hipLaunchKernelGGL((kmesh_y_reg_kernel<a, b, c, true>), dim3(grid), dim3(64), 0, s, FX,   \
-                         nc, qmask, m, yT, qs, Is, goff, mon);                                 \
+                         nc, qmask, m, yT, qs, Is, goff, mon, csign);                          \
     else                                                                                       \
       hipLaunchKernelGGL((kmesh_y_reg_kernel<a, b, c, false>), dim3(grid), dim3(64), 0, s, FX,  \
-                         nc, qmask, m, yT, qs, Is, goff, mon);                                 \
+                         nc, qmask, m, yT, qs, Is, goff, mon, csign);                          \
     FISDF_HIP(hipGetLastError());                                                              \
     return 0;                                                                                  \
   }
-    FISDF_KM(1, 1, 1) FISDF_KM(1, 1, 2) FISDF_KM(2, 2, 2) FISDF_KM(3, 3, 1) FISDF_KM(3, 3, 3)
-    FISDF_KM(4, 4, 4) FISDF_KM(2, 2, 1) FISDF_KM(1, 2, 2) FISDF_KM(4, 4, 1) FISDF_KM(2, 2, 4)
+    FISDF_KM_REG_MESHES(FISDF_KM)
 #undef FISDF_KM
   }
+  FISDF_CHECK(!conj_out, "kmesh_y: conj_out needs the register kernel's k-mesh");
   int CT = 64;
   while (CT > 8 && sizeof(cplx) * ((size_t)nk * (CT + 1) + 3 * KM_MAXN) > 64 * 1024) CT /= 2;
   const size_t lds = sizeof(cplx) * ((size_t)nk * (CT + 1) + 3 * KM_MAXN) + sizeof(int) * nk;

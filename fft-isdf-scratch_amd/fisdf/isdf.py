@@ -594,6 +594,8 @@ def build(df_obj):
     X = df_obj._dev_state["X"]
     nip = X.shape[1]
 
+    # X_{-k} = conj(X_k) for real AOs: x2_k (x4) and fx_k (y) formed for half the k-mesh (:38, :76)
+    d.ctx.call("fisdf_set_time_reversal", 1 if df_obj.time_reversal else 0)
     x4 = d.empty((nk, nip, nip))
     d.ctx.call("fisdf_build_x4", _lib.ptr(X), nip, nao, km_p, a_p, _lib.ptr(x4))   # :38-48
 
@@ -632,8 +634,6 @@ def build(df_obj):
         if nq:
             d.ctx.call("fisdf_factor_x4_async", _lib.ptr(x4), qs_c, nq, nip,
                        float(df_obj.fit_tol), km_p if df_obj.real_self_conjugate else None)
-    # fx_{-k} = conj(fx_k) for real AOs: fx_k computed for half the k-mesh (:76)
-    d.ctx.call("fisdf_set_time_reversal", 1 if df_obj.time_reversal else 0)
     d.ctx.call("fisdf_set_omega", float(getattr(df_obj, "_fit_omega", 0.0)))
     df_obj._omega_dfs = {}                   # range-separated states of an earlier build
     if not sharded:

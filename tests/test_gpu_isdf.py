@@ -244,9 +244,20 @@ def test_x4_and_y_parity(name):
     cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(name)
     d = df.device
     nk, ngrid, nip, nao = chi.shape[0], chi.shape[1], o["xip"].shape[1], chi.shape[2]
-    yT = d.empty((nk, nip, ngrid))
     km, kmp = L.iarr(kmesh)
     a, ap = L.darr(cell.a.ravel())
+    # x4 through the C-ABI with every x2_k formed and with the representatives k <= -k only
+    # (x2_{-k} = conj(x2_k)); both through the register k-mesh DFT pair and, FISDF_X4_DFT=0 in
+    # another process, the dense Phi GEMMs (the build above)
+    x4b = d.empty((nk, nip, nip))
+    for tr in (0, 1):
+        d.ctx.call("fisdf_set_time_reversal", tr)
+        x4b.zero_()
+        d.ctx.call("fisdf_build_x4", L.ptr(df._dev_state["X"]), nip, nao, kmp, ap, L.ptr(x4b))
+        rel = abs(x4b.cpu().numpy() - o["x4"]).max() / abs(o["x4"]).max()
+        print(f"{name} x4 time_reversal={tr}: max rel |x4 - x4_oracle| = {rel:.2e}")
+        assert rel < 1e-12
+    yT = d.empty((nk, nip, ngrid))
     # two blocks to exercise the g0 offset; every k computed, then fx_k for half the k-mesh
     # with fx_{-k} = conj(fx_k) (fisdf_set_time_reversal)
     h = ngrid // 2
