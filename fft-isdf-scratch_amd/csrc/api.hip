@@ -2274,18 +2274,25 @@ int fisdf_build_ws_qs(fisdf_ctx* c, const void* Wqv, const int* h_qs, const doub
   return 0;
 }
 
-int fisdf_build_ws_rows(fisdf_ctx* c, const void* Wqv, const int* h_qs, const double* h_wt, int nq,
-                        int nip, const int kmesh[3], const double a[9], int i0, int i1,
-                        void* Wsv) {
-  FISDF_TRY(device_guard(c));
-  FISDF_CHECK(0 <= i0 && i0 <= i1 && i1 <= nip, "build_ws_rows: bad row range");
+// W_s row blocks [rows[b], rows[b+1]) of a q-list's partial sum, block b at Wsb + b * chunk
+// doubles (chunk 0: one block): the phase table uploaded once, one GEMM per block
+static int ws_row_blocks(fisdf_ctx* c, const void* Wqv, const int* h_qs, const double* h_wt, int nq,
+                         int nip, const int kmesh[3], const double a[9], int nblk,
+                         const int* rows, long chunk, void* Wsv) {
   StageTimer tm(c, FISDF_ST_WS);
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
   FISDF_TRY(check_qlist(h_qs, nq, nk, "build_ws_rows"));
-  const long nb = i1 - i0, nn = (long)nip * nip;
-  if (nb == 0) return 0;
+  FISDF_CHECK(nblk >= 1, "build_ws_rows: no blocks");
+  for (int b = 0; b < nblk; ++b)
+    FISDF_CHECK(0 <= rows[b] && rows[b] <= rows[b + 1] && rows[b + 1] <= nip &&
+                    (nblk == 1 || (long)nk * (rows[b + 1] - rows[b]) * nip <= chunk),
+                "build_ws_rows: bad row range");
+  const long nn = (long)nip * nip;
+  double* Ws = (double*)Wsv;
   if (nq == 0) {
-    FISDF_HIP(hipMemsetAsync(Wsv, 0, sizeof(double) * nk * nb * nip, c->stream));
+    for (int b = 0; b < nblk; ++b)
+      FISDF_HIP(hipMemsetAsync(Ws + b * chunk, 0,
+                               sizeof(double) * nk * (rows[b + 1] - rows[b]) * nip, c->stream));
     return 0;
   }
   CellGeom g;
@@ -2311,10 +2318,30 @@ int fisdf_build_ws_rows(fisdf_ctx* c, const void* Wqv, const int* h_qs, const do
   FISDF_TRY(upload_bytes(c, ph.data(), sizeof(cplx) * ph.size(), dph));
   // W_s[R][i0:i1] = sqrt(nk) Re(sum_i Phi_sel[R,i] W_{q_i}[i0:i1]) (fftisdf.py:205-207): the same
   // GEMM as fisdf_build_ws_qs on the row block (B = W_q rows i0..i1, ld nip^2), written (nk, nb, nip)
-  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, (int)(nb * nip), nq, cmk(std::sqrt((double)nk), 0), dph,
-                  nq, 0, (const cplx*)Wqv + (long)i0 * nip, nn, 0, ZERO, (cplx*)Wsv, nb * nip, 0, 1,
-                  1, nullptr, EPI_REAL, nullptr));
+  for (int b = 0; b < nblk; ++b) {
+    const long nb = rows[b + 1] - rows[b];
+    if (nb == 0) continue;
+    FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, (int)(nb * nip), nq, cmk(std::sqrt((double)nk), 0),
+                    dph, nq, 0, (const cplx*)Wqv + (long)rows[b] * nip, nn, 0, ZERO,
+                    (cplx*)(Ws + b * chunk), nb * nip, 0, 1, 1, nullptr, EPI_REAL, nullptr));
+  }
   return 0;
+}
+
+int fisdf_build_ws_rows(fisdf_ctx* c, const void* Wqv, const int* h_qs, const double* h_wt, int nq,
+                        int nip, const int kmesh[3], const double a[9], int i0, int i1,
+                        void* Wsv) {
+  FISDF_TRY(device_guard(c));
+  const int rows[2] = {i0, i1};
+  return ws_row_blocks(c, Wqv, h_qs, h_wt, nq, nip, kmesh, a, 1, rows, 0, Wsv);
+}
+
+int fisdf_build_ws_blocks(fisdf_ctx* c, const void* Wqv, const int* h_qs, const double* h_wt,
+                          int nq, int nip, const int kmesh[3], const double a[9], int nblk,
+                          const int* h_rows, long chunk, void* Wsbv) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(h_rows != nullptr && chunk >= 0, "build_ws_blocks: bad arguments");
+  return ws_row_blocks(c, Wqv, h_qs, h_wt, nq, nip, kmesh, a, nblk, h_rows, chunk, Wsbv);
 }
 
 int fisdf_build_ws(fisdf_ctx* c, const void* Wqv, int q0, int q1, int nip, const int kmesh[3],

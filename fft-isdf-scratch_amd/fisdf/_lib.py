@@ -84,6 +84,7 @@ _SIGS = {
     "fisdf_get_k_rows": ([_vp, _vp, _vp, _vp, _i, _i, _i, _ip, _dp, _i, _i, _vp], _i),
     "fisdf_get_k_rows_local": ([_vp, _vp, _vp, _vp, _i, _i, _i, _ip, _dp, _i, _i, _vp], _i),
     "fisdf_build_ws_rows": ([_vp, _vp, _ip, _dp, _i, _i, _ip, _dp, _i, _i, _vp], _i),
+    "fisdf_build_ws_blocks": ([_vp, _vp, _ip, _dp, _i, _i, _ip, _dp, _i, _ip, _l, _vp], _i),
     "fisdf_get_eri": ([_vp, _vp, _i, _i, _ip, _vp, C.POINTER(_vp), _ip, _vp], _i),
     "fisdf_zgemm": ([_vp, _i, _i, _i, _i, _i, _dp, _vp, _l, _l, _vp, _l, _l, _dp, _vp, _l, _l,
                      _i, _i], _i),

@@ -698,11 +698,11 @@ def build(df_obj):
         rows = [kshard.shard_range(nip, r, d.size) for r in range(d.size)]
         chunk = nk * max(b - a for a, b in rows) * nip
         Wsb = d.empty((chunk * d.size,), "f64")         # W_s is real (fftisdf.py:207)
-        for r, (i0, i1) in enumerate(rows):
-            if i1 > i0:
-                d.ctx.call("fisdf_build_ws_rows", _lib.ptr(Wq), qs_c,
-                           my_wt.ctypes.data_as(_lib._dp), nq, nip, km_p, a_p, i0, i1,
-                           _lib.ptr(Wsb[r * chunk:]))
+        bounds = np.ascontiguousarray([a for a, _ in rows] + [rows[-1][1]], dtype=np.int32)
+        assert all(rows[r][1] == bounds[r + 1] for r in range(d.size))
+        d.ctx.call("fisdf_build_ws_blocks", _lib.ptr(Wq), qs_c, my_wt.ctypes.data_as(_lib._dp),
+                   nq, nip, km_p, a_p, d.size, bounds.ctypes.data_as(_lib._ip), chunk,
+                   _lib.ptr(Wsb))
         i0, i1 = rows[d.rank]
         Ws = kshard.reduce_scatter_rows(Wsb, chunk, nk * (i1 - i0) * nip, d.rank, d.size,
                                         d.comm, rows=(i0, i1)).reshape(nk, i1 - i0, nip)

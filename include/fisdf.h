@@ -334,6 +334,12 @@ int fisdf_build_ws_qs(fisdf_ctx* ctx, const void* d_Wq, const int* h_qs, const d
 int fisdf_build_ws_rows(fisdf_ctx* ctx, const void* d_Wq, const int* h_qs, const double* h_wt,
                         int nq, int nip, const int kmesh[3], const double a[9], int i0, int i1,
                         void* d_Ws);
+/* Every rank's row block in one call (the reduce-scatter input): block b = rows
+ * [h_rows[b], h_rows[b+1]) written as (nk, rows, nip) float64 at d_Wsb + b * chunk doubles.
+ * asynchronous. */
+int fisdf_build_ws_blocks(fisdf_ctx* ctx, const void* d_Wq, const int* h_qs, const double* h_wt,
+                          int nq, int nip, const int kmesh[3], const double a[9], int nblk,
+                          const int* h_rows, long chunk, void* d_Wsb);
 
 /* ---- A7: get_j_kpts (fftisdf.py:133-171) ------------------------------------
  * d_dms (nset, nk, nao, nao); d_vj same shape (complex; caller takes .real for Gamma). */
