@@ -611,29 +611,40 @@ __global__ __launch_bounds__(256) void herk_reduce_kernel(int n, int ksplit,
                                                           const cplx* __restrict__ work, double alpha,
                                                           cplx* __restrict__ C, long ldc,
                                                           unsigned long long* __restrict__ span) {
+  // one 16 x 16 lower block per workgroup (the partials hold exactly those: the HERK computes the
+  // lower 16 x 16 blocks), one element per thread, 8 partials in flight per thread; every
+  // element sums its partials in ascending s.  (32 x 32 tiles with one load in flight per thread
+  // gave ~190 workgroups at 0.7 TB/s: latency-bound.)
   span_begin(span);
-  __shared__ cplx tile[32][33];
+  __shared__ cplx tile[16][17];
   int t = blockIdx.x, ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
   while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
   while (ti * (ti + 1) / 2 > t) --ti;
   const int tj = t - ti * (ti + 1) / 2;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const long nn = (long)n * n;
-  for (int rr = ty; rr < 32; rr += 8) {
-    const int r = ti * 32 + rr, c = tj * 32 + tx;
-    cplx acc = cmk(0, 0);
-    const bool valid = r < n && c < n && (r >> 4) >= (c >> 4);
-    if (valid) {
-      for (int s = 0; s < ksplit; ++s) acc = cadd(acc, work[s * nn + (long)r * n + c]);
-      acc = cscale(acc, alpha);
-      C[(long)r * ldc + c] = acc;
-    }
-    tile[rr][tx] = acc;
+  const int r = ti * 16 + ty, c = tj * 16 + tx;
+  const bool valid = r < n && c < n;
+  const cplx* w = work + (valid ? (long)r * n + c : 0);
+  cplx acc = cmk(0, 0);
+  for (int s0 = 0; s0 < ksplit; s0 += 8) {
+    cplx v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (s0 + u < ksplit && valid) ? w[(long)(s0 + u) * nn] : cmk(0, 0);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (s0 + u < ksplit) acc = cadd(acc, v[u]);
   }
+  cplx a = cmk(0, 0);
+  if (valid) {
+    a = cscale(acc, alpha);
+    C[(long)r * ldc + c] = a;
+  }
+  tile[ty][tx] = a;
   __syncthreads();
-  for (int rr = ty; rr < 32; rr += 8) {  // C[tj*32 + rr][ti*32 + tx] = conj(C[ti*32 + tx][tj*32 + rr])
-    const int sr = ti * 32 + tx, sc = tj * 32 + rr;
-    if (sr < n && sc < n && (sr >> 4) > (sc >> 4)) C[(long)sc * ldc + sr] = cconj(tile[tx][rr]);
+  if (ti > tj) {  // C[tj*16 + ty][ti*16 + tx] = conj(C[ti*16 + tx][tj*16 + ty])
+    const int sr = tj * 16 + ty, sc = ti * 16 + tx;
+    if (sr < n && sc < n) C[(long)sr * ldc + sc] = cconj(tile[tx][ty]);
   }
   span_end(span);
 }
@@ -782,8 +793,8 @@ int herk(hipStream_t s, int n, int K, double alpha, const cplx* A, long lda, cpl
   ksplit = 1;
 #endif
   if (ksplit > 1) {
-    const int t32 = (n + 31) / 32;
-    hipLaunchKernelGGL(herk_reduce_kernel, dim3(t32 * (t32 + 1) / 2), dim3(256), 0, s, n, ksplit,
+    const int t16 = (n + 15) / 16;
+    hipLaunchKernelGGL(herk_reduce_kernel, dim3(t16 * (t16 + 1) / 2), dim3(256), 0, s, n, ksplit,
                        (const cplx*)work, alpha, C, ldc, ev.span);
     FISDF_HIP(hipGetLastError());
   }
