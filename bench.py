@@ -198,8 +198,17 @@ def emulate_ranks(args):
         df._kmesh()
         df._ao_parent, df._ao_grid = ref._ao_parent, ref._ao_grid
 
+        # FISDF_WHATIF_GIVEN_X=1 (a what-if, not the benchmark): the interpolation points handed
+        # over, so the replicated selection is left out of every rank's step — how much of the
+        # rank the selection front holds
+        given_x = os.environ.get("FISDF_WHATIF_GIVEN_X") == "1"
+
         def step():
-            df._dev_state = None
+            if given_x:
+                df._dev_state = {"X": X}
+                df.perm = ref.perm
+            else:
+                df._dev_state = None
             df.build()
             df.get_jk(dm)
         for _ in range(args.warmup):
@@ -229,7 +238,10 @@ def emulate_ranks(args):
     a2a_in = nmine * nip * (ngrid - ng_self) * 16
     a2a_out = (len(fit_qs) - nmine) * nip * ng_self * 16
     ws_rs = (N - 1) / N * nk * nip * nip * 8
-    out = {"metric": "per-rank compute time of an emulated k-sharded step", "config": args.config,
+    metric = "per-rank compute time of an emulated k-sharded step"
+    if os.environ.get("FISDF_WHATIF_GIVEN_X") == "1":
+        metric += " (WHAT-IF: interpolation points given, selection left out)"
+    out = {"metric": metric, "config": args.config,
            "n_ranks": N, "steps": args.steps, "warmup": args.warmup,
            "one_gpu_reference": "bench.py default line (same config)",
            "max_rank_ms": worst["ms_per_step"], "worst_rank": R,
