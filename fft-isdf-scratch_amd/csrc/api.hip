@@ -395,9 +395,22 @@ int free_factors(fisdf_ctx* c) {
 // Hermitian update P P^H (only its real part is used: Re(P P^H) = Re(conj(P) P^T)).
 // `tmp` must hold ng0*nq*nao complex.
 int select_gram(fisdf_ctx* c, const cplx* x0, int nk, int q0, int q1, int ng0, int nao, cplx* x2,
-                cplx* tmp) {
-  const int nq = q1 - q0;
-  FISDF_TRY(permute_kgm(c->stream, x0 + (long)q0 * ng0 * nao, nq, ng0, nao, tmp));
+                cplx* tmp, const int* kmesh) {
+  int nq = q1 - q0;
+  if (kmesh && c->time_reversal && q0 == 0 && q1 == nk) {
+    // time reversal (x0_{-q} = conj(x0_q)): Re(x0_{-q} x0_{-q}^H) = Re(x0_q x0_q^H), so the sum
+    // over the k-mesh is the sum over the representatives q <= -q with a paired one counted
+    // twice — its copy scaled by sqrt(2): 36 of 64 k at 4x4x4
+    std::vector<int> reps;
+    std::vector<char> self;
+    kmesh_reps(kmesh, &reps, &self);
+    std::vector<double> sc(reps.size());
+    for (size_t j = 0; j < reps.size(); ++j) sc[j] = self[j] ? 1.0 : std::sqrt(2.0);
+    nq = (int)reps.size();
+    FISDF_TRY(permute_kgm_sel(c->stream, x0, reps.data(), sc.data(), nq, ng0, nao, tmp));
+  } else {
+    FISDF_TRY(permute_kgm(c->stream, x0 + (long)q0 * ng0 * nao, nq, ng0, nao, tmp));
+  }
   const int K = nq * nao;
   int ks = 1;
   const long tiles = (long)((ng0 + 63) / 64) * ((ng0 + 63) / 64 + 1) / 2;
@@ -1001,9 +1014,28 @@ static int select_pivots_dev(fisdf_ctx* c, const cplx* X2, double scale, int ng0
   return 0;
 }
 
+static int select_points_impl(fisdf_ctx* c, const void* x0v, int nk, const int* kmesh, int ng0,
+                              int nao, int nip_max, double tol, int* h_perm, int* h_npiv,
+                              int* h_full_rank);
+
 int fisdf_select_points(fisdf_ctx* c, const void* x0v, int nk, int ng0, int nao, int nip_max,
                         double tol, int* h_perm, int* h_npiv, int* h_full_rank) {
   FISDF_TRY(device_guard(c));
+  return select_points_impl(c, x0v, nk, nullptr, ng0, nao, nip_max, tol, h_perm, h_npiv,
+                            h_full_rank);
+}
+
+int fisdf_select_points_km(fisdf_ctx* c, const void* x0v, const int kmesh[3], int ng0, int nao,
+                           int nip_max, double tol, int* h_perm, int* h_npiv, int* h_full_rank) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(kmesh && kmesh[0] > 0 && kmesh[1] > 0 && kmesh[2] > 0, "select_points: bad k-mesh");
+  return select_points_impl(c, x0v, kmesh[0] * kmesh[1] * kmesh[2], kmesh, ng0, nao, nip_max, tol,
+                            h_perm, h_npiv, h_full_rank);
+}
+
+static int select_points_impl(fisdf_ctx* c, const void* x0v, int nk, const int* kmesh, int ng0,
+                              int nao, int nip_max, double tol, int* h_perm, int* h_npiv,
+                              int* h_full_rank) {
   FISDF_CHECK(nk > 0 && ng0 > 0 && nao > 0 && nip_max > 0, "select_points: bad sizes");
   nip_max = std::min(nip_max, ng0);
   StageTimer tm(c, FISDF_ST_SELECT);
@@ -1025,7 +1057,7 @@ int fisdf_select_points(fisdf_ctx* c, const void* x0v, int nk, int ng0, int nao,
   cplx* X4 = (cplx*)(b + oX4);
   // x2 = sum_q conj(x0_q) x0_q^T   (fftisdf.py:376-378; real part taken below) as one
   // K = nk*nao Hermitian rank-K update of the permuted x0
-  FISDF_TRY(select_gram(c, x0, nk, 0, nk, ng0, nao, X2, (cplx*)(b + oPm)));
+  FISDF_TRY(select_gram(c, x0, nk, 0, nk, ng0, nao, X2, (cplx*)(b + oPm), kmesh));
   // x4 = Re(x2)^2 / nk (:379) and the greedy pivoted Cholesky (:381-384), first nip_max
   // pivots: real blocked panels (X4's storage holds the real trailing matrix)
   int rank = 0;
@@ -1048,7 +1080,7 @@ int fisdf_select_gram(fisdf_ctx* c, const void* x0, int nk, int q0, int q1, int 
   }
   void* base;
   FISDF_TRY(arena_get(c, sizeof(cplx) * (size_t)ng0 * (q1 - q0) * nao, &base));
-  return select_gram(c, (const cplx*)x0, nk, q0, q1, ng0, nao, (cplx*)x2, (cplx*)base);
+  return select_gram(c, (const cplx*)x0, nk, q0, q1, ng0, nao, (cplx*)x2, (cplx*)base, nullptr);
 }
 
 int fisdf_select_pivots(fisdf_ctx* c, const void* x2, int nk, int ng0, int nip_max, double tol,
@@ -2704,6 +2736,9 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
   // the previous build's buffers go back first (its factor chain may still read x4)
   if (c->f_pending) FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
   build_return_all(c);
+  // time reversal (X_{-k} = conj(X_k), real AOs): the selection Gram, x2_k (x4) and fx_k (y)
+  // are formed for the representatives k <= -k only
+  FISDF_TRY(fisdf_set_time_reversal(c, o.time_reversal ? 1 : 0));
   fisdf_ctx::Build& B = c->bld;
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
   const long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
@@ -2716,7 +2751,8 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
     const int cap = o.nip_max > 0 ? std::min(o.nip_max, ng0) : ng0;
     perm.assign(cap, 0);
     int npiv = 0, full = 0;
-    FISDF_TRY(fisdf_select_points(c, x0, nk, ng0, nao, cap, o.select_tol, perm.data(), &npiv, &full));
+    FISDF_TRY(fisdf_select_points_km(c, x0, kmesh, ng0, nao, cap, o.select_tol, perm.data(), &npiv,
+                                     &full));
     perm.resize(std::min(cap, npiv));                                             // :383
   }
   const int nip = (int)perm.size();
@@ -2726,9 +2762,6 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
   FISDF_TRY(build_alloc(c, BR_X, sizeof(cplx) * (size_t)nk * nip * nao, &X));
   FISDF_TRY(fisdf_gather_points(c, x0, nk, ng0, nao, perm.data(), nip, X));        // :388
   FISDF_TRY(build_alloc(c, BR_X4, sizeof(cplx) * (size_t)nk * nn, &x4));
-  // time reversal (X_{-k} = conj(X_k)) before x4: its x2_k and the y build's fx_k are then
-  // formed for the representatives k <= -k only
-  FISDF_TRY(fisdf_set_time_reversal(c, o.time_reversal ? 1 : 0));
   FISDF_TRY(fisdf_build_x4(c, X, nip, nao, kmesh, a, x4));                         // :38-48
   std::vector<int> qs, partner;
   std::vector<double> wt;

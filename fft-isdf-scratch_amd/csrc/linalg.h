@@ -23,6 +23,11 @@ int trsm_merged_batched(hipStream_t s, const cplx* Q, long sQ, int r, cplx* X, l
 int trsm_split_k(int nc, int b1);
 long trsm_split_work_elems(int r, int batch);
 int set_identity(hipStream_t s, cplx* X, int n, int batch);
+// out[g][j*nao + m] = h_sc[j] * x0[h_k[j]][g][m], nsel <= 64 listed k
+int permute_kgm_sel(hipStream_t s, const cplx* x0, const int* h_k, const double* h_sc, int nsel,
+                    int ng, int nao, cplx* out);
+// the time-reversal representatives k <= -k (ascending) and whether each is self-paired
+void kmesh_reps(const int kmesh[3], std::vector<int>* reps, std::vector<char>* self);
 int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, long ldl, long sL, int r,
                  const cplx* Linv, long sLi, int nb, cplx* B, long ldb, long sB, cplx* X, long ldx,
                  long sX, int ncol, int batch, int a_real = 0);

@@ -1570,6 +1570,51 @@ int pair_product(hipStream_t s, const cplx* A, int n1, const cplx* B, int n2, in
   return 0;
 }
 
+// out[g][j*nao + m] = scale_j * x0[k_j][g][m] for the listed k (the time-reversal-folded Gram)
+struct KgmSel {
+  int k[64];
+  double sc[64];
+};
+__global__ void permute_kgm_sel_kernel(const cplx* __restrict__ x0, KgmSel sel, int nsel, int ng,
+                                       int nao, cplx* __restrict__ out) {
+  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long tot = (long)nsel * ng * nao;
+  if (e >= tot) return;
+  const int m = (int)(e % nao);
+  const int g = (int)((e / nao) % ng);
+  const int j = (int)(e / ((long)nao * ng));
+  out[(long)g * nsel * nao + (long)j * nao + m] = cscale(x0[((long)sel.k[j] * ng + g) * nao + m], sel.sc[j]);
+}
+
+int permute_kgm_sel(hipStream_t s, const cplx* x0, const int* h_k, const double* h_sc, int nsel,
+                    int ng, int nao, cplx* out) {
+  FISDF_CHECK(nsel >= 1 && nsel <= 64, "permute_kgm_sel: 1..64 k-points");
+  KgmSel sel;
+  for (int j = 0; j < nsel; ++j) {
+    sel.k[j] = h_k[j];
+    sel.sc[j] = h_sc[j];
+  }
+  const long n = (long)nsel * ng * nao;
+  hipLaunchKernelGGL(permute_kgm_sel_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, x0,
+                     sel, nsel, ng, nao, out);
+  FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+// the time-reversal representatives k <= -k of the k-mesh and whether each is its own partner
+void kmesh_reps(const int kmesh[3], std::vector<int>* reps, std::vector<char>* self) {
+  const int nk = kmesh[0] * kmesh[1] * kmesh[2];
+  reps->clear();
+  self->clear();
+  for (int k = 0; k < nk; ++k) {
+    const int p = kmesh_partner(k, kmesh[0], kmesh[1], kmesh[2]);
+    if (k <= p) {
+      reps->push_back(k);
+      self->push_back(k == p ? 1 : 0);
+    }
+  }
+}
+
 int permute_kgm(hipStream_t s, const cplx* x0, int nq, int ng, int nao, cplx* out) {
   long n = (long)nq * ng * nao;
   if (n == 0) return 0;

@@ -42,6 +42,7 @@ _SIGS = {
     "fisdf_timings": ([_vp, _dp, _ip], _i),
     "fisdf_max_imag": ([_vp, _dp], _i),
     "fisdf_select_points": ([_vp, _vp, _i, _i, _i, _i, _d, _ip, _ip, _ip], _i),
+    "fisdf_select_points_km": ([_vp, _vp, _ip, _i, _i, _i, _d, _ip, _ip, _ip], _i),
     "fisdf_gather_points": ([_vp, _vp, _i, _i, _i, _ip, _i, _vp], _i),
     "fisdf_eval_ao": ([_vp, _vp, _i, _i, _dp, _i, _ip, _ip, _ip, _dp, _dp, _i, _ip, _ip, _dp, _d,
                        _i, _vp], _i),

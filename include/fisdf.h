@@ -170,6 +170,11 @@ int fisdf_eval_ao_band(fisdf_ctx* ctx, const void* d_coords, int ng, int natm, c
  *   *h_full_rank = 1 if the tolerance (not nip_max) stopped the factorisation. */
 int fisdf_select_points(fisdf_ctx* ctx, const void* d_x0, int nk, int ng0, int nao, int nip_max,
                         double tol, int* h_perm, int* h_npiv, int* h_full_rank);
+/* The same for a k-mesh (x0 in get_kpts order over kmesh[0]*kmesh[1]*kmesh[2] k-points): with
+ * fisdf_set_time_reversal on (real AOs, x0_{-k} = conj(x0_k)) the Gram sums the representatives
+ * k <= -k only, a paired one counted twice (36 of 64 k at 4x4x4). */
+int fisdf_select_points_km(fisdf_ctx* ctx, const void* d_x0, const int kmesh[3], int ng0, int nao,
+                           int nip_max, double tol, int* h_perm, int* h_npiv, int* h_full_rank);
 
 /* The two halves of fisdf_select_points, for a k-point-sharded selection:
  * fisdf_select_gram: d_x2 (ng0, ng0) c128 = Re(sum_{q in [q0,q1)} x0_q x0_q^H) + 0i (the real

@@ -1,4 +1,4 @@
-# 1-GPU A/B on one box: the final library vs the one before the round's last three changes
+# 1-GPU A/B on one box: the working library vs libfisdf_pre.so (tools/build_base.sh REV pre)
 # (DFT x4, one-call W_s blocks, the faster HERK reduce), three alternating pairs
 set -o pipefail
 for i in 1 2 3; do
