@@ -507,7 +507,7 @@ __device__ __forceinline__ bool sc_better(double v2, int i2, double v, int i) {
 __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
     const cplx* __restrict__ X2, double scale, int n, int rmax, double tol, int RW, int K, int tpr,
     int* __restrict__ piv, int* __restrict__ rank, u32x4* __restrict__ rec,
-    double* __restrict__ Lg, int* __restrict__ err) {
+    double* __restrict__ Lg, int* __restrict__ err, unsigned long long* __restrict__ prof) {
   extern __shared__ double sm[];
   double* Lr = sm;                    // RW x K, row-major (columns >= K only in the global L)
   double* Lp = Lr + (long)RW * K;     // pivot row L[p, :j]
@@ -550,6 +550,9 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
         sc_store_rec(rec + (j & 1) * G + w, r);
       }
     }
+    // timing probe (FISDF_SEL_PROF): workgroup 0's phase boundaries of every step
+    const bool pr = prof != nullptr && w == 0 && tid == 0 && j < rmax;
+    if (pr) prof[4L * j] = __builtin_amdgcn_s_memrealtime();
     // ---- poll ----
     {
       double v = -1e300;
@@ -606,6 +609,7 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
     }
     const int p = s_p;
     const double dp = s_dp;
+    if (pr) prof[4L * j + 1] = __builtin_amdgcn_s_memrealtime();
     // ---- gather ----
     for (int c = tid; c < j; c += SC_THREADS)
       Lp[c] = __hip_atomic_load(&Lg[(long)p * rmax + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -614,6 +618,7 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
       w0[r] = x * x * scale;
     }
     __syncthreads();
+    if (pr) prof[4L * j + 2] = __builtin_amdgcn_s_memrealtime();
     // ---- column j ----
     {
       const double sq = sqrt(dp), inv = 1.0 / sq;
@@ -652,6 +657,7 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
       }
     }
     __syncthreads();
+    if (pr) prof[4L * j + 3] = __builtin_amdgcn_s_memrealtime();
     if (j + 1 >= rmax) return;
   }
 }
@@ -948,8 +954,15 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
     attr = true;
   }
+  // FISDF_SEL_PROF=1: per-step phase timestamps of workgroup 0 (timing probe), printed below
+  static unsigned long long* prof = nullptr;
+  const bool want_prof = getenv("FISDF_SEL_PROF") != nullptr;
+  if (want_prof && !prof) FISDF_HIP(hipMalloc(&prof, sizeof(unsigned long long) * 4 * 8192));
+  unsigned long long* profp = want_prof ? prof : nullptr;
+  if (profp) FISDF_HIP(hipMemsetAsync(profp, 0, sizeof(unsigned long long) * 4 * rmax, s));
   void* args[] = {(void*)&X2, (void*)&scale, (void*)&n,   (void*)&rmax, (void*)&tol, (void*)&RW,
-                  (void*)&K,   (void*)&tpr,   (void*)&piv, (void*)&rank, (void*)&rec, (void*)&Lg,   (void*)&err};
+                  (void*)&K,   (void*)&tpr,   (void*)&piv, (void*)&rank, (void*)&rec, (void*)&Lg,
+                  (void*)&err, (void*)&profp};
   const hipError_t e = hipLaunchCooperativeKernel((const void*)pchol_select_coop, dim3(G),
                                                   dim3(SC_THREADS), args, (unsigned)lds, s);
   if (e != hipSuccess) {  // refused (e.g. not co-resident): the caller's blocked path runs
@@ -958,6 +971,27 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
   }
   *err_dev = err;
   *handled = true;
+  if (profp && rmax <= 8192) {
+    std::vector<unsigned long long> h(4 * (size_t)rmax);
+    FISDF_HIP(hipMemcpyAsync(h.data(), profp, sizeof(unsigned long long) * h.size(),
+                             hipMemcpyDeviceToHost, s));
+    FISDF_HIP(hipStreamSynchronize(s));
+    double ph[4] = {0, 0, 0, 0};
+    int cnt = 0;
+    for (int j = 1; j < rmax; ++j) {
+      const unsigned long long* a = &h[4 * (size_t)j];
+      const unsigned long long prev = h[4 * (size_t)(j - 1) + 3];
+      if (!a[0] || !a[1] || !a[2] || !a[3] || !prev) continue;
+      ph[0] += (double)(a[0] - prev);  // step start -> record posted (the post's reduction)
+      ph[1] += (double)(a[1] - a[0]);  // posted -> winner known (poll + block arg-max)
+      ph[2] += (double)(a[2] - a[1]);  // gather of L[p, :j] and x4[p, rows]
+      ph[3] += (double)(a[3] - a[2]);  // column j
+      ++cnt;
+    }
+    if (cnt)  // s_memrealtime: 100 MHz
+      fprintf(stderr, "select coop G=%d RW=%d: per step (us) post %.2f, exchange %.2f, gather %.2f, column %.2f\n",
+              G, RW, ph[0] / cnt / 100.0, ph[1] / cnt / 100.0, ph[2] / cnt / 100.0, ph[3] / cnt / 100.0);
+  }
   return 0;
 }
 
