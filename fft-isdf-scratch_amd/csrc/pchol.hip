@@ -485,8 +485,11 @@ __global__ __launch_bounds__(256) void syrk_real_update(double* __restrict__ W, 
 // and stores (no per-step L2 write-back/invalidate).  Records are double-buffered by step
 // parity (a workgroup runs at most one step ahead).  Every wait is bounded: a stalled step
 // sets *err and every workgroup exits (the caller then falls back to the blocked path).
-constexpr int SC_THREADS = 256;
-constexpr int SC_MAXRW = SC_THREADS / 8;  // 8 threads per owned row
+// 512 threads: the column step's dot products over the owned L rows take 16 threads per row at C3
+// (27 rows) instead of 8, halving the dependent LDS-load chain of the step's longest phase
+// (per-step phase timing, FISDF_SEL_PROF: 1.86 of ≈ 5.9 us at 256 threads)
+constexpr int SC_THREADS = 512;
+constexpr int SC_MAXRW = SC_THREADS / 8;  // at least 8 threads per owned row
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void sc_store_rec(u32x4* addr, u32x4 v) {
@@ -928,7 +931,7 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
   size_t lds = sizeof(double) * ((size_t)RW * rmax + rmax + 2 * (size_t)RW);
   if (lds > kLds || kcap > 0) {
     // the owned L rows do not fit: one workgroup per CU, the first K columns in LDS and the
-    // rest read back (agent-coherent) from the global L; 16 threads per row when RW <= 16
+    // rest read back (agent-coherent) from the global L
     G = std::min(ncu, (n + 7) / 8);
     RW = (n + G - 1) / G;
     G = (n + RW - 1) / RW;
@@ -936,10 +939,12 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
     if (kcap > 0) K = std::min(K, kcap);
     if (K < 16) return 0;
     K = std::min(K, rmax);
-    tpr = RW <= SC_THREADS / 16 ? 16 : 8;
+    tpr = 8;
     lds = sizeof(double) * ((size_t)RW * K + rmax + 2 * (size_t)RW);
   }
   if (lds > kLds || RW > SC_MAXRW) return 0;
+  // threads per owned row: the most (a power of two, <= 32) that the workgroup holds
+  while (tpr < 32 && RW * tpr * 2 <= SC_THREADS) tpr *= 2;
   // scratch in the caller's work area (n*n doubles): records, global L, error flag
   u32x4* rec = (u32x4*)work;
   double* Lg = work + 4 * G;
