@@ -8,6 +8,8 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -18,12 +20,18 @@ namespace fisdf {
 
 static thread_local std::string g_last_error;
 // the context the calling thread is working on (set by the entry points' guards): a failure is
-// recorded in it too, so fisdf_last_error(ctx) reports that context's own last failure
+// recorded in it too, so fisdf_last_error(ctx) reports that context's own last failure.  Only a
+// context that is still alive is written (one destroyed on another thread must not
+// be), and fisdf_create clears it, so its failures go to fisdf_last_error(NULL) only
 static thread_local fisdf_ctx* t_cur_ctx = nullptr;
+static std::mutex g_live_mu;
+static std::set<const fisdf_ctx*> g_live;
 void set_ctx_error(fisdf_ctx* c, const std::string& msg);
 void set_error(const std::string& msg) {
   g_last_error = msg;
-  if (t_cur_ctx) set_ctx_error(t_cur_ctx, msg);
+  if (!t_cur_ctx) return;
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  if (g_live.count(t_cur_ctx)) set_ctx_error(t_cur_ctx, msg);
 }
 
 LaunchEvents& launch_events() {
@@ -97,6 +105,11 @@ struct fisdf_ctx {
   // extra streams of the fit lanes (fisdf_fit_coulomb_qs)
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
+  // cross-stream ordering of buffers handed back to the caller's allocator: a
+  // call that gives aux[i] work bumps aux_use[i]; joining aux[i] into `stream` (aux_join) sets
+  // aux_joined[i] = aux_use[i].  build_return asserts every aux stream is joined, so a buffer
+  // freed stream-ordered on `stream` has no reader left on another stream
+  unsigned aux_use[3] = {0, 0, 0}, aux_joined[3] = {0, 0, 0};
   hipEvent_t ev_ybuf[4] = {nullptr, nullptr, nullptr, nullptr};  // y pipeline: fx ready / free
   std::vector<hipEvent_t> ev_q;  // FISDF_FIT_PIPE: Yhat of fitted q ready (FFT stream)
   std::vector<hipEvent_t> ev_free;  // FISDF_FIT_PIPE: Yhat ring slot read by its lane
@@ -131,6 +144,11 @@ struct fisdf_ctx {
   hipEvent_t ev_stage = nullptr;
   // reality-invariant monitors
   unsigned long long* maximag = nullptr;  // 3 slots
+  // time-reversal check of the build's AO inputs (x0, f): {max dev, max |a|} x 2 on the device,
+  // read back through tr_pinned when ev_tr completes
+  unsigned long long* trmon = nullptr;
+  unsigned long long* tr_pinned = nullptr;
+  hipEvent_t ev_tr = nullptr, ev_trfork = nullptr;
   // timing
   bool timing = false;
   struct Ev { int stage; hipEvent_t a, b; int span; };
@@ -145,6 +163,8 @@ struct fisdf_ctx {
   struct Build {
     bool valid = false;
     int nk = 0, nip = 0, nao = 0, ng0 = 0, nfit = 0, used_pivoted = 0, min_norm = 0;
+    int time_reversal = 0;  // 1: one q of each (q, -q) pair fitted (the inputs passed the check)
+    double tr_deviation = 0.0;
     int kmesh[3] = {0, 0, 0}, mesh[3] = {0, 0, 0};
     double a[9] = {0};
     std::vector<int> perm, fit_qs, partner, ranks;
@@ -600,6 +620,25 @@ std::vector<int> q_range(int q0, int q1) {
   return v;
 }
 
+// aux[i] is given work that may read a build buffer (fork side of the invariant above)
+void aux_fork(fisdf_ctx* c, int i) { ++c->aux_use[i]; }
+
+// join aux[i] into the main stream: later work (and frees) on `stream` are ordered after it
+int aux_join(fisdf_ctx* c, int i) {
+  FISDF_HIP(hipEventRecord(c->ev_join[i], c->aux[i]));
+  FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_join[i], 0));
+  c->aux_joined[i] = c->aux_use[i];
+  return 0;
+}
+
+int check_aux_joined(fisdf_ctx* c, const char* what) {
+  for (int i = 0; i < 3; ++i)
+    FISDF_CHECK(c->aux_joined[i] == c->aux_use[i],
+                std::string(what) + ": aux stream " + std::to_string(i) +
+                    " not joined into the context stream (a buffer would be freed under a reader)");
+  return 0;
+}
+
 int check_qlist(const int* qs, int nq, int nk, const char* who) {
   FISDF_CHECK(nq >= 0 && (nq == 0 || qs != nullptr), std::string(who) + ": bad q-list");
   for (int i = 0; i < nq; ++i)
@@ -650,6 +689,7 @@ const char* fisdf_last_error(const fisdf_ctx* c) {
 }
 
 int fisdf_create(int device, void* stream, fisdf_ctx** out) {
+  t_cur_ctx = nullptr;
   FISDF_CHECK(out != nullptr, "out is null");
   int ndev = 0;
   FISDF_HIP(hipGetDeviceCount(&ndev));
@@ -662,12 +702,20 @@ int fisdf_create(int device, void* stream, fisdf_ctx** out) {
   c->own_stream = false;
   FISDF_HIP(hipMalloc(&c->maximag, 4 * sizeof(unsigned long long)));
   FISDF_HIP(hipMemsetAsync(c->maximag, 0, 4 * sizeof(unsigned long long), c->stream));
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    g_live.insert(c);
+  }
   *out = c;
   return 0;
 }
 
 int fisdf_destroy(fisdf_ctx* c) {
   if (!c) return 0;
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    g_live.erase(c);
+  }
   if (t_cur_ctx == c) t_cur_ctx = nullptr;
   FISDF_HIP(hipSetDevice(c->device));
   FISDF_HIP(hipStreamSynchronize(c->stream));
@@ -717,6 +765,10 @@ int fisdf_destroy(fisdf_ctx* c) {
   if (c->stage_pinned) (void)hipHostFree(c->stage_pinned);
   if (c->sel_pinned) (void)hipHostFree(c->sel_pinned);
   if (c->maximag) (void)hipFree(c->maximag);
+  if (c->ev_tr) (void)hipEventSynchronize(c->ev_tr), (void)hipEventDestroy(c->ev_tr);
+  if (c->ev_trfork) (void)hipEventDestroy(c->ev_trfork);
+  if (c->trmon) (void)hipFree(c->trmon);
+  if (c->tr_pinned) (void)hipHostFree(c->tr_pinned);
   if (c->spans) (void)hipFree(c->spans);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1325,6 +1377,7 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
   if (nbuf == 2) {
     FISDF_TRY(ensure_aux(c));
     sk = c->aux[0];
+    aux_fork(c, 0);
     FISDF_HIP(hipEventRecord(c->ev_fork, c->stream));
     FISDF_HIP(hipStreamWaitEvent(sk, c->ev_fork, 0));
   }
@@ -1356,10 +1409,8 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
                       (long)g0 + s0, half, c->maximag + 1));
     if (nbuf == 2) FISDF_HIP(hipEventRecord(c->ev_ybuf[2 + bi], sk));
   }
-  if (nbuf == 2) {  // later work on the main stream (the fit, the arena's next user) sees y
-    FISDF_HIP(hipEventRecord(c->ev_join[0], sk));
-    FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_join[0], 0));
-  }
+  if (nbuf == 2) FISDF_TRY(aux_join(c, 0));  // later work on the main stream (the fit, the
+                                             // arena's next user) sees y
   return 0;
 }
 
@@ -2026,6 +2077,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     for (int l = 0; l < NL; ++l) {
       lane_st[l] = c->aux[l];
       aux_used[l] = true;
+      aux_fork(c, l);
       FISDF_HIP(hipStreamWaitEvent(lane_st[l], c->ev_ready[0], 0));
     }
     FISDF_HIP(hipMemsetAsync(G, 0, sizeof(cplx) * nq * rr, lane_st[0]));
@@ -2034,6 +2086,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     if (pipe) {
       fst = c->aux[2];
       aux_used[2] = true;
+      aux_fork(c, 2);
       FISDF_HIP(hipStreamWaitEvent(fst, c->ev_fork, 0));
     }
   } else if (NL > 1 || pipe) {
@@ -2043,11 +2096,13 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     for (int l = 1; l < NL; ++l) {
       lane_st[l] = c->aux[l - 1];
       aux_used[l - 1] = true;
+      aux_fork(c, l - 1);
       FISDF_HIP(hipStreamWaitEvent(lane_st[l], c->ev_fork, 0));
     }
     if (pipe) {
       fst = c->aux[2];
       aux_used[2] = true;
+      aux_fork(c, 2);
       FISDF_HIP(hipStreamWaitEvent(fst, c->ev_fork, 0));
     }
   } else {
@@ -2198,11 +2253,10 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   }
   // join the lanes (and the FFT stream: that keeps the arena reuse ordered) before the batched
   // small stage on the main stream
-  for (int i = 0; i < 3; ++i) {
-    if (!aux_used[i]) continue;
-    FISDF_HIP(hipEventRecord(c->ev_join[i], c->aux[i]));
-    FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_join[i], 0));
-  }
+  // (this join is what makes fisdf_build's build_return(c, yT) right after this call safe: every
+  // FFT / lane read of y is ordered before the caller's stream-ordered free on c->stream)
+  for (int i = 0; i < 3; ++i)
+    if (aux_used[i]) FISDF_TRY(aux_join(c, i));
   FISDF_TRY(join_factors(c));
   {
     StageTimer tm(c, FISDF_ST_SMALL);
@@ -2636,16 +2690,26 @@ int build_alloc(fisdf_ctx* c, int role, size_t bytes, void** out) {
   return 0;
 }
 
-// hand one lent buffer back (stream-ordered: its last use is enqueued on c->stream)
-void build_return(fisdf_ctx* c, void* p) {
-  if (!c->alloc_fn || !p) return;
+// hand one lent buffer back (stream-ordered: its last use is enqueued on c->stream, and every
+// aux stream that read it has been joined into c->stream — checked)
+int build_return(fisdf_ctx* c, void* p) {
+  if (!c->alloc_fn || !p) return 0;
   auto it = std::find(c->lent.begin(), c->lent.end(), p);
-  if (it == c->lent.end()) return;
+  if (it == c->lent.end()) return 0;
+  FISDF_TRY(check_aux_joined(c, "build_return"));
   c->lent.erase(it);
   if (c->free_fn) c->free_fn(p, c->alloc_user);
+  return 0;
 }
 
 void build_return_all(fisdf_ctx* c) {
+  // an earlier call that failed between a fork and its join may have left an aux stream with
+  // work: drain it before the caller's allocator gets the buffers back
+  for (int i = 0; i < 3; ++i)
+    if (c->aux_joined[i] != c->aux_use[i]) {
+      if (c->aux[i]) (void)hipStreamSynchronize(c->aux[i]);
+      c->aux_joined[i] = c->aux_use[i];
+    }
   std::vector<void*> l;
   l.swap(c->lent);
   if (c->free_fn)
@@ -2677,9 +2741,91 @@ void tr_classes(const int km[3], bool on, std::vector<int>& reps, std::vector<in
   }
 }
 
+// time reversal of the AO inputs (what the fold over k <= -k of the selection Gram, x4 and y, and
+// W_{-q} = conj(W_q), rely on): a[-k] = conj(a[k]) holds for real basis functions on a k-mesh
+// containing -k (get_kpts order, no shift).  The check reads x0 and f once on stream `st` (about
+// 0.25 ms at C3) and lands in tr_pinned behind ev_tr; tr_verdict waits for it.
+int tr_alloc(fisdf_ctx* c) {
+  if (c->trmon) return 0;
+  FISDF_HIP(hipMalloc(&c->trmon, 4 * sizeof(unsigned long long)));
+  FISDF_HIP(hipHostMalloc((void**)&c->tr_pinned, 4 * sizeof(unsigned long long),
+                          hipHostMallocDefault));
+  FISDF_HIP(hipEventCreateWithFlags(&c->ev_tr, hipEventDisableTiming));
+  FISDF_HIP(hipEventCreateWithFlags(&c->ev_trfork, hipEventDisableTiming));
+  FISDF_HIP(hipEventRecord(c->ev_tr, c->stream));
+  return 0;
+}
+
+int tr_check_enqueue(fisdf_ctx* c, hipStream_t st, const cplx* x0, long ng0, const cplx* f,
+                     long ngrid, int nao, const int kmesh[3]) {
+  FISDF_TRY(tr_alloc(c));
+  FISDF_HIP(hipEventSynchronize(c->ev_tr));  // the pinned words are rewritten below
+  FISDF_HIP(hipMemsetAsync(c->trmon, 0, 4 * sizeof(unsigned long long), st));
+  FISDF_TRY(tr_check(st, x0, ng0 * nao, ng0 * nao, kmesh, c->trmon));
+  if (f) FISDF_TRY(tr_check(st, f, ngrid * nao, ngrid * nao, kmesh, c->trmon + 2));
+  FISDF_HIP(hipMemcpyAsync(c->tr_pinned, c->trmon, 4 * sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, st));
+  FISDF_HIP(hipEventRecord(c->ev_tr, st));
+  return 0;
+}
+
+// the largest relative violation max |a[-k] - conj(a[k])| / max |a| of the last check
+int tr_verdict(fisdf_ctx* c, double* rel) {
+  FISDF_HIP(hipEventSynchronize(c->ev_tr));
+  double v[4];
+  for (int i = 0; i < 4; ++i) v[i] = __builtin_bit_cast(double, c->tr_pinned[i]);
+  *rel = 0.0;
+  for (int i = 0; i < 2; ++i)
+    if (v[2 * i + 1] > 0.0) *rel = std::max(*rel, v[2 * i] / v[2 * i + 1]);
+  return 0;
+}
+
+// tolerance of the check: rounding of the lattice phases e^{ik.T} is ~1e-15 relative; a complex
+// basis or a shifted k-mesh violates the symmetry at O(1)
+constexpr double kTrTol = 1e-9;
+
+// the composite build's context-wide stage settings, restored when fisdf_build returns (ADVICE
+// r04: a stage-API caller on the same context must not inherit them)
+struct StageSettings {
+  fisdf_ctx* c;
+  bool time_reversal;
+  int force_pivoted, fit_mode, half_grid, factor_hi;
+  double omega;
+  explicit StageSettings(fisdf_ctx* cc)
+      : c(cc), time_reversal(cc->time_reversal), force_pivoted(cc->force_pivoted),
+        fit_mode(cc->fit_mode), half_grid(cc->half_grid), factor_hi(cc->factor_hi),
+        omega(cc->omega) {}
+  ~StageSettings() {
+    c->time_reversal = time_reversal;
+    c->force_pivoted = force_pivoted;
+    c->fit_mode = fit_mode;
+    c->half_grid = half_grid;
+    c->factor_hi = factor_hi;
+    c->omega = omega;
+  }
+};
+
 }  // namespace
 
 extern "C" {
+
+int fisdf_check_time_reversal(fisdf_ctx* c, const void* d_a, long k_stride, long per_k,
+                              const int kmesh[3], double* h_out) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(d_a && kmesh && h_out, "check_time_reversal: null argument");
+  FISDF_CHECK(kmesh[0] > 0 && kmesh[1] > 0 && kmesh[2] > 0, "check_time_reversal: bad k-mesh");
+  FISDF_CHECK(per_k > 0 && k_stride >= per_k, "check_time_reversal: bad sizes");
+  FISDF_TRY(tr_alloc(c));
+  FISDF_HIP(hipEventSynchronize(c->ev_tr));
+  FISDF_HIP(hipMemsetAsync(c->trmon, 0, 4 * sizeof(unsigned long long), c->stream));
+  FISDF_TRY(tr_check(c->stream, (const cplx*)d_a, k_stride, per_k, kmesh, c->trmon));
+  unsigned long long h[2];
+  FISDF_HIP(hipMemcpyAsync(h, c->trmon, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  FISDF_HIP(hipStreamSynchronize(c->stream));
+  h_out[0] = __builtin_bit_cast(double, h[0]);
+  h_out[1] = __builtin_bit_cast(double, h[1]);
+  return 0;
+}
 
 void fisdf_build_opts_default(fisdf_build_opts* o) {
   if (!o) return;
@@ -2736,24 +2882,53 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
   // the previous build's buffers go back first (its factor chain may still read x4)
   if (c->f_pending) FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
   build_return_all(c);
-  // time reversal (X_{-k} = conj(X_k), real AOs): the selection Gram, x2_k (x4) and fx_k (y)
-  // are formed for the representatives k <= -k only
-  FISDF_TRY(fisdf_set_time_reversal(c, o.time_reversal ? 1 : 0));
+  StageSettings keep(c);
   fisdf_ctx::Build& B = c->bld;
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
   const long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
   FISDF_CHECK(ngrid < (1L << 31), "build: mesh too large");
+  FISDF_TRY(fisdf_set_factor_priority(c, 0));
+  // time reversal (X_{-k} = conj(X_k), real AOs): the selection Gram, x2_k (x4) and fx_k (y)
+  // are formed for the representatives k <= -k only.  The inputs are checked on the side
+  // stream beside the selection; a violation (complex basis, shifted k-mesh) is found when the
+  // selection returns, and the build then starts over with every q fitted
+  bool tr = o.time_reversal != 0;
+  double tr_dev = 0.0;
+  // FISDF_TR_CHECK=0 trusts the inputs (A/B of the check's cost only)
+  static const bool tr_check_on = [] {
+    const char* e = getenv("FISDF_TR_CHECK");
+    return !(e && e[0] == '0');
+  }();
+  const bool check_tr = tr && tr_check_on;
+  if (check_tr) {
+    FISDF_TRY(ensure_side(c));
+    FISDF_TRY(tr_alloc(c));
+    FISDF_HIP(hipEventRecord(c->ev_trfork, c->stream));
+    FISDF_HIP(hipStreamWaitEvent(c->side, c->ev_trfork, 0));
+    FISDF_TRY(tr_check_enqueue(c, c->side, (const cplx*)x0, ng0, (const cplx*)f, ngrid, nao,
+                               kmesh));
+  }
   // interpolation points (:33 -> :357-388), or the caller's
   std::vector<int> perm;
-  if (o.perm) {
-    perm.assign(o.perm, o.perm + o.n_perm);
-  } else {
-    const int cap = o.nip_max > 0 ? std::min(o.nip_max, ng0) : ng0;
-    perm.assign(cap, 0);
-    int npiv = 0, full = 0;
-    FISDF_TRY(fisdf_select_points_km(c, x0, kmesh, ng0, nao, cap, o.select_tol, perm.data(), &npiv,
-                                     &full));
-    perm.resize(std::min(cap, npiv));                                             // :383
+  for (int attempt = 0;; ++attempt) {
+    FISDF_TRY(fisdf_set_time_reversal(c, tr ? 1 : 0));
+    if (o.perm) {
+      perm.assign(o.perm, o.perm + o.n_perm);
+    } else {
+      const int cap = o.nip_max > 0 ? std::min(o.nip_max, ng0) : ng0;
+      perm.assign(cap, 0);
+      int npiv = 0, full = 0;
+      FISDF_TRY(fisdf_select_points_km(c, x0, kmesh, ng0, nao, cap, o.select_tol, perm.data(),
+                                       &npiv, &full));
+      perm.resize(std::min(cap, npiv));                                           // :383
+    }
+    if (!check_tr || attempt > 0) break;
+    FISDF_TRY(tr_verdict(c, &tr_dev));
+    if (tr_dev <= kTrTol) break;
+    if (getenv("FISDF_VERBOSE"))
+      fprintf(stderr, "fisdf: build: AO inputs violate time reversal (max |a[-k] - conj(a[k])| / "
+                      "max |a| = %.3e): every q fitted\n", tr_dev);
+    tr = false;
   }
   const int nip = (int)perm.size();
   FISDF_CHECK(nip > 0, "build: no interpolation points");
@@ -2765,13 +2940,12 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
   FISDF_TRY(fisdf_build_x4(c, X, nip, nao, kmesh, a, x4));                         // :38-48
   std::vector<int> qs, partner;
   std::vector<double> wt;
-  tr_classes(kmesh, o.time_reversal != 0, qs, partner, wt);
+  tr_classes(kmesh, tr, qs, partner, wt);
   const int nq = (int)qs.size();
   // the factorisation (replaces zgelsy's QRCP, :108) on the side stream, overlapped with y
   FISDF_TRY(fisdf_set_pivoted_fit(c, o.pivoted_fit));
   FISDF_TRY(fisdf_set_fit_mode(c, o.fit_mode));
   FISDF_TRY(fisdf_set_half_grid(c, o.half_grid));
-  FISDF_TRY(fisdf_set_factor_priority(c, 0));
   FISDF_TRY(fisdf_factor_x4_mark(c));
   FISDF_TRY(fisdf_set_omega(c, o.omega));
   void* yT;
@@ -2789,7 +2963,9 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
   int used = 0, ncod = 0;
   FISDF_TRY(fisdf_factor_info(c, &used));
   FISDF_TRY(fisdf_min_norm_info(c, &ncod));
-  build_return(c, yT);  // y is dead once the fit is enqueued (stream-ordered)
+  // y is dead once the fit is enqueued: fit_coulomb_qs joined its lanes and FFT stream into
+  // c->stream, so the caller's stream-ordered free cannot overtake a reader
+  FISDF_TRY(build_return(c, yT));
   FISDF_TRY(build_alloc(c, BR_WS, sizeof(double) * (size_t)nk * nn, &Ws));
   FISDF_TRY(fisdf_build_ws_qs(c, Wq, qs.data(), wt.data(), nq, nip, kmesh, a, Ws)); // :204-207
   B.valid = true;
@@ -2800,6 +2976,8 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
   B.nfit = nq;
   B.used_pivoted = used;
   B.min_norm = ncod;
+  B.time_reversal = tr ? 1 : 0;
+  B.tr_deviation = tr_dev;
   for (int i = 0; i < 3; ++i) B.kmesh[i] = kmesh[i], B.mesh[i] = mesh[i];
   for (int i = 0; i < 9; ++i) B.a[i] = a[i];
   B.perm = perm;
@@ -2834,6 +3012,8 @@ int fisdf_build_get(fisdf_ctx* c, fisdf_build_result* out) {
   out->d_x4 = B.x4;
   out->d_Wq = B.Wq;
   out->d_Ws = B.Ws;
+  out->time_reversal = B.time_reversal;
+  out->tr_deviation = B.tr_deviation;
   return 0;
 }
 

@@ -1570,34 +1570,40 @@ int pair_product(hipStream_t s, const cplx* A, int n1, const cplx* B, int n2, in
   return 0;
 }
 
-// out[g][j*nao + m] = scale_j * x0[k_j][g][m] for the listed k (the time-reversal-folded Gram)
+// out[g][j*nao + m] = scale_j * x0[k_j][g][m] for the listed k (the time-reversal-folded Gram);
+// the k list travels in the kernel argument block, 64 entries per launch: a longer list (more
+// than 64 representatives, e.g. 112 at 6x6x6) runs as several launches over column ranges
 struct KgmSel {
   int k[64];
   double sc[64];
 };
-__global__ void permute_kgm_sel_kernel(const cplx* __restrict__ x0, KgmSel sel, int nsel, int ng,
-                                       int nao, cplx* __restrict__ out) {
+__global__ void permute_kgm_sel_kernel(const cplx* __restrict__ x0, KgmSel sel, int j0, int nchunk,
+                                       int nsel, int ng, int nao, cplx* __restrict__ out) {
   long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  const long tot = (long)nsel * ng * nao;
+  const long tot = (long)nchunk * ng * nao;
   if (e >= tot) return;
   const int m = (int)(e % nao);
   const int g = (int)((e / nao) % ng);
   const int j = (int)(e / ((long)nao * ng));
-  out[(long)g * nsel * nao + (long)j * nao + m] = cscale(x0[((long)sel.k[j] * ng + g) * nao + m], sel.sc[j]);
+  out[(long)g * nsel * nao + (long)(j0 + j) * nao + m] =
+      cscale(x0[((long)sel.k[j] * ng + g) * nao + m], sel.sc[j]);
 }
 
 int permute_kgm_sel(hipStream_t s, const cplx* x0, const int* h_k, const double* h_sc, int nsel,
                     int ng, int nao, cplx* out) {
-  FISDF_CHECK(nsel >= 1 && nsel <= 64, "permute_kgm_sel: 1..64 k-points");
-  KgmSel sel;
-  for (int j = 0; j < nsel; ++j) {
-    sel.k[j] = h_k[j];
-    sel.sc[j] = h_sc[j];
+  FISDF_CHECK(nsel >= 1, "permute_kgm_sel: no k-points");
+  for (int j0 = 0; j0 < nsel; j0 += 64) {
+    const int nc = std::min(64, nsel - j0);
+    KgmSel sel;
+    for (int j = 0; j < nc; ++j) {
+      sel.k[j] = h_k[j0 + j];
+      sel.sc[j] = h_sc[j0 + j];
+    }
+    const long n = (long)nc * ng * nao;
+    hipLaunchKernelGGL(permute_kgm_sel_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s,
+                       x0, sel, j0, nc, nsel, ng, nao, out);
+    FISDF_HIP(hipGetLastError());
   }
-  const long n = (long)nsel * ng * nao;
-  hipLaunchKernelGGL(permute_kgm_sel_kernel, dim3(nblocks(n, 256, 1L << 30)), dim3(256), 0, s, x0,
-                     sel, nsel, ng, nao, out);
-  FISDF_HIP(hipGetLastError());
   return 0;
 }
 
@@ -1613,6 +1619,46 @@ void kmesh_reps(const int kmesh[3], std::vector<int>* reps, std::vector<char>* s
       self->push_back(k == p ? 1 : 0);
     }
   }
+}
+
+// time-reversal check of Bloch AO values a[k][r][m] (k stride ks): mon[0] = max over the
+// representatives k <= -k of |a[-k] - conj(a[k])| (2 |Im a[k]| on a self-paired k), mon[1] = max
+// |a[k]|, both as the ordered bit patterns of non-negative doubles.  Every pair is read once.
+__global__ void tr_check_kernel(const cplx* __restrict__ a, long ks, long per_k, int n0, int n1,
+                                int n2, unsigned long long* __restrict__ mon) {
+  const int nk = n0 * n1 * n2;
+  double dev = 0.0, mag = 0.0;
+  const long tot = (long)nk * per_k;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot;
+       e += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(e / per_k);
+    const long r = e - (long)k * per_k;
+    const int p = kmesh_partner(k, n0, n1, n2);
+    if (p < k) continue;
+    const cplx u = a[k * ks + r];
+    const cplx v = p == k ? u : a[p * ks + r];
+    dev = fmax(dev, fmax(fabs(v.x - u.x), fabs(v.y + u.y)));
+    mag = fmax(mag, fmax(fabs(u.x), fabs(u.y)));
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    dev = fmax(dev, __shfl_xor(dev, o, 64));
+    mag = fmax(mag, __shfl_xor(mag, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(mon, (unsigned long long)__double_as_longlong(dev));
+    atomicMax(mon + 1, (unsigned long long)__double_as_longlong(mag));
+  }
+}
+
+int tr_check(hipStream_t s, const cplx* a, long ks, long per_k, const int kmesh[3],
+             unsigned long long* mon) {
+  FISDF_CHECK(per_k > 0 && ks >= per_k && kmesh[0] > 0 && kmesh[1] > 0 && kmesh[2] > 0,
+              "tr_check: bad sizes");
+  const long n = (long)kmesh[0] * kmesh[1] * kmesh[2] * per_k;
+  hipLaunchKernelGGL(tr_check_kernel, dim3(nblocks(n, 256, 4096)), dim3(256), 0, s, a, ks, per_k,
+                     kmesh[0], kmesh[1], kmesh[2], mon);
+  FISDF_HIP(hipGetLastError());
+  return 0;
 }
 
 int permute_kgm(hipStream_t s, const cplx* x0, int nq, int ng, int nao, cplx* out) {

@@ -959,11 +959,16 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
     attr = true;
   }
-  // FISDF_SEL_PROF=1: per-step phase timestamps of workgroup 0 (timing probe), printed below
-  static unsigned long long* prof = nullptr;
-  const bool want_prof = getenv("FISDF_SEL_PROF") != nullptr;
-  if (want_prof && !prof) FISDF_HIP(hipMalloc(&prof, sizeof(unsigned long long) * 4 * 8192));
-  unsigned long long* profp = want_prof ? prof : nullptr;
+  // FISDF_SEL_PROF=1: per-step phase timestamps of workgroup 0 (timing probe), printed below;
+  // one 8192-step buffer per device, the probe off for longer selections
+  constexpr int kProfSteps = 8192;
+  static unsigned long long* prof[64] = {};
+  int pdev = 0;
+  FISDF_HIP(hipGetDevice(&pdev));
+  const bool want_prof = getenv("FISDF_SEL_PROF") != nullptr && rmax <= kProfSteps && pdev < 64;
+  if (want_prof && !prof[pdev])
+    FISDF_HIP(hipMalloc(&prof[pdev], sizeof(unsigned long long) * 4 * kProfSteps));
+  unsigned long long* profp = want_prof ? prof[pdev] : nullptr;
   if (profp) FISDF_HIP(hipMemsetAsync(profp, 0, sizeof(unsigned long long) * 4 * rmax, s));
   void* args[] = {(void*)&X2, (void*)&scale, (void*)&n,   (void*)&rmax, (void*)&tol, (void*)&RW,
                   (void*)&K,   (void*)&tpr,   (void*)&piv, (void*)&rank, (void*)&rec, (void*)&Lg,
@@ -976,7 +981,7 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
   }
   *err_dev = err;
   *handled = true;
-  if (profp && rmax <= 8192) {
+  if (profp) {
     std::vector<unsigned long long> h(4 * (size_t)rmax);
     FISDF_HIP(hipMemcpyAsync(h.data(), profp, sizeof(unsigned long long) * h.size(),
                              hipMemcpyDeviceToHost, s));

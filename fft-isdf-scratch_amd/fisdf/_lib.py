@@ -107,7 +107,11 @@ _SIGS = {
     "fisdf_get_wq": ([_vp, _vp], _i),
     "fisdf_get_jk": ([_vp, _vp, _i, _i, _i, _vp, _vp], _i),
     "fisdf_set_allocator": ([_vp, _vp, _vp, _vp], _i),
+    "fisdf_check_time_reversal": ([_vp, _vp, _l, _l, _ip, _dp], _i),
 }
+
+# FISDF_ABI_VERSION of include/fisdf.h this binding's structs follow
+ABI_VERSION = 3
 
 
 class BuildOpts(C.Structure):
@@ -121,7 +125,8 @@ class BuildResult(C.Structure):
     """struct fisdf_build_result (include/fisdf.h)."""
     _fields_ = [("nk", _i), ("nip", _i), ("nao", _i), ("nfit", _i), ("used_pivoted_fit", _i),
                 ("min_norm_slots", _i), ("perm", _ip), ("fit_qs", _ip), ("ranks", _ip),
-                ("partner", _ip), ("d_X", _vp), ("d_x4", _vp), ("d_Wq", _vp), ("d_Ws", _vp)]
+                ("partner", _ip), ("d_X", _vp), ("d_x4", _vp), ("d_Wq", _vp), ("d_Ws", _vp),
+                ("time_reversal", _i), ("tr_deviation", _d)]
 
 
 # fisdf_alloc_fn / fisdf_free_fn
@@ -149,6 +154,9 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
+    if not os.environ.get("FISDF_LIB_VARIANT") and lib.fisdf_abi_version() != ABI_VERSION:
+        raise FisdfError(f"{path}: ABI version {lib.fisdf_abi_version()}, the binding expects "
+                         f"{ABI_VERSION} (rebuild the library)")
     _lib = lib
     return lib
 

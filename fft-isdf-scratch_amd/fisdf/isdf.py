@@ -219,8 +219,10 @@ class InterpolativeSeparableDensityFitting:
         self._select()
         return self._dev_state["X"].cpu().numpy()
 
-    def _select(self):
+    def _select(self, time_reversal=None):
         d = self.device
+        if time_reversal is None:
+            time_reversal = self.time_reversal
         kmesh = self._kmesh()
         nk = int(np.prod(kmesh))
         nao = self.cell.nao_nr()
@@ -234,7 +236,7 @@ class InterpolativeSeparableDensityFitting:
         npiv = C_int()
         full = C_int()
         # time reversal (real AOs): the Gram over the representatives k <= -k only
-        d.ctx.call("fisdf_set_time_reversal", 1 if self.time_reversal else 0)
+        d.ctx.call("fisdf_set_time_reversal", 1 if time_reversal else 0)
         km_c, km_p = _lib.iarr(kmesh)
         if d.size == 1:
             d.ctx.call("fisdf_select_points_km", _lib.ptr(x0), km_p, ng0, nao, nip_max,
@@ -479,7 +481,7 @@ class InterpolativeSeparableDensityFitting:
 
 ISDF = InterpolativeSeparableDensityFitting
 
-from ctypes import c_int as C_int, c_long as C_long, byref  # noqa: E402
+from ctypes import c_double as C_double, c_int as C_int, c_long as C_long, byref  # noqa: E402
 
 
 class _TorchBuffers:
@@ -496,7 +498,11 @@ class _TorchBuffers:
         d.ctx.call("fisdf_set_allocator", self.alloc_cb, self.free_cb, None)
 
     def _alloc(self, nbytes, user):
-        t = self.d.torch.empty(int(nbytes), dtype=self.d.torch.uint8, device=self.d.dev)
+        # on the context's stream whatever stream is current when build() runs: the caching
+        # allocator hands a freed block out again only to work ordered on the stream it was
+        # allocated on, and fisdf.h's free_fn contract orders the buffer's last use on ctx.stream
+        with self.d.torch.cuda.stream(self.d.stream):
+            t = self.d.torch.empty(int(nbytes), dtype=self.d.torch.uint8, device=self.d.dev)
         self.live[t.data_ptr()] = t
         return t.data_ptr()
 
@@ -566,8 +572,45 @@ def _build_one_gpu(df_obj):
     df_obj.ranks = np.ctypeslib.as_array(r.ranks, (nq,)).copy()
     df_obj.used_pivoted_fit = bool(r.used_pivoted_fit)
     df_obj.min_norm_slots = int(r.min_norm_slots)
+    df_obj.time_reversal_used = bool(r.time_reversal)
+    df_obj.tr_deviation = float(r.tr_deviation)
     df_obj.nip = nip
     return df_obj
+
+
+# relative tolerance of the time-reversal check (fisdf_build's kTrTol): rounding of the lattice
+# phases is ~1e-15; a complex basis or a shifted k-mesh violates the symmetry at O(1)
+TR_TOL = 1e-9
+
+
+def _time_reversal_holds(df_obj, x0, f, kmesh):
+    """x0_{-k} = conj(x0_k) and f_{-k} = conj(f_k) on the device (fisdf_check_time_reversal):
+    what folding the selection Gram, x4 and y over k <= -k and W_{-q} = conj(W_q) rely on.
+    The k-sharded build's counterpart of fisdf_build's own check; every rank
+    holds the same inputs, so every rank reaches the same verdict.  The verdict is kept while the
+    input tensors are unchanged (same storage, torch version counter and shape): a repeated
+    build on resident inputs reads them once."""
+    key = tuple((int(a.data_ptr()), int(a._version), tuple(a.shape)) for a in (x0, f))
+    key += tuple(int(k) for k in kmesh)
+    cached = getattr(df_obj, "_tr_cache", None)
+    if cached is not None and cached[0] == key:
+        df_obj.tr_deviation = cached[2]
+        return cached[1]
+    km_c, km_p = _lib.iarr(kmesh)
+    out = (C_double * 2)()
+    worst = 0.0
+    for a in (x0, f):
+        per_k = int(a.shape[1]) * int(a.shape[2])
+        df_obj.device.ctx.call("fisdf_check_time_reversal", _lib.ptr(a), per_k, per_k, km_p, out)
+        if out[1] > 0:
+            worst = max(worst, out[0] / out[1])
+    df_obj.tr_deviation = worst
+    ok = worst <= TR_TOL
+    df_obj._tr_cache = (key, ok, worst)
+    if not ok:
+        log.warning("AO inputs violate time reversal (max |a[-k] - conj(a[k])| / max |a| = "
+                    "%.3e): every q fitted", worst)
+    return ok
 
 
 def build(df_obj):
@@ -592,20 +635,27 @@ def build(df_obj):
     mesh_c, mesh_p = _lib.iarr(df_obj.mesh)
     ngrid = int(np.prod(df_obj.mesh))
 
+    if df_obj._ao_parent is None:
+        df_obj._ao_parent = df_obj._eval_ao(cell.gen_uniform_grids(df_obj.m0))
+    if df_obj._ao_grid is None:
+        df_obj._ao_grid = df_obj._eval_ao(df_obj.grids_coords())
+    tr = bool(df_obj.time_reversal) and _time_reversal_holds(df_obj, df_obj._ao_parent,
+                                                              df_obj._ao_grid, kmesh)
+    df_obj.time_reversal_used = tr
     if df_obj._dev_state is None or "X" not in df_obj._dev_state:
-        df_obj._select()                                                 # fftisdf.py:33
+        df_obj._select(time_reversal=tr)                                 # fftisdf.py:33
     X = df_obj._dev_state["X"]
     nip = X.shape[1]
 
     # X_{-k} = conj(X_k) for real AOs: x2_k (x4) and fx_k (y) formed for half the k-mesh (:38, :76)
-    d.ctx.call("fisdf_set_time_reversal", 1 if df_obj.time_reversal else 0)
+    d.ctx.call("fisdf_set_time_reversal", 1 if tr else 0)
     x4 = d.empty((nk, nip, nip))
     d.ctx.call("fisdf_build_x4", _lib.ptr(X), nip, nao, km_p, a_p, _lib.ptr(x4))   # :38-48
 
     # q to fit: time-reversal representatives (W_{-q} = conj(W_q)) or every q, shared among the
     # ranks by cost: a self-conjugate q fitted with real arithmetic on its half
     # grid costs about 0.6 of a complex one; longest-first greedy (kshard.assign_q)
-    fit_qs, partner, weight = _fit_qset(df_obj, kmesh)
+    fit_qs, partner, weight = _fit_qset(df_obj, kmesh, tr)
     real_q = np.array([bool(df_obj.real_self_conjugate and partner[q] == q) for q in fit_qs])
     parts = kshard.assign_q(np.where(real_q, 0.6, 1.0), d.size)
     mine = parts[d.rank]
@@ -613,8 +663,6 @@ def build(df_obj):
     my_wt = np.ascontiguousarray(weight[mine], dtype=np.float64)
     nq = len(my_qs)
     qs_c = my_qs.ctypes.data_as(_lib._ip)
-    if df_obj._ao_grid is None:
-        df_obj._ao_grid = df_obj._eval_ao(df_obj.grids_coords())
     f = df_obj._ao_grid
     # x4_q factorisation (replaces zgelsy's QRCP, :108) on the library's side stream,
     # overlapped with the y build enqueued next on the main stream
@@ -727,10 +775,10 @@ def build(df_obj):
     return df_obj
 
 
-def _fit_qset(df_obj, kmesh):
+def _fit_qset(df_obj, kmesh, time_reversal=None):
     """(fit_qs, partner, weight): the q whose W_q is computed, the -q map and the W_s weights."""
     nk = int(np.prod(kmesh))
-    if df_obj.time_reversal:
+    if df_obj.time_reversal if time_reversal is None else time_reversal:
         return kshard.time_reversal_reps(kmesh)
     return (np.arange(nk, dtype=np.int32), np.arange(nk, dtype=np.int32), np.ones(nk))
 

@@ -1,21 +1,27 @@
-"""k-point (q) sharding over the GPUs of a node.
+"""q sharding of the k-point ISDF build over the GPUs of a node.
 
-One process per GPU.  Each rank owns a contiguous q-range: it builds y_q, fits and
-Coulomb-transforms only its own q (fftisdf.py:97-122 are independent per q).  The only
-exchange steps are the ones the algorithm has:
+One process per GPU.  The fitted q (time-reversal representatives) are shared among the ranks
+by cost, longest first (``assign_q``: a self-conjugate q fitted on its half grid costs about 0.6
+of a complex one); a rank's q need not be contiguous.  Each rank factorises, fits and
+Coulomb-transforms only its own q (fftisdf.py:97-122 are independent per q).  The exchange
+steps are the ones the algorithm has:
 
-* W_s = sqrt(nk) Re(sum_q Phi[R,q] W_q) (fftisdf.py:204-207) mixes all q: each rank
-  forms its partial sum and the partials are summed with one all-reduce (RCCL over
-  xGMI on the GPUs; gloo in the CPU tests);
-* get_j uses W_0 (fftisdf.py:159), owned by the rank holding q = 0: one broadcast.
+* the selection (fftisdf.py:357-388) is REPLICATED: every rank forms the whole Gram in the
+  1-GPU order and runs the same pivoted Cholesky, so the pivots are the 1-GPU build's on every
+  rank with no collective (``ISDF.sharded_gram`` keeps the k-sharded Gram + ``allreduce_real_part``,
+  whose summation order can flip tied pivots);
+* the y build is sharded over plane-aligned grid slices (``grid_slices``; y_k = Phi^T (Phi fx_k)^2
+  mixes all k at each grid point, fftisdf.py:79-84): ``exchange_y_chunked`` runs one async
+  all-to-all per local q index, each piece sent from its place in the send buffer and read in
+  place by the fit (fisdf_set_y_slices);
+* W_s = sqrt(nk) Re(sum_q Phi[R,q] W_q) (fftisdf.py:204-207) mixes all q: each rank forms every
+  rank's interpolation-point row block of its partial sum and ``reduce_scatter_rows`` leaves each
+  rank its own rows (get_k contracts only those);
+* get_j uses W_0 (fftisdf.py:159), owned by the rank holding q = 0: ``broadcast_w0``; get_j / get_k
+  end with ``allreduce_sum`` of nset * nk * nao^2 values.
 
-* the y build is sharded over plane-aligned grid slices (y_k = Phi^T (Phi fx_k)^2 mixes
-  all k at each grid point, fftisdf.py:79-84): one all-to-all hands each rank the y_q of
-  its q-shard;
-* the selection Gram (fftisdf.py:376-378) is a sum over q: per-rank partials + all-reduce.
-
-These helpers take torch tensors on any device, so the same code runs the CPU gloo
-tests and the RCCL path.
+These helpers take torch tensors on any device, so the same code runs the CPU gloo tests and the
+RCCL path; ``EmulatedGroup`` runs one rank's share alone on one GPU (bench.py --emulate-ranks).
 """
 from __future__ import annotations
 

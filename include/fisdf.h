@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FISDF_ABI_VERSION 2
+#define FISDF_ABI_VERSION 3
 
 typedef struct fisdf_ctx fisdf_ctx;
 
@@ -81,7 +81,9 @@ typedef struct fisdf_build_opts {
   double fit_tol;          /* relative pivot cut of the x4_q factorisation (1e-14) */
   int pivoted_fit;         /* -1 default (fisdf_set_pivoted_fit), 0, 1 */
   int half_grid;           /* -1 default (fisdf_set_half_grid), 0, 1 */
-  int time_reversal;       /* 1: fit one q of each (q, -q) pair, W_{-q} = conj(W_q) (default) */
+  int time_reversal;       /* 1: fit one q of each (q, -q) pair, W_{-q} = conj(W_q) (default);
+                              the build checks x0_{-k} = conj(x0_k), f_{-k} = conj(f_k) on the device
+                              (relative 1e-9) and fits every q when they do not hold */
   int real_self_conjugate; /* 1: q with 2 k_q in the reciprocal lattice fitted in real arithmetic */
   double omega;            /* Coulomb kernel (fisdf_set_omega); 0 = 1/r */
 } fisdf_build_opts;
@@ -97,7 +99,8 @@ int fisdf_build(fisdf_ctx* ctx, const void* d_x0, int ng0, const void* d_f, int 
                 const fisdf_build_opts* opts, int* h_nip);
 
 /* What the last build left resident.  Pointers stay valid until the next fisdf_build,
- * fisdf_build_release or fisdf_destroy on the context. */
+ * fisdf_build_release or fisdf_destroy on the context.  fisdf_build restores the context's stage
+ * settings (time reversal, fit mode, pivoted fit, half grid, omega, factor priority) on return. */
 typedef struct fisdf_build_result {
   int nk, nip, nao, nfit;     /* k-points, interpolation points, AOs, fitted q */
   int used_pivoted_fit;       /* 1: some x4_q needed the pivoted (rank-revealing) factorisation */
@@ -110,8 +113,16 @@ typedef struct fisdf_build_result {
   const void* d_x4;           /* (nk, nip, nip) c128 */
   const void* d_Wq;           /* (nfit, nip, nip) c128 */
   const void* d_Ws;           /* (nk, nip, nip) float64: W_s = Re(...) (fftisdf.py:207) */
+  int time_reversal;          /* 1: one q of each (q, -q) pair fitted, W_{-q} = conj(W_q); 0: every
+                                 q fitted (asked for, or the inputs failed the check below) */
+  double tr_deviation;        /* max |a[-k] - conj(a[k])| / max |a| over x0 and f (0 unchecked) */
 } fisdf_build_result;
 int fisdf_build_get(fisdf_ctx* ctx, fisdf_build_result* out);
+/* Time-reversal check of Bloch AO values d_a[k][per_k] (k stride k_stride elements, get_kpts
+ * order over kmesh): h_out[0] = max |a[-k] - conj(a[k])| (2 |Im a| on a self-paired k), h_out[1] =
+ * max |a|.  What the fold over k <= -k relies on (fisdf_set_time_reversal).  synchronous. */
+int fisdf_check_time_reversal(fisdf_ctx* ctx, const void* d_a, long k_stride, long per_k,
+                              const int kmesh[3], double* h_out);
 int fisdf_build_release(fisdf_ctx* ctx);
 
 /* Host copies of the reference's attributes (fftisdf.py:125-128): h_x (nk, nip, nao) = _x,

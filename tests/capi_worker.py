@@ -88,6 +88,13 @@ def main(case, out):
     assert "no build" in err2, err2
     assert lib.fisdf_last_error(ctx) == before
     assert lib.fisdf_destroy(ctx2) == 0
+    # a failed fisdf_create reports through fisdf_last_error(NULL) and leaves every live
+    # context's message alone
+    ctx3 = C.c_void_p()
+    assert lib.fisdf_create(1 << 20, None, C.byref(ctx3)) != 0
+    assert b"device id" in lib.fisdf_last_error(None)
+    assert lib.fisdf_last_error(ctx) == before
+    assert r.time_reversal == 1 and r.tr_deviation < 1e-12, (r.time_reversal, r.tr_deviation)
     for p in (d_x0, d_f, d_dms, d_vj, d_vk):
         call("fisdf_free", p)
     call("fisdf_build_release")

@@ -26,6 +26,9 @@ CASES = {
     # exceeds the parent-Gram rank, so nip = rank (fftisdf.py:383) and every x4_q is
     # rank-deficient
     "toy222_rank": (lambda: C.toy_cell(mesh=(12, 12, 12)), (2, 2, 2), (9, 9, 9), 100.0),
+    # a k-mesh with more time-reversal representatives (112) than one kernel argument block
+    # holds (64): the folded selection Gram, x4 and y take their multi-launch / generic paths
+    "toy666": (lambda: C.toy_cell(mesh=(10, 10, 10)), (6, 6, 6), (7, 7, 7), 5.0),
 }
 
 

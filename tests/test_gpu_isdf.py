@@ -34,7 +34,8 @@ def make_df(name, inject=True, time_reversal=True, real_sc=True, pivoted=None, f
 
 
 @pytest.mark.parametrize("name", ["toy222", "toy331", "toy331_fr", "toy333_fr",
-                                  "diamond_szv_gamma", "nio_small", "si_small", "toy222_rank"])
+                                  "diamond_szv_gamma", "nio_small", "si_small", "toy222_rank",
+                                  "toy666"])
 def test_jk_parity_vs_oracle(name):
     df, o, dm = make_df(name)
     df.build()
@@ -43,8 +44,8 @@ def test_jk_parity_vs_oracle(name):
     ej = abs(vj - o["vj"]).max()
     ek = abs(vk - o["vk"]).max()
     full_rank = min(df.ranks) == df.nip
-    print(f"{name}: nip={df.nip} ranks={list(df.ranks)} fit q={list(df.fit_qs)} "
-          f"|dJ|={ej:.2e} |dK|={ek:.2e}")
+    print(f"{name}: nip={df.nip} ranks {min(df.ranks)}-{max(df.ranks)}, {len(df.fit_qs)} q "
+          f"fitted: |dJ|={ej:.2e} |dK|={ek:.2e}")
     assert df.min_norm_slots == sum(int(r < df.nip) for r in df.ranks)
     assert ej < JK_TOL
     assert ek < JK_TOL
@@ -531,3 +532,43 @@ def test_arena_failed_growth_is_recoverable():
                L.ptr(dB), 80, 0, zero.ctypes.data_as(L._dp), L.ptr(dC), 80, 0, 1, 4)  # split-K: arena
     ref = A @ B
     assert (dC.cpu() - ref).abs().max() < 1e-12 * ref.abs().max()
+
+
+def test_time_reversal_guard():
+    """Bloch AO inputs without x_{-k} = conj(x_k) — here a k-dependent phase
+    e^{i theta_k} with theta_{-k} != -theta_k — fail fisdf_build's device check, and the build fits
+    every q (the reference's own path) instead of trusting W_{-q} = conj(W_q).  The oracle runs on
+    the same inputs; the ISDF quantities are gauge invariant, so J/K also equal the untransformed
+    case's."""
+    from fisdf import ISDF
+    from oracle import isdf_ref as R
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs("toy331_fr")
+    o = oracle("toy331_fr")
+    nk = int(np.prod(kmesh))
+    ph = np.exp(1j * 0.37 * (1 + np.arange(nk)))
+    x0g, chig = x0 * ph[:, None, None], chi * ph[:, None, None]
+    perm = o["perm"]
+    out = R.build(x0g[:, perm], chig, coords, cell.a, kmesh, cell.mesh)
+    phase = R.get_phase(cell.a, R.get_kpts(cell.a, kmesh), kmesh)
+    vj0 = R.get_j_kpts(x0g[:, perm], out["w0"], dm)
+    vk0 = R.get_k_kpts(x0g[:, perm], out["wq"], dm, phase)
+    df = ISDF(cell, cell.get_kpts(kmesh), m0=list(m0), c0=c0)
+    d = df.device
+    df._kmesh()
+    df._ao_parent, df._ao_grid = d.to_dev(x0g), d.to_dev(chig)
+    df.set_interpolation_points(perm)
+    df.build()
+    vj, vk = df.get_jk(dm)
+    ej, ek = abs(vj - vj0).max(), abs(vk - vk0).max()
+    print(f"toy331_fr gauge-twisted: time reversal used {df.time_reversal_used}, deviation "
+          f"{df.tr_deviation:.2e}, fitted q {len(df.fit_qs)}/{nk}: |dJ|={ej:.2e} |dK|={ek:.2e}; "
+          f"vs untwisted {abs(vj - o['vj']).max():.2e} / {abs(vk - o['vk']).max():.2e}")
+    assert not df.time_reversal_used and df.tr_deviation > 1e-3
+    assert len(df.fit_qs) == nk
+    assert ej < JK_TOL and ek < JK_TOL
+    assert abs(vj - o["vj"]).max() < JK_TOL and abs(vk - o["vk"]).max() < JK_TOL
+    # the untwisted inputs pass the check and fold (the default path)
+    df2, _, _ = make_df("toy331_fr")
+    df2.build()
+    assert df2.time_reversal_used and df2.tr_deviation < 1e-12, df2.tr_deviation
+    assert len(df2.fit_qs) < nk

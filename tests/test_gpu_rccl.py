@@ -71,6 +71,8 @@ def test_emulated_rank_reproduces_its_q(name, n):
     yall = d.empty((len(qs), nip, ngrid))
     km_c, km_p = _lib.iarr(kmesh)
     a_c, a_p = _lib.darr(cell.a.ravel())
+    # the 1-GPU build's y arithmetic (fisdf_build restores the context's stage settings on return)
+    d.ctx.call("fisdf_set_time_reversal", 1 if df1.time_reversal_used else 0)
     d.ctx.call("fisdf_build_y_qs", _lib.ptr(df1._ao_grid), ngrid * nao, 0, ngrid, ngrid,
                _lib.ptr(X), nip, nao, km_p, a_p, qs.ctypes.data_as(_lib._ip), len(qs),
                _lib.ptr(yall))

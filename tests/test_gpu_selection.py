@@ -54,6 +54,25 @@ def gpu_select(x0, nao, nip_max, tol=-1.0):
     return perm[:min(nip_max, npiv.value)]
 
 
+def gpu_select_km(x0, kmesh, nao, nip_max, tol=-1.0, time_reversal=True):
+    """fisdf_select_points_km: with time reversal the Gram is folded over the representatives
+    k <= -k (fisdf_set_time_reversal)."""
+    import ctypes as C
+    import torch
+    from fisdf import _lib as L
+    ctx = L.Context(0, torch.cuda.current_stream().cuda_stream)
+    ctx.call("fisdf_set_time_reversal", 1 if time_reversal else 0)
+    dx0 = torch.from_numpy(np.ascontiguousarray(x0)).cuda()
+    ng0 = x0.shape[1]
+    perm = np.zeros(nip_max, np.int32)
+    npiv, full = C.c_int(), C.c_int()
+    km = (C.c_int * 3)(*[int(k) for k in kmesh])
+    ctx.call("fisdf_select_points_km", L.ptr(dx0), km, ng0, nao, nip_max, tol,
+             perm.ctypes.data_as(L._ip), C.byref(npiv), C.byref(full))
+    ctx.close()
+    return perm[:min(nip_max, npiv.value)]
+
+
 def _cell_x0(cfg):
     import bench
     from fisdf import cell as C
@@ -97,3 +116,34 @@ def test_selection_vs_dpstrf(cfg):
         assert dres <= tie_tol
     else:
         print(msg)
+
+
+def _tie_certified(x4, perm_g, perm_l, what):
+    nip = len(perm_l)
+    assert len(perm_g) == nip, (what, len(perm_g), nip)
+    same = perm_g == perm_l
+    first = int(np.argmin(same)) if not same.all() else nip
+    print(f"{what}: identical prefix {first}/{nip}")
+    if first == nip:
+        return
+    tie_tol = x4.shape[0] * np.finfo(float).eps * np.diag(x4).max()
+    before, res_g = residual_along(x4, perm_g)
+    _, res_l = residual_along(x4, perm_l)
+    dp = before[first]
+    assert dp.max() - dp[perm_g[first]] <= tie_tol
+    assert abs(res_g.max() - res_l.max()) <= tie_tol
+
+
+@pytest.mark.timeout(300)
+def test_selection_folded_gram_large_kmesh():
+    """a k-mesh with more than 64 time-reversal representatives (6x6x6: 112)
+    goes through the folded selection Gram in several 64-k launches; the pivots are dpstrf's
+    (or tie-certified) with and without the fold."""
+    from oracle import isdf_ref as R
+    from cases import inputs
+    cell, kmesh, m0, c0, x0 = inputs("toy666")[:5]
+    nao = cell.nao_nr()
+    perm_l, rank, nip, x4 = R.select_interpolation_points(x0, nao, c0)
+    for tr in (True, False):
+        perm_g = gpu_select_km(x0, kmesh, nao, int(nao * c0), time_reversal=tr)
+        _tie_certified(x4, perm_g, perm_l, f"toy666 time_reversal={tr}")
