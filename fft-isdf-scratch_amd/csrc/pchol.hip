@@ -14,6 +14,8 @@
 // updates the residual diagonal d, then a per-matrix arg-max picks pivot j+1
 // (first index on ties, as LAPACK's MAXLOC).  Chosen rows are marked d = -1.
 #include <cstdio>
+#include <cstring>
+#include <vector>
 
 #include "common.h"
 
@@ -665,6 +667,455 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
   }
 }
 
+// ---- batched-candidate selection (default where the owned rows fit, C1-C4) -------------------
+// pchol_select_coop needs a grid-wide arg-max and a pivot-row hand-off for EVERY pivot: two
+// dependent cross-XCD round trips, ~6 us per pivot at C3 whatever the exchange's shape
+// (4.0 ms of every k-shard rank).  Here the grid exchanges once per BATCH:
+//  * owners (workgroups 0..G-1, RW <= 16 rows each, their L rows in LDS and in the row-major
+//    global L) post their residual diagonal as tagged 16-byte granules {d, row, batch};
+//  * the leader (workgroup G) reads them all, takes the M largest (value desc, row asc: LAPACK's
+//    first index on ties) as candidates C and the next one as the bound B, forms the candidates'
+//    residual block R = x4[C,C] - L[C,:j] L[C,:j]^T on FP64 MFMA from the global L rows, and runs
+//    the greedy steps on R alone while the chosen diagonal beats B.  No other row can win such a
+//    step: its residual diagonal only decreases (d -= l^2), and at the batch start it was <= B —
+//    so every accepted step is exactly the greedy (dpstrf) pivot of the whole matrix;
+//  * the leader publishes the batch (pivots, their d, the candidates' new L entries and
+//    residuals); each owner forms its rows' new columns with one MFMA pass against the pivot
+//    rows (acc = L[rows,:j] L[piv,:j]^T) plus the in-batch triangular part, and posts again.
+// Simulated on the C3 parent grid (n 3375, 600 pivots): 100 batches at M = 16 (6 pivots each).
+// Hand-offs: sc1 (write-through) stores of every handed-off byte, s_waitcnt vmcnt(0) and a
+// workgroup barrier before the signalling store, sc1 loads on the reading side (the pattern of
+// pchol_select_coop).  Every wait is bounded: a stalled wait sets *err and the grid drains.
+constexpr int SB_THREADS = 512;
+constexpr int SB_M = 16;          // candidates per batch (one 16 x 16 MFMA block)
+constexpr int SB_GR = 8;          // granules per leader thread: n <= 8 * 512
+constexpr int SB_KPW = 40;        // K steps (4 columns) per wave in the MFMA passes: rmax <= 1280
+constexpr long SB_SPIN = 1L << 22;
+
+struct SelPub {      // the leader's batch result (global, written with sc1 stores)
+  u32x4 hdr;         // {s, s, stop, batch}: written last, the owners poll its batch word
+  int pv[SB_M];      // pivots (rows), in order
+  int pidx[SB_M];    // candidate index of each pivot
+  int cand[SB_M];    // candidate rows (-1: none)
+  double dp[SB_M];   // residual diagonal of each pivot when chosen
+  double dnew[SB_M]; // candidates' residual diagonal after the batch (-1e300: chosen)
+  double Lnew[SB_M * SB_M];  // [candidate][k]: the candidates' entries of the batch's columns
+};
+
+__device__ __forceinline__ double sb_dbl(u32x4 g) {
+  return __longlong_as_double((long long)(((unsigned long long)g.y << 32) | g.x));
+}
+__device__ __forceinline__ void sb_st_d(double* a, double v) {
+  __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double sb_ld_d(const double* a) {
+  return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sb_st_i(int* a, int v) {
+  __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int sb_ld_i(const int* a) {
+  return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// spin until *flag's tag word (w) equals `tag`; false on a stall or another workgroup's error
+__device__ __forceinline__ bool sb_wait(const u32x4* flag, unsigned tag, int* err, u32x4* out) {
+  for (long spins = 0;; ++spins) {
+    const u32x4 g = sc_load_rec(flag);
+    if (g.w == tag) { *out = g; return true; }
+    __builtin_amdgcn_s_sleep(1);
+    if (spins > SB_SPIN ||
+        ((spins & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      atomicExch(err, 1);
+      return false;
+    }
+  }
+}
+
+__global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
+    const cplx* __restrict__ X2, double scale, int n, int rmax, double tol, int RW,
+    int* __restrict__ piv, int* __restrict__ rank, u32x4* __restrict__ ddg,
+    SelPub* __restrict__ pub, double* __restrict__ Lg, int* __restrict__ err,
+    unsigned long long* __restrict__ prof) {
+  extern __shared__ double sm[];
+  constexpr int M = SB_M;
+  const int G = gridDim.x - 1, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i16 = lane & 15, kq = lane >> 4;
+  double* red = sm;                 // [8 waves][256] MFMA partials
+  __shared__ int s_i[4 * M + 8];
+  __shared__ double s_d[3 * M + 8];
+  __shared__ int s_bad;
+  if (tid == 0) s_bad = 0;
+  if ((int)blockIdx.x < G) {
+    // ======================= owner: rows [r0, r0 + nr) =======================
+    double* Lr = red + 8 * 256;     // RW x rmax, row-major
+    double* Lnew = Lr + (long)RW * rmax;  // M x M (the publish's candidate entries)
+    double* x4p = Lnew + M * M;     // [row][k] = x4[row, p_k]
+    double* acc = x4p + 16 * M;     // [row][k] = L[row, :j] . L[p_k, :j]
+    int* pv = s_i;                  // published pivots, their candidate index, the candidates
+    int* pidx = s_i + M;
+    int* cand = s_i + 2 * M;
+    int* hdr = s_i + 3 * M;         // s, stop
+    double* dpv = s_d;
+    double* dnew = s_d + M;
+    const int r0 = blockIdx.x * RW, nr = max(0, min(RW, n - r0));
+    double dd = -1e300;             // thread r < nr: residual diagonal of row r0 + r
+    if (tid < nr) {
+      const double x = X2[(long)(r0 + tid) * n + r0 + tid].x;
+      dd = x * x * scale;
+    }
+    int j = 0;
+    for (unsigned b = 1;; ++b) {
+      if (tid < nr) {  // post (after the previous batch's stores completed: barrier below)
+        const unsigned long long vb = (unsigned long long)__double_as_longlong(dd);
+        u32x4 g;
+        g.x = (unsigned)vb;
+        g.y = (unsigned)(vb >> 32);
+        g.z = (unsigned)(r0 + tid);
+        g.w = b;
+        sc_store_rec(ddg + r0 + tid, g);
+      }
+      if (tid == 0) {
+        u32x4 h;
+        if (sb_wait(&pub->hdr, b, err, &h)) {
+          hdr[0] = (int)h.y;
+          hdr[1] = (int)h.z;
+        } else {
+          s_bad = 1;
+        }
+      }
+      __syncthreads();
+      if (s_bad) return;
+      const int s = hdr[0], stop = hdr[1];
+      if (tid < M) {
+        pv[tid] = sb_ld_i(&pub->pv[tid]);
+        pidx[tid] = sb_ld_i(&pub->pidx[tid]);
+        cand[tid] = sb_ld_i(&pub->cand[tid]);
+        dpv[tid] = sb_ld_d(&pub->dp[tid]);
+        dnew[tid] = sb_ld_d(&pub->dnew[tid]);
+      }
+      for (int e = tid; e < M * M; e += SB_THREADS) Lnew[e] = sb_ld_d(&pub->Lnew[e]);
+      __syncthreads();
+      if (s > 0) {
+        // x4[row, p_k] (row p_k of x4 is contiguous over this workgroup's rows)
+        if (tid < 16 * M) {
+          const int r = tid & 15, k = tid >> 4;
+          double v = 0.0;
+          if (r < nr && k < s) {
+            const double x = X2[(long)pv[k] * n + r0 + r].x;
+            v = x * x * scale;
+          }
+          x4p[r * M + k] = v;
+        }
+        // acc[r][k] = sum_{l < j} L[r0 + r, l] L[p_k, l]: FP64 MFMA, A = the owned rows (LDS),
+        // B = the pivot rows (global L), K split over the 8 waves, every B load issued up front
+        f64x4 D = {0, 0, 0, 0};
+        const int nks = (j + 3) >> 2;
+        const double* lgp = Lg + (long)pv[min(i16, s - 1)] * rmax;
+        const bool bok = i16 < s, aok = i16 < nr;
+        double bv[SB_KPW];
+#pragma unroll
+        for (int u = 0; u < SB_KPW; ++u) {
+          const int l = (w + 8 * u) * 4 + kq;
+          bv[u] = 0.0;
+          if (w + 8 * u < nks) {
+            const double t = sb_ld_d(lgp + min(l, max(j - 1, 0)));
+            bv[u] = (bok && l < j) ? t : 0.0;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < SB_KPW; ++u) {
+          if (w + 8 * u >= nks) break;
+          const int l = (w + 8 * u) * 4 + kq;
+          const double a = (aok && l < j) ? Lr[(long)i16 * rmax + l] : 0.0;
+          D = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv[u], D, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[w * 256 + (kq + 4 * r) * 16 + i16] = D[r];
+        __syncthreads();
+        if (tid < 256) {
+          double t = 0.0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) t += red[q * 256 + tid];
+          acc[(tid >> 4) * M + (tid & 15)] = t;
+        }
+        __syncthreads();
+        // the batch's columns of each owned row, in order (one thread per row)
+        if (tid < nr) {
+          const int row = r0 + tid;
+          int ci = -1;
+#pragma unroll
+          for (int c = 0; c < M; ++c)
+            if (cand[c] == row) ci = c;
+          double* lr = Lr + (long)tid * rmax + j;
+          double* lg = Lg + (long)row * rmax + j;
+          if (ci >= 0) {  // a candidate: the leader's entries and residual (a pivot: -1e300)
+            for (int k = 0; k < s; ++k) {
+              const double l = Lnew[ci * M + k];
+              lr[k] = l;
+              sb_st_d(lg + k, l);
+            }
+            dd = dnew[ci];
+          } else {
+            for (int k = 0; k < s; ++k) {
+              double l = 0.0;
+              if (dd > -1e299) {
+                const double* lp = Lnew + pidx[k] * M;  // L[p_k, j + k'] for k' < k
+                double v = x4p[tid * M + k] - acc[tid * M + k];
+                for (int k2 = 0; k2 < k; ++k2) v -= lr[k2] * lp[k2];
+                l = v / sqrt(dpv[k]);
+                dd -= l * l;
+              }
+              lr[k] = l;
+              sb_st_d(lg + k, l);
+            }
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+      __syncthreads();  // every store of this batch complete before the next post
+      j += s;
+      if (stop) return;
+    }
+  }
+  // ======================= leader =======================
+  double* R = red + 8 * 256;        // M x M candidates' residual block
+  double* lv = R + M * M;           // per-wave top-(M+1) lists: value
+  int* li = (int*)(lv + 8 * (M + 1));  // row
+  double* Ldn = (double*)(li + 8 * (M + 1) + 2);  // [c][k] entries of the batch's columns
+  int* cand = s_i;                  // candidates (rows; -1 none)
+  int* pv = s_i + M;
+  int* pidx = s_i + 2 * M;
+  int* st = s_i + 3 * M;            // s, stop, rank, Brow
+  double* cd = s_d;                 // candidates' residual diagonal (batch start)
+  double* dpv = s_d + M;
+  double* misc = s_d + 2 * M;       // thr, Bv
+  int j = 0;
+  for (unsigned b = 1;; ++b) {
+    const bool pr = prof != nullptr && tid == 0 && b <= 8192;
+    // ---- gather every row's residual diagonal ----
+    double v[SB_GR];
+    int rw[SB_GR];
+    bool bad = false;
+#pragma unroll
+    for (int u = 0; u < SB_GR; ++u) {
+      const int row = tid + SB_THREADS * u;
+      v[u] = -1e300;
+      rw[u] = 0x7fffffff;
+      if (row < n && !bad) {
+        u32x4 g;
+        if (sb_wait(ddg + row, b, err, &g)) {
+          v[u] = sb_dbl(g);
+          rw[u] = row;
+        } else {
+          bad = true;
+        }
+      }
+    }
+    if (bad) s_bad = 1;
+    __syncthreads();
+    if (s_bad) return;
+    if (pr) prof[4L * (b - 1)] = __builtin_amdgcn_s_memrealtime();
+    // ---- top-(M+1) by (value desc, row asc): per wave by repeated extraction, then merged ----
+    for (int rd = 0; rd <= M; ++rd) {
+      double bv = -1e300;
+      int bi = 0x7fffffff, bu = -1;
+#pragma unroll
+      for (int u = 0; u < SB_GR; ++u)
+        if (sc_better(v[u], rw[u], bv, bi)) { bv = v[u]; bi = rw[u]; bu = u; }
+      double mv = bv;
+      int mi = bi;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double v2 = __shfl_xor(mv, o, 64);
+        const int i2 = __shfl_xor(mi, o, 64);
+        if (sc_better(v2, i2, mv, mi)) { mv = v2; mi = i2; }
+      }
+      if (bi == mi && bu >= 0 && mi != 0x7fffffff) {
+#pragma unroll
+        for (int u = 0; u < SB_GR; ++u)
+          if (u == bu) { v[u] = -1e300; rw[u] = 0x7fffffff; }
+      }
+      if (lane == 0) { lv[w * (M + 1) + rd] = mv; li[w * (M + 1) + rd] = mi; }
+    }
+    __syncthreads();
+    if (w == 0) {
+      double mv2[3];
+      int mi2[3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int e = lane + 64 * u;
+        mv2[u] = e < 8 * (M + 1) ? lv[e] : -1e300;
+        mi2[u] = e < 8 * (M + 1) ? li[e] : 0x7fffffff;
+      }
+      for (int rd = 0; rd <= M; ++rd) {
+        double bv = -1e300;
+        int bi = 0x7fffffff, bu = -1;
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+          if (sc_better(mv2[u], mi2[u], bv, bi)) { bv = mv2[u]; bi = mi2[u]; bu = u; }
+        double mv = bv;
+        int mi = bi;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const double v2 = __shfl_xor(mv, o, 64);
+          const int i2 = __shfl_xor(mi, o, 64);
+          if (sc_better(v2, i2, mv, mi)) { mv = v2; mi = i2; }
+        }
+        if (bi == mi && bu >= 0 && mi != 0x7fffffff) {
+#pragma unroll
+          for (int u = 0; u < 3; ++u)
+            if (u == bu) { mv2[u] = -1e300; mi2[u] = 0x7fffffff; }
+        }
+        if (lane == 0) {
+          const bool valid = mi != 0x7fffffff && mv > -1e299;
+          if (rd < M) {
+            cand[rd] = valid ? mi : -1;
+            cd[rd] = valid ? mv : -1e300;
+          } else {
+            misc[1] = valid ? mv : -1e300;   // the bound B (largest non-candidate)
+            st[3] = valid ? mi : 0x7fffffff;
+          }
+        }
+      }
+      if (lane == 0 && b == 1)
+        misc[0] = tol > 0 ? tol * cd[0] : (double)n * 2.220446049250313e-16 * cd[0];
+    }
+    __syncthreads();
+    if (pr) prof[4L * (b - 1) + 1] = __builtin_amdgcn_s_memrealtime();
+    // ---- R = x4[C,C] - L[C,:j] L[C,:j]^T (FP64 MFMA, K over the 8 waves; A = B^T) ----
+    {
+      f64x4 D = {0, 0, 0, 0};
+      const int nks = (j + 3) >> 2;
+      const int ci = cand[i16];
+      const double* lgc = Lg + (long)max(ci, 0) * rmax;
+      double av[SB_KPW];
+#pragma unroll
+      for (int u = 0; u < SB_KPW; ++u) {
+        const int l = (w + 8 * u) * 4 + kq;
+        av[u] = 0.0;
+        if (w + 8 * u < nks) {
+          const double t = sb_ld_d(lgc + min(l, max(j - 1, 0)));
+          av[u] = (ci >= 0 && l < j) ? t : 0.0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < SB_KPW; ++u) {
+        if (w + 8 * u >= nks) break;
+        D = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], av[u], D, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[w * 256 + (kq + 4 * r) * 16 + i16] = D[r];
+      __syncthreads();
+      if (tid < 256) {
+        const int a = tid >> 4, c = tid & 15;
+        double t = 0.0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) t += red[q * 256 + tid];
+        double x = 0.0;
+        if (cand[a] >= 0 && cand[c] >= 0) {
+          const double y = X2[(long)cand[a] * n + cand[c]].x;
+          x = y * y * scale;
+        }
+        R[a * M + c] = x - t;
+      }
+      __syncthreads();
+    }
+    if (pr) prof[4L * (b - 1) + 2] = __builtin_amdgcn_s_memrealtime();
+    // ---- the greedy steps on the candidates (wave 0; lane c < M holds candidate c) ----
+    if (w == 0) {
+      const double thr = misc[0], Bv = misc[1];
+      const int Brow = st[3];
+      const int myrow = lane < M ? cand[lane] : -1;
+      double d = lane < M ? cd[lane] : -1e300;
+      bool chosen = myrow < 0;
+      int k = 0, stop = 0, rk = 0;
+      for (;;) {
+        if (j + k >= rmax) { stop = 1; rk = rmax; break; }
+        double mv = (lane < M && !chosen) ? d : -1e300;
+        int mi = (lane < M && !chosen) ? myrow : 0x7fffffff;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {
+          const double v2 = __shfl_xor(mv, o, 64);
+          const int i2 = __shfl_xor(mi, o, 64);
+          if (sc_better(v2, i2, mv, mi)) { mv = v2; mi = i2; }
+        }
+        mv = __shfl(mv, 0, 64);
+        mi = __shfl(mi, 0, 64);
+        if (mi == 0x7fffffff) {  // every candidate chosen
+          if (Brow == 0x7fffffff) { stop = 1; rk = j + k; }  // ... and no other row left
+          break;
+        }
+        if (!sc_better(mv, mi, Bv, Brow)) break;  // a non-candidate could win the next step
+        if (!(mv > thr)) { stop = 1; rk = j + k; break; }  // the global max is below dpstrf's tol
+        const int pc = __builtin_amdgcn_readfirstlane(__ffsll((long long)__ballot(lane < M && myrow == mi)) - 1);
+        const double sq = sqrt(mv), inv = 1.0 / sq;
+        double l = 0.0;
+        if (lane < M) {
+          l = lane == pc ? sq : (chosen ? 0.0 : R[lane * M + pc] * inv);
+          Ldn[lane * M + k] = l;
+        }
+        if (lane == 0) {
+          pv[k] = mi;
+          pidx[k] = pc;
+          dpv[k] = mv;
+          piv[j + k] = mi;
+        }
+        // rank-1 update of the candidates' residual block (row `lane`; all lanes shuffle)
+        double lc[M];
+#pragma unroll
+        for (int c = 0; c < M; ++c) lc[c] = __shfl(l, c, 64);
+        if (lane < M && !chosen && lane != pc) {
+          d -= l * l;
+#pragma unroll
+          for (int c = 0; c < M; ++c) R[lane * M + c] -= l * lc[c];
+        }
+        if (lane == pc) {
+          chosen = true;
+          d = -1e300;
+        }
+        ++k;
+      }
+      if (k == 0 && !stop) {  // cannot happen (the top candidate beats B); never spin on it
+        stop = 1;
+        rk = j;
+        if (lane == 0) atomicExch(err, 1);
+      }
+      if (lane < M) misc[2 + lane] = d;
+      if (lane == 0) {
+        st[0] = k;
+        st[1] = stop;
+        st[2] = rk;
+        if (stop) rank[0] = rk;
+      }
+    }
+    __syncthreads();
+    // ---- publish ----
+    const int s = st[0], stop = st[1];
+    if (tid < M) {
+      sb_st_i(&pub->pv[tid], tid < s ? pv[tid] : 0);
+      sb_st_i(&pub->pidx[tid], tid < s ? pidx[tid] : 0);
+      sb_st_i(&pub->cand[tid], cand[tid]);
+      sb_st_d(&pub->dp[tid], tid < s ? dpv[tid] : 1.0);
+      sb_st_d(&pub->dnew[tid], misc[2 + tid]);
+    }
+    for (int e = tid; e < M * M; e += SB_THREADS) sb_st_d(&pub->Lnew[e], (e % M) < s ? Ldn[e] : 0.0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      u32x4 h;
+      h.x = (unsigned)s;
+      h.y = (unsigned)s;
+      h.z = (unsigned)stop;
+      h.w = b;
+      sc_store_rec(&pub->hdr, h);
+    }
+    if (pr) prof[4L * (b - 1) + 3] = __builtin_amdgcn_s_memrealtime();
+    j += s;
+    if (stop) return;
+    __syncthreads();  // the shared lists are rewritten by the next batch
+  }
+}
+
 __global__ void real_square_scale_kernel(const cplx* __restrict__ in, double s,
                                          double* __restrict__ out, double* __restrict__ d,
                                          long n2, int n) {
@@ -1005,13 +1456,122 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
   return 0;
 }
 
+// FISDF_SEL_MODE (read per call: the GPU tests compare the paths): "batch" (default) tries the
+// batched-candidate kernel, then the cooperative one; "coop" starts at the cooperative kernel;
+// "blocked" (or FISDF_SEL_COOP=0) runs the blocked single-CU path only
+int select_mode() {
+  const char* e = getenv("FISDF_SEL_MODE");
+  if (!select_coop_enabled()) return 2;
+  if (!e) return 0;
+  if (!strcmp(e, "coop")) return 1;
+  if (!strcmp(e, "blocked")) return 2;
+  return 0;
+}
+
+// launches pchol_select_batch when the owned rows fit (n <= 4096, 16 rows per workgroup on at
+// most ncu - 1 workgroups, rmax <= 1024); *handled = false otherwise or if the launch is refused.
+int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n, int rmax,
+                              double tol, int* piv, int* rank, double* work, bool* handled,
+                              const int** err_dev) {
+  *handled = false;
+  *err_dev = nullptr;
+  if (n < 2 * SB_M || n > SB_GR * SB_THREADS || rmax > 4 * 8 * SB_KPW) return 0;
+  static const int ncu = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return v;
+  }();
+  const int RW = 16;
+  const int G = (n + RW - 1) / RW;
+  if (G + 1 > ncu) return 0;
+  constexpr size_t kLds = 150 * 1024;
+  const size_t owner = sizeof(double) * (8 * 256 + 3 * 256 + (size_t)RW * rmax);
+  const size_t leader = sizeof(double) * (8 * 256 + 2 * 256 + 8 * (SB_M + 1) + 128);
+  const size_t lds = std::max(owner, leader);
+  if (lds > kLds) return 0;
+  // scratch in the caller's work area (n*n doubles): granules, publish area, global L, error flag
+  u32x4* ddg = (u32x4*)work;
+  const long pub_d = (long)((sizeof(SelPub) + 15) / 16) * 2;
+  SelPub* pub = (SelPub*)(work + 2L * n);
+  double* Lg = work + 2L * n + pub_d;
+  int* err = (int*)(Lg + (long)n * rmax);
+  if (2L * n + pub_d + (long)n * rmax + 2 > (long)n * n) return 0;
+  FISDF_HIP(hipMemsetAsync(ddg, 0, sizeof(u32x4) * n, s));
+  FISDF_HIP(hipMemsetAsync(pub, 0, sizeof(u32x4), s));
+  FISDF_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
+  FISDF_HIP(hipMemsetAsync(rank, 0, sizeof(int), s));
+  static bool attr = false;
+  if (!attr) {
+    FISDF_HIP(hipFuncSetAttribute((const void*)pchol_select_batch,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
+    attr = true;
+  }
+  // FISDF_SEL_PROF=1: per-batch phase timestamps of the leader (timing probe), printed below
+  constexpr int kProfBatches = 8192;
+  static unsigned long long* prof[64] = {};
+  int pdev = 0;
+  FISDF_HIP(hipGetDevice(&pdev));
+  const bool want_prof = getenv("FISDF_SEL_PROF") != nullptr && pdev < 64;
+  if (want_prof && !prof[pdev])
+    FISDF_HIP(hipMalloc(&prof[pdev], sizeof(unsigned long long) * 4 * kProfBatches));
+  unsigned long long* profp = want_prof ? prof[pdev] : nullptr;
+  const int nb_cap = std::min(rmax, kProfBatches);
+  if (profp) FISDF_HIP(hipMemsetAsync(profp, 0, sizeof(unsigned long long) * 4 * nb_cap, s));
+  int rw = RW;
+  void* args[] = {(void*)&X2,  (void*)&scale, (void*)&n,   (void*)&rmax, (void*)&tol,
+                  (void*)&rw,  (void*)&piv,   (void*)&rank, (void*)&ddg, (void*)&pub,
+                  (void*)&Lg,  (void*)&err,   (void*)&profp};
+  const hipError_t e = hipLaunchCooperativeKernel((const void*)pchol_select_batch, dim3(G + 1),
+                                                  dim3(SB_THREADS), args, (unsigned)lds, s);
+  if (e != hipSuccess) {  // refused (e.g. not co-resident): the caller's next path runs
+    (void)hipGetLastError();
+    return 0;
+  }
+  *err_dev = err;
+  *handled = true;
+  if (profp) {
+    std::vector<unsigned long long> h(4 * (size_t)nb_cap);
+    FISDF_HIP(hipMemcpyAsync(h.data(), profp, sizeof(unsigned long long) * h.size(),
+                             hipMemcpyDeviceToHost, s));
+    FISDF_HIP(hipStreamSynchronize(s));
+    double ph[4] = {0, 0, 0, 0};
+    int cnt = 0, nb = 0;
+    for (int b = 0; b < nb_cap; ++b) {
+      const unsigned long long* a = &h[4 * (size_t)b];
+      if (!a[0]) break;
+      ++nb;
+      if (b == 0 || !a[1] || !a[2] || !a[3]) continue;
+      const unsigned long long prev = h[4 * (size_t)(b - 1) + 3];
+      ph[0] += (double)(a[0] - prev);  // published -> every row's residual gathered
+      ph[1] += (double)(a[1] - a[0]);  // candidate selection
+      ph[2] += (double)(a[2] - a[1]);  // candidates' residual block (MFMA Gram)
+      ph[3] += (double)(a[3] - a[2]);  // greedy steps + publish
+      ++cnt;
+    }
+    if (cnt)  // s_memrealtime: 100 MHz
+      fprintf(stderr, "select batch G=%d RW=%d: %d batches, per batch (us) owners+gather %.2f, "
+                      "select %.2f, gram %.2f, steps+publish %.2f\n",
+              G, RW, nb, ph[0] / cnt / 100.0, ph[1] / cnt / 100.0, ph[2] / cnt / 100.0,
+              ph[3] / cnt / 100.0);
+  }
+  return 0;
+}
+
 int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rmax, double tol,
                       int* piv, int* rank, double* work, int* flags, bool* handled,
                       bool allow_coop, const int** coop_err) {
   *handled = false;
   *coop_err = nullptr;
   if (rmax <= 0) return 0;
-  if (allow_coop) {
+  const int mode = select_mode();
+  if (allow_coop && mode == 0) {
+    FISDF_TRY(pchol_select_batch_launch(s, X2, scale, n, rmax, tol, piv, rank, work, handled,
+                                        coop_err));
+    if (*handled) return 0;
+  }
+  if (allow_coop && mode <= 1) {
     FISDF_TRY(pchol_select_coop_launch(s, X2, scale, n, rmax, tol, piv, rank, work, handled,
                                        coop_err));
     if (*handled) return 0;

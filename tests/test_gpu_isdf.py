@@ -277,15 +277,19 @@ def test_x4_and_y_parity(name):
 
 @pytest.mark.parametrize("name", ["toy222", "diamond_szv_gamma", "si_small"])
 def test_selection_paths_agree(name, monkeypatch):
-    """The cooperative left-looking selection (default), its split form with only the first
-    K columns of the owned L rows in LDS (forced here with FISDF_SEL_LDS_COLS; the default when
-    the rows do not fit, as in C5) and the blocked right-looking one (FISDF_SEL_COOP=0) pick
-    the same pivots as dpstrf on these cases."""
+    """The batched-candidate selection (default), the cooperative left-looking one
+    (FISDF_SEL_MODE=coop), its split form with only the first K columns of the owned L rows in
+    LDS (forced here with FISDF_SEL_LDS_COLS; the default when the rows do not fit, as in C5) and
+    the blocked right-looking one (FISDF_SEL_COOP=0) pick the same pivots as dpstrf on these
+    cases."""
     perms = {}
-    for mode, env in (("coop", {"FISDF_SEL_COOP": "1"}),
-                      ("split", {"FISDF_SEL_COOP": "1", "FISDF_SEL_LDS_COLS": "20"}),
+    for mode, env in (("batch", {"FISDF_SEL_COOP": "1", "FISDF_SEL_MODE": "batch"}),
+                      ("coop", {"FISDF_SEL_COOP": "1", "FISDF_SEL_MODE": "coop"}),
+                      ("split", {"FISDF_SEL_COOP": "1", "FISDF_SEL_MODE": "coop",
+                                 "FISDF_SEL_LDS_COLS": "20"}),
                       ("blocked", {"FISDF_SEL_COOP": "0"})):
         monkeypatch.delenv("FISDF_SEL_LDS_COLS", raising=False)
+        monkeypatch.delenv("FISDF_SEL_MODE", raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         df, o, dm = make_df(name, inject=False)

@@ -1,5 +1,5 @@
-"""The C3 selection alone (fisdf_select_points: real-part Gram + cooperative pivoted Cholesky +
-one pinned read-back), ms per call and per pivot.
+"""The C3 selection alone (fisdf_select_points: real-part Gram + pivoted Cholesky + one pinned
+read-back), ms per call and per pivot; FISDF_SEL_MODE picks the kernel (batch / coop / blocked).
   python tools/select_bench.py [--cfg c3] [--reps 10]"""
 import argparse
 import os
@@ -18,6 +18,7 @@ import bench  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--cfg", default="c3")
 ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--save", default=None, help="write the pivots (npz) to compare selection modes")
 a = ap.parse_args()
 kind, basis, mesh, kmesh, m0, nip = bench.CONFIGS[a.cfg]
 cell = {"diamond": C.diamond_cell, "nio": C.nio_cell, "si": C.si_supercell}[kind](basis=basis, mesh=mesh)
@@ -42,6 +43,8 @@ t = time.perf_counter()
 for _ in range(a.reps):
     run()
 ms = (time.perf_counter() - t) / a.reps * 1e3
-print(f"select {a.cfg} ng0 {ng0} nip {nip}: {ms:.3f} ms per call, {npiv.value} pivots "
-      f"({ms / max(npiv.value, 1) * 1e3:.2f} us per pivot incl. Gram) exp={os.environ.get('FISDF_SEL_EXP', '0')}",
-      flush=True)
+print(f"select {a.cfg} ng0 {ng0} nip {nip} mode {os.environ.get('FISDF_SEL_MODE', 'batch')}: "
+      f"{ms:.3f} ms per call, {npiv.value} pivots "
+      f"({ms / max(npiv.value, 1) * 1e3:.2f} us per pivot incl. Gram)", flush=True)
+if a.save:
+    np.savez(a.save, perm=perm[:min(nip, npiv.value)].copy())
