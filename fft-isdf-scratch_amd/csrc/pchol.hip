@@ -690,20 +690,28 @@ constexpr int SB_THREADS = 512;
 constexpr int SB_M = 16;          // candidates per batch (one 16 x 16 MFMA block)
 constexpr int SB_GR = 8;          // granules per leader thread: n <= 8 * 512
 constexpr int SB_KPW = 40;        // K steps (4 columns) per wave in the MFMA passes: rmax <= 1280
+constexpr int SB_NPUB = 1 + 2 * SB_M + SB_M * SB_M;  // granules of one publish
+constexpr int SB_LIST = 8 * (SB_M + 1) + 24;          // the leader's candidate list capacity
 constexpr long SB_SPIN = 1L << 22;
 
-struct SelPub {      // the leader's batch result (global, written with sc1 stores)
-  u32x4 hdr;         // {s, s, stop, batch}: written last, the owners poll its batch word
-  int pv[SB_M];      // pivots (rows), in order
-  int pidx[SB_M];    // candidate index of each pivot
-  int cand[SB_M];    // candidate rows (-1: none)
-  double dp[SB_M];   // residual diagonal of each pivot when chosen
-  double dnew[SB_M]; // candidates' residual diagonal after the batch (-1e300: chosen)
-  double Lnew[SB_M * SB_M];  // [candidate][k]: the candidates' entries of the batch's columns
-};
-
+// The leader's publish: SB_NPUB 16-byte granules {payload lo, payload hi, aux, batch}, each
+// written whole by one sc1 store (untorn), so a reader checks every granule's batch word and
+// re-reads a stale one — no flag-after-payload ordering is needed:
+//   [0]            {s, stop, rank, b}
+//   [1 + c]        {dnew_c (the candidate's residual after the batch, -1e300 once chosen), row_c}
+//   [1 + M + k]    {d of pivot k when chosen, candidate index of pivot k}
+//   [1 + 2M + e]   {Lnew[e] = L[cand e / M, j + e % M] (the batch's columns), e}
 __device__ __forceinline__ double sb_dbl(u32x4 g) {
   return __longlong_as_double((long long)(((unsigned long long)g.y << 32) | g.x));
+}
+__device__ __forceinline__ u32x4 sb_gran(double v, unsigned aux, unsigned tag) {
+  const unsigned long long vb = (unsigned long long)__double_as_longlong(v);
+  u32x4 g;
+  g.x = (unsigned)vb;
+  g.y = (unsigned)(vb >> 32);
+  g.z = aux;
+  g.w = tag;
+  return g;
 }
 __device__ __forceinline__ void sb_st_d(double* a, double v) {
   __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -711,39 +719,39 @@ __device__ __forceinline__ void sb_st_d(double* a, double v) {
 __device__ __forceinline__ double sb_ld_d(const double* a) {
   return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void sb_st_i(int* a, int v) {
-  __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int sb_ld_i(const int* a) {
-  return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// spin until *flag's tag word (w) equals `tag`; false on a stall or another workgroup's error
-__device__ __forceinline__ bool sb_wait(const u32x4* flag, unsigned tag, int* err, u32x4* out) {
-  for (long spins = 0;; ++spins) {
-    const u32x4 g = sc_load_rec(flag);
-    if (g.w == tag) { *out = g; return true; }
+// re-read a granule until its batch word is `tag`; false on a stall or another workgroup's error
+__device__ __forceinline__ bool sb_repoll(const u32x4* gp, unsigned tag, int* err, u32x4* g) {
+  for (long spins = 0; g->w != tag; ++spins) {
     __builtin_amdgcn_s_sleep(1);
     if (spins > SB_SPIN ||
         ((spins & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
       atomicExch(err, 1);
       return false;
     }
+    *g = sc_load_rec(gp);
   }
+  return true;
+}
+__device__ __forceinline__ double sb_readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
 __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
     const cplx* __restrict__ X2, double scale, int n, int rmax, double tol, int RW,
     int* __restrict__ piv, int* __restrict__ rank, u32x4* __restrict__ ddg,
-    SelPub* __restrict__ pub, double* __restrict__ Lg, int* __restrict__ err,
+    u32x4* __restrict__ pub, double* __restrict__ Lg, int* __restrict__ err,
     unsigned long long* __restrict__ prof) {
   extern __shared__ double sm[];
   constexpr int M = SB_M;
   const int G = gridDim.x - 1, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i16 = lane & 15, kq = lane >> 4;
   double* red = sm;                 // [8 waves][256] MFMA partials
-  __shared__ int s_i[4 * M + 8];
+  __shared__ int s_i[3 * M + 8];
   __shared__ double s_d[3 * M + 8];
-  __shared__ int s_bad;
+  __shared__ int s_bad, s_cnt;
   if (tid == 0) s_bad = 0;
   if ((int)blockIdx.x < G) {
     // ======================= owner: rows [r0, r0 + nr) =======================
@@ -751,10 +759,9 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
     double* Lnew = Lr + (long)RW * rmax;  // M x M (the publish's candidate entries)
     double* x4p = Lnew + M * M;     // [row][k] = x4[row, p_k]
     double* acc = x4p + 16 * M;     // [row][k] = L[row, :j] . L[p_k, :j]
-    int* pv = s_i;                  // published pivots, their candidate index, the candidates
-    int* pidx = s_i + M;
-    int* cand = s_i + 2 * M;
-    int* hdr = s_i + 3 * M;         // s, stop
+    int* pidx = s_i;                // candidate index of pivot k
+    int* cand = s_i + M;            // candidates (rows, -1 none)
+    int* hdr = s_i + 2 * M;         // s, stop
     double* dpv = s_d;
     double* dnew = s_d + M;
     const int r0 = blockIdx.x * RW, nr = max(0, min(RW, n - r0));
@@ -765,20 +772,12 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
     }
     int j = 0;
     for (unsigned b = 1;; ++b) {
-      if (tid < nr) {  // post (after the previous batch's stores completed: barrier below)
-        const unsigned long long vb = (unsigned long long)__double_as_longlong(dd);
-        u32x4 g;
-        g.x = (unsigned)vb;
-        g.y = (unsigned)(vb >> 32);
-        g.z = (unsigned)(r0 + tid);
-        g.w = b;
-        sc_store_rec(ddg + r0 + tid, g);
-      }
-      if (tid == 0) {
-        u32x4 h;
-        if (sb_wait(&pub->hdr, b, err, &h)) {
-          hdr[0] = (int)h.y;
-          hdr[1] = (int)h.z;
+      if (tid < nr) sc_store_rec(ddg + r0 + tid, sb_gran(dd, (unsigned)(r0 + tid), b));  // post
+      if (tid == 0) {  // the batch's header, then every payload granule (re-read if stale)
+        u32x4 h = sc_load_rec(pub);
+        if (sb_repoll(pub, b, err, &h)) {
+          hdr[0] = (int)h.x;
+          hdr[1] = (int)h.y;
         } else {
           s_bad = 1;
         }
@@ -786,31 +785,28 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
       __syncthreads();
       if (s_bad) return;
       const int s = hdr[0], stop = hdr[1];
-      if (tid < M) {
-        pv[tid] = sb_ld_i(&pub->pv[tid]);
-        pidx[tid] = sb_ld_i(&pub->pidx[tid]);
-        cand[tid] = sb_ld_i(&pub->cand[tid]);
-        dpv[tid] = sb_ld_d(&pub->dp[tid]);
-        dnew[tid] = sb_ld_d(&pub->dnew[tid]);
-      }
-      for (int e = tid; e < M * M; e += SB_THREADS) Lnew[e] = sb_ld_d(&pub->Lnew[e]);
-      __syncthreads();
-      if (s > 0) {
-        // x4[row, p_k] (row p_k of x4 is contiguous over this workgroup's rows)
-        if (tid < 16 * M) {
-          const int r = tid & 15, k = tid >> 4;
-          double v = 0.0;
-          if (r < nr && k < s) {
-            const double x = X2[(long)pv[k] * n + r0 + r].x;
-            v = x * x * scale;
-          }
-          x4p[r * M + k] = v;
+      if (tid >= 1 && tid < SB_NPUB) {
+        u32x4 g = sc_load_rec(pub + tid);
+        if (!sb_repoll(pub + tid, b, err, &g)) s_bad = 1;
+        const double v = sb_dbl(g);
+        if (tid < 1 + M) {
+          cand[tid - 1] = (int)g.z;
+          dnew[tid - 1] = v;
+        } else if (tid < 1 + 2 * M) {
+          pidx[tid - 1 - M] = (int)g.z;
+          dpv[tid - 1 - M] = v;
+        } else {
+          Lnew[tid - 1 - 2 * M] = v;
         }
+      }
+      __syncthreads();
+      if (s_bad) return;
+      if (s > 0) {
         // acc[r][k] = sum_{l < j} L[r0 + r, l] L[p_k, l]: FP64 MFMA, A = the owned rows (LDS),
-        // B = the pivot rows (global L), K split over the 8 waves, every B load issued up front
-        f64x4 D = {0, 0, 0, 0};
+        // B = the pivot rows (global L), K split over the 8 waves; every load issued up front
         const int nks = (j + 3) >> 2;
-        const double* lgp = Lg + (long)pv[min(i16, s - 1)] * rmax;
+        const int pcol = cand[pidx[min(i16, s - 1)]];
+        const double* lgp = Lg + (long)pcol * rmax;
         const bool bok = i16 < s, aok = i16 < nr;
         double bv[SB_KPW];
 #pragma unroll
@@ -822,6 +818,11 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
             bv[u] = (bok && l < j) ? t : 0.0;
           }
         }
+        // x4[row, p_k] (row p_k of x4 is contiguous over this workgroup's rows)
+        double xv = 0.0;
+        const int xr = tid & 15, xk = (tid >> 4) & 15;
+        if (tid < 16 * M && xr < nr && xk < s) xv = X2[(long)cand[pidx[xk]] * n + r0 + xr].x;
+        f64x4 D = {0, 0, 0, 0};
 #pragma unroll
         for (int u = 0; u < SB_KPW; ++u) {
           if (w + 8 * u >= nks) break;
@@ -831,6 +832,7 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) red[w * 256 + (kq + 4 * r) * 16 + i16] = D[r];
+        if (tid < 16 * M) x4p[xr * M + xk] = xv * xv * scale;
         __syncthreads();
         if (tid < 256) {
           double t = 0.0;
@@ -869,30 +871,37 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
               sb_st_d(lg + k, l);
             }
           }
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // before the next post (barrier)
         }
       }
-      __syncthreads();  // every store of this batch complete before the next post
+      __syncthreads();
       j += s;
       if (stop) return;
     }
   }
   // ======================= leader =======================
-  double* R = red + 8 * 256;        // M x M candidates' residual block
-  double* lv = R + M * M;           // per-wave top-(M+1) lists: value
-  int* li = (int*)(lv + 8 * (M + 1));  // row
-  double* Ldn = (double*)(li + 8 * (M + 1) + 2);  // [c][k] entries of the batch's columns
+  double* lv = red + 8 * 256;       // candidate list (value, row)
+  int* li = (int*)(lv + SB_LIST);
+  double* tv = (double*)(li + SB_LIST);  // per-thread best (value, row)
+  int* ti = (int*)(tv + SB_THREADS);
+  double* Rs = (double*)(ti + SB_THREADS);  // M x M candidates' residual block
+  double* Ldn = Rs + M * M;         // [c][k] entries of the batch's columns
   int* cand = s_i;                  // candidates (rows; -1 none)
-  int* pv = s_i + M;
-  int* pidx = s_i + 2 * M;
-  int* st = s_i + 3 * M;            // s, stop, rank, Brow
+  int* pidx = s_i + M;
+  int* st = s_i + 2 * M;            // s, stop, rank, Brow, nvalid
   double* cd = s_d;                 // candidates' residual diagonal (batch start)
   double* dpv = s_d + M;
-  double* misc = s_d + 2 * M;       // thr, Bv
+  double* misc = s_d + 2 * M;       // thr, Bv, tau value, then dnew (M)
   int j = 0;
   for (unsigned b = 1;; ++b) {
     const bool pr = prof != nullptr && tid == 0 && b <= 8192;
-    // ---- gather every row's residual diagonal ----
+    // ---- every row's residual diagonal: all loads in flight, stale granules re-read ----
+    u32x4 g[SB_GR];
+#pragma unroll
+    for (int u = 0; u < SB_GR; ++u) {
+      const int row = min(tid + SB_THREADS * u, n - 1);
+      g[u] = sc_load_rec(ddg + row);
+    }
     double v[SB_GR];
     int rw[SB_GR];
     bool bad = false;
@@ -902,89 +911,81 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
       v[u] = -1e300;
       rw[u] = 0x7fffffff;
       if (row < n && !bad) {
-        u32x4 g;
-        if (sb_wait(ddg + row, b, err, &g)) {
-          v[u] = sb_dbl(g);
-          rw[u] = row;
+        if (sb_repoll(ddg + row, b, err, &g[u])) {
+          v[u] = sb_dbl(g[u]);
+          if (v[u] > -1e299) rw[u] = row;
         } else {
           bad = true;
         }
       }
     }
     if (bad) s_bad = 1;
-    __syncthreads();
+    // ---- candidates: the M best (value desc, row asc) and the bound B (the (M+1)-th) ----
+    // each thread's best; tau = the (M+1)-th best of those: every key >= tau comes from a thread
+    // whose best is >= tau (at most M+1 threads x SB_GR keys), and the M+1 best keys are >= tau
+    double bv = -1e300;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int u = 0; u < SB_GR; ++u)
+      if (sc_better(v[u], rw[u], bv, bi)) { bv = v[u]; bi = rw[u]; }
+    tv[tid] = bv;
+    ti[tid] = bi;
+    if (tid == 0) s_cnt = 0;
+    const int nvalid = __syncthreads_count(bi != 0x7fffffff);
     if (s_bad) return;
     if (pr) prof[4L * (b - 1)] = __builtin_amdgcn_s_memrealtime();
-    // ---- top-(M+1) by (value desc, row asc): per wave by repeated extraction, then merged ----
-    for (int rd = 0; rd <= M; ++rd) {
-      double bv = -1e300;
-      int bi = 0x7fffffff, bu = -1;
-#pragma unroll
-      for (int u = 0; u < SB_GR; ++u)
-        if (sc_better(v[u], rw[u], bv, bi)) { bv = v[u]; bi = rw[u]; bu = u; }
-      double mv = bv;
-      int mi = bi;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const double v2 = __shfl_xor(mv, o, 64);
-        const int i2 = __shfl_xor(mi, o, 64);
-        if (sc_better(v2, i2, mv, mi)) { mv = v2; mi = i2; }
+    if (bi != 0x7fffffff && nvalid > M) {
+      int rk = 0;
+      for (int t = 0; t < SB_THREADS; ++t) rk += sc_better(tv[t], ti[t], bv, bi) ? 1 : 0;
+      if (rk == M) {
+        misc[2] = bv;
+        st[3] = bi;
       }
-      if (bi == mi && bu >= 0 && mi != 0x7fffffff) {
-#pragma unroll
-        for (int u = 0; u < SB_GR; ++u)
-          if (u == bu) { v[u] = -1e300; rw[u] = 0x7fffffff; }
-      }
-      if (lane == 0) { lv[w * (M + 1) + rd] = mv; li[w * (M + 1) + rd] = mi; }
     }
     __syncthreads();
-    if (w == 0) {
-      double mv2[3];
-      int mi2[3];
+    const double tau = nvalid > M ? misc[2] : -1e300;
+    const int taui = nvalid > M ? st[3] : 0x7fffffff;
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const int e = lane + 64 * u;
-        mv2[u] = e < 8 * (M + 1) ? lv[e] : -1e300;
-        mi2[u] = e < 8 * (M + 1) ? li[e] : 0x7fffffff;
-      }
-      for (int rd = 0; rd <= M; ++rd) {
-        double bv = -1e300;
-        int bi = 0x7fffffff, bu = -1;
-#pragma unroll
-        for (int u = 0; u < 3; ++u)
-          if (sc_better(mv2[u], mi2[u], bv, bi)) { bv = mv2[u]; bi = mi2[u]; bu = u; }
-        double mv = bv;
-        int mi = bi;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          const double v2 = __shfl_xor(mv, o, 64);
-          const int i2 = __shfl_xor(mi, o, 64);
-          if (sc_better(v2, i2, mv, mi)) { mv = v2; mi = i2; }
-        }
-        if (bi == mi && bu >= 0 && mi != 0x7fffffff) {
-#pragma unroll
-          for (int u = 0; u < 3; ++u)
-            if (u == bu) { mv2[u] = -1e300; mi2[u] = 0x7fffffff; }
-        }
-        if (lane == 0) {
-          const bool valid = mi != 0x7fffffff && mv > -1e299;
-          if (rd < M) {
-            cand[rd] = valid ? mi : -1;
-            cd[rd] = valid ? mv : -1e300;
-          } else {
-            misc[1] = valid ? mv : -1e300;   // the bound B (largest non-candidate)
-            st[3] = valid ? mi : 0x7fffffff;
-          }
+    for (int u = 0; u < SB_GR; ++u)
+      if (rw[u] != 0x7fffffff && !sc_better(tau, taui, v[u], rw[u])) {
+        const int p = atomicAdd(&s_cnt, 1);
+        if (p < SB_LIST) {
+          lv[p] = v[u];
+          li[p] = rw[u];
         }
       }
-      if (lane == 0 && b == 1)
-        misc[0] = tol > 0 ? tol * cd[0] : (double)n * 2.220446049250313e-16 * cd[0];
+    __syncthreads();
+    const int cnt = min(s_cnt, SB_LIST);
+    if (tid <= M) {  // defaults: no candidate / no bound
+      if (tid < M) {
+        cand[tid] = -1;
+        cd[tid] = -1e300;
+      } else {
+        misc[1] = -1e300;
+        st[3] = 0x7fffffff;
+      }
     }
     __syncthreads();
+    if (tid < cnt) {
+      int rk = 0;
+      for (int t = 0; t < cnt; ++t) rk += sc_better(lv[t], li[t], lv[tid], li[tid]) ? 1 : 0;
+      if (rk < M) {
+        cand[rk] = li[tid];
+        cd[rk] = lv[tid];
+      } else if (rk == M) {
+        misc[1] = lv[tid];
+        st[3] = li[tid];
+      }
+    }
+    __syncthreads();
+    if (tid == 0 && b == 1)
+      misc[0] = tol > 0 ? tol * cd[0] : (double)n * 2.220446049250313e-16 * cd[0];
     if (pr) prof[4L * (b - 1) + 1] = __builtin_amdgcn_s_memrealtime();
     // ---- R = x4[C,C] - L[C,:j] L[C,:j]^T (FP64 MFMA, K over the 8 waves; A = B^T) ----
     {
-      f64x4 D = {0, 0, 0, 0};
+      double xv = 0.0;
+      const int xa = (tid >> 4) & 15, xc = tid & 15;
+      if (tid < 256 && cand[xa] >= 0 && cand[xc] >= 0) xv = X2[(long)cand[xa] * n + cand[xc]].x;
       const int nks = (j + 3) >> 2;
       const int ci = cand[i16];
       const double* lgc = Lg + (long)max(ci, 0) * rmax;
@@ -998,6 +999,7 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
           av[u] = (ci >= 0 && l < j) ? t : 0.0;
         }
       }
+      f64x4 D = {0, 0, 0, 0};
 #pragma unroll
       for (int u = 0; u < SB_KPW; ++u) {
         if (w + 8 * u >= nks) break;
@@ -1007,68 +1009,65 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
       for (int r = 0; r < 4; ++r) red[w * 256 + (kq + 4 * r) * 16 + i16] = D[r];
       __syncthreads();
       if (tid < 256) {
-        const int a = tid >> 4, c = tid & 15;
         double t = 0.0;
 #pragma unroll
         for (int q = 0; q < 8; ++q) t += red[q * 256 + tid];
-        double x = 0.0;
-        if (cand[a] >= 0 && cand[c] >= 0) {
-          const double y = X2[(long)cand[a] * n + cand[c]].x;
-          x = y * y * scale;
-        }
-        R[a * M + c] = x - t;
+        Rs[tid] = xv * xv * scale - t;
       }
       __syncthreads();
     }
     if (pr) prof[4L * (b - 1) + 2] = __builtin_amdgcn_s_memrealtime();
-    // ---- the greedy steps on the candidates (wave 0; lane c < M holds candidate c) ----
+    // ---- the greedy steps on the candidates (wave 0; lane c < M holds candidate c's R row) ----
     if (w == 0) {
       const double thr = misc[0], Bv = misc[1];
       const int Brow = st[3];
       const int myrow = lane < M ? cand[lane] : -1;
       double d = lane < M ? cd[lane] : -1e300;
       bool chosen = myrow < 0;
+      double Rr[M];
+#pragma unroll
+      for (int c = 0; c < M; ++c) Rr[c] = lane < M ? Rs[lane * M + c] : 0.0;
       int k = 0, stop = 0, rk = 0;
       for (;;) {
         if (j + k >= rmax) { stop = 1; rk = rmax; break; }
-        double mv = (lane < M && !chosen) ? d : -1e300;
-        int mi = (lane < M && !chosen) ? myrow : 0x7fffffff;
+        const double dv = (lane < M && !chosen) ? d : -1e300;
+        const int dr = (lane < M && !chosen) ? myrow : 0x7fffffff;
+        double mv = -1e300;
+        int mi = 0x7fffffff, pc = -1;
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1) {
-          const double v2 = __shfl_xor(mv, o, 64);
-          const int i2 = __shfl_xor(mi, o, 64);
-          if (sc_better(v2, i2, mv, mi)) { mv = v2; mi = i2; }
+        for (int c = 0; c < M; ++c) {
+          const double vc = sb_readlane_d(dv, c);
+          const int ic = __builtin_amdgcn_readlane(dr, c);
+          if (sc_better(vc, ic, mv, mi)) { mv = vc; mi = ic; pc = c; }
         }
-        mv = __shfl(mv, 0, 64);
-        mi = __shfl(mi, 0, 64);
         if (mi == 0x7fffffff) {  // every candidate chosen
           if (Brow == 0x7fffffff) { stop = 1; rk = j + k; }  // ... and no other row left
           break;
         }
         if (!sc_better(mv, mi, Bv, Brow)) break;  // a non-candidate could win the next step
         if (!(mv > thr)) { stop = 1; rk = j + k; break; }  // the global max is below dpstrf's tol
-        const int pc = __builtin_amdgcn_readfirstlane(__ffsll((long long)__ballot(lane < M && myrow == mi)) - 1);
         const double sq = sqrt(mv), inv = 1.0 / sq;
+        double rp = 0.0;
+#pragma unroll
+        for (int c = 0; c < M; ++c) rp = c == pc ? Rr[c] : rp;
         double l = 0.0;
         if (lane < M) {
-          l = lane == pc ? sq : (chosen ? 0.0 : R[lane * M + pc] * inv);
+          l = lane == pc ? sq : (chosen ? 0.0 : rp * inv);
           Ldn[lane * M + k] = l;
         }
         if (lane == 0) {
-          pv[k] = mi;
           pidx[k] = pc;
           dpv[k] = mv;
           piv[j + k] = mi;
         }
-        // rank-1 update of the candidates' residual block (row `lane`; all lanes shuffle)
-        double lc[M];
+        // rank-1 update of the candidates' residual block
+        const bool upd = lane < M && !chosen && lane != pc;
 #pragma unroll
-        for (int c = 0; c < M; ++c) lc[c] = __shfl(l, c, 64);
-        if (lane < M && !chosen && lane != pc) {
-          d -= l * l;
-#pragma unroll
-          for (int c = 0; c < M; ++c) R[lane * M + c] -= l * lc[c];
+        for (int c = 0; c < M; ++c) {
+          const double lc = sb_readlane_d(l, c);
+          if (upd) Rr[c] -= l * lc;
         }
+        if (upd) d -= l * l;
         if (lane == pc) {
           chosen = true;
           d = -1e300;
@@ -1080,7 +1079,7 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
         rk = j;
         if (lane == 0) atomicExch(err, 1);
       }
-      if (lane < M) misc[2 + lane] = d;
+      if (lane < M) misc[3 + lane] = d;
       if (lane == 0) {
         st[0] = k;
         st[1] = stop;
@@ -1089,25 +1088,24 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
       }
     }
     __syncthreads();
-    // ---- publish ----
+    // ---- publish: one granule per thread (header included; readers re-read stale ones) ----
     const int s = st[0], stop = st[1];
-    if (tid < M) {
-      sb_st_i(&pub->pv[tid], tid < s ? pv[tid] : 0);
-      sb_st_i(&pub->pidx[tid], tid < s ? pidx[tid] : 0);
-      sb_st_i(&pub->cand[tid], cand[tid]);
-      sb_st_d(&pub->dp[tid], tid < s ? dpv[tid] : 1.0);
-      sb_st_d(&pub->dnew[tid], misc[2 + tid]);
-    }
-    for (int e = tid; e < M * M; e += SB_THREADS) sb_st_d(&pub->Lnew[e], (e % M) < s ? Ldn[e] : 0.0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
     if (tid == 0) {
       u32x4 h;
       h.x = (unsigned)s;
-      h.y = (unsigned)s;
-      h.z = (unsigned)stop;
+      h.y = (unsigned)stop;
+      h.z = (unsigned)st[2];
       h.w = b;
-      sc_store_rec(&pub->hdr, h);
+      sc_store_rec(pub, h);
+    } else if (tid < 1 + M) {
+      const int c = tid - 1;
+      sc_store_rec(pub + tid, sb_gran(misc[3 + c], (unsigned)cand[c], b));
+    } else if (tid < 1 + 2 * M) {
+      const int k = tid - 1 - M;
+      sc_store_rec(pub + tid, sb_gran(k < s ? dpv[k] : 1.0, k < s ? (unsigned)pidx[k] : 0u, b));
+    } else if (tid < SB_NPUB) {
+      const int e = tid - 1 - 2 * M;
+      sc_store_rec(pub + tid, sb_gran((e % M) < s ? Ldn[e] : 0.0, (unsigned)e, b));
     }
     if (pr) prof[4L * (b - 1) + 3] = __builtin_amdgcn_s_memrealtime();
     j += s;
@@ -1488,18 +1486,18 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
   if (G + 1 > ncu) return 0;
   constexpr size_t kLds = 150 * 1024;
   const size_t owner = sizeof(double) * (8 * 256 + 3 * 256 + (size_t)RW * rmax);
-  const size_t leader = sizeof(double) * (8 * 256 + 2 * 256 + 8 * (SB_M + 1) + 128);
+  const size_t leader = sizeof(double) * (8 * 256 + 2 * SB_LIST + 2 * SB_THREADS + 2 * 256 + 64);
   const size_t lds = std::max(owner, leader);
   if (lds > kLds) return 0;
   // scratch in the caller's work area (n*n doubles): granules, publish area, global L, error flag
   u32x4* ddg = (u32x4*)work;
-  const long pub_d = (long)((sizeof(SelPub) + 15) / 16) * 2;
-  SelPub* pub = (SelPub*)(work + 2L * n);
+  const long pub_d = 2L * SB_NPUB;
+  u32x4* pub = (u32x4*)(work + 2L * n);
   double* Lg = work + 2L * n + pub_d;
   int* err = (int*)(Lg + (long)n * rmax);
   if (2L * n + pub_d + (long)n * rmax + 2 > (long)n * n) return 0;
   FISDF_HIP(hipMemsetAsync(ddg, 0, sizeof(u32x4) * n, s));
-  FISDF_HIP(hipMemsetAsync(pub, 0, sizeof(u32x4), s));
+  FISDF_HIP(hipMemsetAsync(pub, 0, sizeof(u32x4) * SB_NPUB, s));  // no stale batch words
   FISDF_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
   FISDF_HIP(hipMemsetAsync(rank, 0, sizeof(int), s));
   static bool attr = false;
