@@ -673,34 +673,37 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
 // (4.0 ms of every k-shard rank).  Here the grid exchanges once per BATCH:
 //  * owners (workgroups 0..G-1, RW <= 16 rows each, their L rows in LDS and in the row-major
 //    global L) post their residual diagonal as tagged 16-byte granules {d, row, batch};
-//  * the leader (workgroup G) reads them all, takes the M largest (value desc, row asc: LAPACK's
-//    first index on ties) as candidates C and the next one as the bound B, forms the candidates'
-//    residual block R = x4[C,C] - L[C,:j] L[C,:j]^T on FP64 MFMA from the global L rows, and runs
-//    the greedy steps on R alone while the chosen diagonal beats B.  No other row can win such a
-//    step: its residual diagonal only decreases (d -= l^2), and at the batch start it was <= B —
-//    so every accepted step is exactly the greedy (dpstrf) pivot of the whole matrix;
+//  * the leader (workgroup G) reads them all and takes as candidates C the 4 best rows (value
+//    desc, row asc: LAPACK's first index on ties) of each of its 8 waves' share, and as the bound
+//    B the best row left out; it forms the candidates' residual block R = x4[C,C] - L[C,:j]
+//    L[C,:j]^T on FP64 MFMA from the global L rows and runs the greedy steps on R alone while the
+//    chosen diagonal beats B.  No other row can win such a step: its residual diagonal only
+//    decreases (d -= l^2) and was <= B at the batch start, so every accepted step is exactly the
+//    greedy (dpstrf) pivot of the whole matrix;
 //  * the leader publishes the batch (pivots, their d, the candidates' new L entries and
 //    residuals); each owner forms its rows' new columns with one MFMA pass against the pivot
 //    rows (acc = L[rows,:j] L[piv,:j]^T) plus the in-batch triangular part, and posts again.
-// Simulated on the C3 parent grid (n 3375, 600 pivots): 100 batches at M = 16 (6 pivots each).
-// Hand-offs: sc1 (write-through) stores of every handed-off byte, s_waitcnt vmcnt(0) and a
-// workgroup barrier before the signalling store, sc1 loads on the reading side (the pattern of
-// pchol_select_coop).  Every wait is bounded: a stalled wait sets *err and the grid drains.
+// Simulated on the C3 parent grid (n 3375, 600 pivots): 99 batches of 32 per-wave candidates
+// (100 with the exact top 16, 165 with 2 per wave).  Hand-offs: every handed-off byte is stored
+// sc1 (write-through) and loaded sc1; the owners' L stores wait (vmcnt) behind a barrier before
+// their next post; the published granules carry their batch and a stale one is re-read.  Every
+// wait is bounded: a stalled wait sets *err and the grid drains (the caller then falls back).
 constexpr int SB_THREADS = 512;
-constexpr int SB_M = 16;          // candidates per batch (one 16 x 16 MFMA block)
-constexpr int SB_GR = 8;          // granules per leader thread: n <= 8 * 512
-constexpr int SB_KPW = 40;        // K steps (4 columns) per wave in the MFMA passes: rmax <= 1280
-constexpr int SB_NPUB = 1 + 2 * SB_M + SB_M * SB_M;  // granules of one publish
-constexpr int SB_LIST = 8 * (SB_M + 1) + 24;          // the leader's candidate list capacity
+constexpr int SB_TW = 4;                    // candidates per leader wave
+constexpr int SB_M = 8 * SB_TW;             // candidates per batch
+constexpr int SB_S = 16;                    // pivots per batch at most (one MFMA N block)
+constexpr int SB_GR = 8;                    // granules per leader thread: n <= 8 * 512
+constexpr int SB_KCH = 20;                  // K steps (4 columns) per wave and load chunk
+constexpr int SB_NPUB = 1 + SB_M + SB_S + SB_M * SB_S;  // granules of one publish
 constexpr long SB_SPIN = 1L << 22;
 
 // The leader's publish: SB_NPUB 16-byte granules {payload lo, payload hi, aux, batch}, each
 // written whole by one sc1 store (untorn), so a reader checks every granule's batch word and
 // re-reads a stale one — no flag-after-payload ordering is needed:
-//   [0]            {s, stop, rank, b}
-//   [1 + c]        {dnew_c (the candidate's residual after the batch, -1e300 once chosen), row_c}
-//   [1 + M + k]    {d of pivot k when chosen, candidate index of pivot k}
-//   [1 + 2M + e]   {Lnew[e] = L[cand e / M, j + e % M] (the batch's columns), e}
+//   [0]                  {s, stop, rank, b}
+//   [1 + c]              {dnew_c (the candidate's residual after the batch, -1e300 chosen), row_c}
+//   [1 + M + k]          {d of pivot k when chosen, candidate index of pivot k}
+//   [1 + M + S + c S + k] {L[cand c, j + k] (the batch's columns of the candidates), index}
 __device__ __forceinline__ double sb_dbl(u32x4 g) {
   return __longlong_as_double((long long)(((unsigned long long)g.y << 32) | g.x));
 }
@@ -732,11 +735,45 @@ __device__ __forceinline__ bool sb_repoll(const u32x4* gp, unsigned tag, int* er
   }
   return true;
 }
-__device__ __forceinline__ double sb_readlane_d(double v, int l) {
+// one DPP step of the wave arg-max (value desc, row asc); out-of-row sources keep the own key
+template <int CTRL, int RMASK>
+__device__ __forceinline__ void sb_dpp_step(double& v, int& r) {
   const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)b, l);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  const int lo = (int)b, hi = (int)(b >> 32);
+  const int lo2 = __builtin_amdgcn_update_dpp(lo, lo, CTRL, RMASK, 0xf, false);
+  const int hi2 = __builtin_amdgcn_update_dpp(hi, hi, CTRL, RMASK, 0xf, false);
+  const int r2 = __builtin_amdgcn_update_dpp(r, r, CTRL, RMASK, 0xf, false);
+  const double v2 = __longlong_as_double(((long long)hi2 << 32) | (unsigned)lo2);
+  if (sc_better(v2, r2, v, r)) {
+    v = v2;
+    r = r2;
+  }
+}
+// the wave's best key, uniform in every lane: row_shr 1/2/4/8 leaves each row's best in its
+// lane 15, row_bcast 15/31 carry them up to lane 63
+__device__ __forceinline__ void sb_wave_best(double& v, int& r) {
+  sb_dpp_step<0x111, 0xf>(v, r);
+  sb_dpp_step<0x112, 0xf>(v, r);
+  sb_dpp_step<0x114, 0xf>(v, r);
+  sb_dpp_step<0x118, 0xf>(v, r);
+  sb_dpp_step<0x142, 0xa>(v, r);
+  sb_dpp_step<0x143, 0xc>(v, r);
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, 63);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  v = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  r = __builtin_amdgcn_readlane(r, 63);
+}
+template <int A, int B>
+__device__ __forceinline__ void sb_cx(double (&v)[SB_GR], int (&r)[SB_GR]) {
+  if (sc_better(v[B], r[B], v[A], r[A])) {
+    const double tv = v[A];
+    const int tr = r[A];
+    v[A] = v[B];
+    r[A] = r[B];
+    v[B] = tv;
+    r[B] = tr;
+  }
 }
 
 __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
@@ -745,25 +782,25 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
     u32x4* __restrict__ pub, double* __restrict__ Lg, int* __restrict__ err,
     unsigned long long* __restrict__ prof) {
   extern __shared__ double sm[];
-  constexpr int M = SB_M;
+  constexpr int M = SB_M, S = SB_S;
   const int G = gridDim.x - 1, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i16 = lane & 15, kq = lane >> 4;
-  double* red = sm;                 // [8 waves][256] MFMA partials
-  __shared__ int s_i[3 * M + 8];
-  __shared__ double s_d[3 * M + 8];
-  __shared__ int s_bad, s_cnt;
+  double* red = sm;  // MFMA partials
+  __shared__ int s_i[M + S + 8];
+  __shared__ double s_d[M + S + M + 8];
+  __shared__ int s_bad;
   if (tid == 0) s_bad = 0;
   if ((int)blockIdx.x < G) {
     // ======================= owner: rows [r0, r0 + nr) =======================
     double* Lr = red + 8 * 256;     // RW x rmax, row-major
-    double* Lnew = Lr + (long)RW * rmax;  // M x M (the publish's candidate entries)
-    double* x4p = Lnew + M * M;     // [row][k] = x4[row, p_k]
-    double* acc = x4p + 16 * M;     // [row][k] = L[row, :j] . L[p_k, :j]
-    int* pidx = s_i;                // candidate index of pivot k
-    int* cand = s_i + M;            // candidates (rows, -1 none)
-    int* hdr = s_i + 2 * M;         // s, stop
-    double* dpv = s_d;
-    double* dnew = s_d + M;
+    double* Lnew = Lr + (long)RW * rmax;  // [candidate][k]: the batch's columns of the candidates
+    double* x4p = Lnew + M * S;     // [row][k] = x4[row, p_k]
+    double* acc = x4p + 16 * S;     // [row][k] = L[row, :j] . L[p_k, :j]
+    int* cand = s_i;                // candidates (rows, -1 none)
+    int* pidx = s_i + M;            // candidate index of pivot k
+    int* hdr = s_i + M + S;         // s, stop
+    double* dnew = s_d;
+    double* dpv = s_d + M;
     const int r0 = blockIdx.x * RW, nr = max(0, min(RW, n - r0));
     double dd = -1e300;             // thread r < nr: residual diagonal of row r0 + r
     if (tid < nr) {
@@ -773,72 +810,76 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
     int j = 0;
     for (unsigned b = 1;; ++b) {
       if (tid < nr) sc_store_rec(ddg + r0 + tid, sb_gran(dd, (unsigned)(r0 + tid), b));  // post
-      if (tid == 0) {  // the batch's header, then every payload granule (re-read if stale)
-        u32x4 h = sc_load_rec(pub);
-        if (sb_repoll(pub, b, err, &h)) {
-          hdr[0] = (int)h.x;
-          hdr[1] = (int)h.y;
+      // the leader's publish of this batch: every granule read in one round, stale ones re-read
+      u32x4 g0 = sc_load_rec(pub + tid), g1;
+      const bool two = tid + SB_THREADS < SB_NPUB;
+      if (two) g1 = sc_load_rec(pub + tid + SB_THREADS);
+      bool ok = sb_repoll(pub + tid, b, err, &g0);
+      if (two && ok) ok = sb_repoll(pub + tid + SB_THREADS, b, err, &g1);
+      if (!ok) s_bad = 1;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e = tid + h * SB_THREADS;
+        if (h == 1 && !two) break;
+        const u32x4 g = h ? g1 : g0;
+        const double v = sb_dbl(g);
+        if (e == 0) {
+          hdr[0] = (int)g.x;
+          hdr[1] = (int)g.y;
+        } else if (e < 1 + M) {
+          cand[e - 1] = (int)g.z;
+          dnew[e - 1] = v;
+        } else if (e < 1 + M + S) {
+          pidx[e - 1 - M] = (int)g.z;
+          dpv[e - 1 - M] = v;
         } else {
-          s_bad = 1;
+          Lnew[e - 1 - M - S] = v;
         }
       }
       __syncthreads();
       if (s_bad) return;
       const int s = hdr[0], stop = hdr[1];
-      if (tid >= 1 && tid < SB_NPUB) {
-        u32x4 g = sc_load_rec(pub + tid);
-        if (!sb_repoll(pub + tid, b, err, &g)) s_bad = 1;
-        const double v = sb_dbl(g);
-        if (tid < 1 + M) {
-          cand[tid - 1] = (int)g.z;
-          dnew[tid - 1] = v;
-        } else if (tid < 1 + 2 * M) {
-          pidx[tid - 1 - M] = (int)g.z;
-          dpv[tid - 1 - M] = v;
-        } else {
-          Lnew[tid - 1 - 2 * M] = v;
-        }
-      }
-      __syncthreads();
-      if (s_bad) return;
       if (s > 0) {
         // acc[r][k] = sum_{l < j} L[r0 + r, l] L[p_k, l]: FP64 MFMA, A = the owned rows (LDS),
-        // B = the pivot rows (global L), K split over the 8 waves; every load issued up front
+        // B = the pivot rows (global L), K split over the 8 waves, a chunk's loads issued up front
         const int nks = (j + 3) >> 2;
-        const int pcol = cand[pidx[min(i16, s - 1)]];
-        const double* lgp = Lg + (long)pcol * rmax;
+        const int prow = cand[pidx[min(i16, s - 1)]];
+        const double* lgp = Lg + (long)prow * rmax;
         const bool bok = i16 < s, aok = i16 < nr;
-        double bv[SB_KPW];
-#pragma unroll
-        for (int u = 0; u < SB_KPW; ++u) {
-          const int l = (w + 8 * u) * 4 + kq;
-          bv[u] = 0.0;
-          if (w + 8 * u < nks) {
-            const double t = sb_ld_d(lgp + min(l, max(j - 1, 0)));
-            bv[u] = (bok && l < j) ? t : 0.0;
-          }
-        }
         // x4[row, p_k] (row p_k of x4 is contiguous over this workgroup's rows)
         double xv = 0.0;
         const int xr = tid & 15, xk = (tid >> 4) & 15;
-        if (tid < 16 * M && xr < nr && xk < s) xv = X2[(long)cand[pidx[xk]] * n + r0 + xr].x;
+        if (tid < 16 * S && xr < nr && xk < s) xv = X2[(long)cand[pidx[xk]] * n + r0 + xr].x;
         f64x4 D = {0, 0, 0, 0};
+        for (int c0 = 0; c0 < nks; c0 += 8 * SB_KCH) {
+          double bv[SB_KCH];
 #pragma unroll
-        for (int u = 0; u < SB_KPW; ++u) {
-          if (w + 8 * u >= nks) break;
-          const int l = (w + 8 * u) * 4 + kq;
-          const double a = (aok && l < j) ? Lr[(long)i16 * rmax + l] : 0.0;
-          D = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv[u], D, 0, 0, 0);
+          for (int u = 0; u < SB_KCH; ++u) {
+            const int ks = c0 + w + 8 * u, l = ks * 4 + kq;
+            bv[u] = 0.0;
+            if (ks < nks) {
+              const double t = sb_ld_d(lgp + min(l, j - 1));
+              bv[u] = (bok && l < j) ? t : 0.0;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < SB_KCH; ++u) {
+            const int ks = c0 + w + 8 * u, l = ks * 4 + kq;
+            if (ks < nks) {  // wave-uniform
+              const double a = (aok && l < j) ? Lr[(long)i16 * rmax + l] : 0.0;
+              D = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv[u], D, 0, 0, 0);
+            }
+          }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) red[w * 256 + (kq + 4 * r) * 16 + i16] = D[r];
-        if (tid < 16 * M) x4p[xr * M + xk] = xv * xv * scale;
+        if (tid < 16 * S) x4p[xr * S + xk] = xv * xv * scale;
         __syncthreads();
         if (tid < 256) {
           double t = 0.0;
 #pragma unroll
           for (int q = 0; q < 8; ++q) t += red[q * 256 + tid];
-          acc[(tid >> 4) * M + (tid & 15)] = t;
+          acc[(tid >> 4) * S + (tid & 15)] = t;
         }
         __syncthreads();
         // the batch's columns of each owned row, in order (one thread per row)
@@ -852,7 +893,7 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
           double* lg = Lg + (long)row * rmax + j;
           if (ci >= 0) {  // a candidate: the leader's entries and residual (a pivot: -1e300)
             for (int k = 0; k < s; ++k) {
-              const double l = Lnew[ci * M + k];
+              const double l = Lnew[ci * S + k];
               lr[k] = l;
               sb_st_d(lg + k, l);
             }
@@ -861,8 +902,8 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
             for (int k = 0; k < s; ++k) {
               double l = 0.0;
               if (dd > -1e299) {
-                const double* lp = Lnew + pidx[k] * M;  // L[p_k, j + k'] for k' < k
-                double v = x4p[tid * M + k] - acc[tid * M + k];
+                const double* lp = Lnew + pidx[k] * S;  // L[p_k, j + k'] for k' < k
+                double v = x4p[tid * S + k] - acc[tid * S + k];
                 for (int k2 = 0; k2 < k; ++k2) v -= lr[k2] * lp[k2];
                 l = v / sqrt(dpv[k]);
                 dd -= l * l;
@@ -880,143 +921,160 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
     }
   }
   // ======================= leader =======================
-  double* lv = red + 8 * 256;       // candidate list (value, row)
-  int* li = (int*)(lv + SB_LIST);
-  double* tv = (double*)(li + SB_LIST);  // per-thread best (value, row)
-  int* ti = (int*)(tv + SB_THREADS);
-  double* Rs = (double*)(ti + SB_THREADS);  // M x M candidates' residual block
-  double* Ldn = Rs + M * M;         // [c][k] entries of the batch's columns
+  double* Rs = red + 3 * 8 * 256;   // M x M candidates' residual block
+  double* Lb = Rs + M * M;          // the step's column, broadcast through LDS
+  double* Ldn = Lb + 64;            // [c][k] the batch's columns of the candidates
+  double* wbv = Ldn + M * S;        // per-wave bound (value, row)
+  int* wbi = (int*)(wbv + 8);
   int* cand = s_i;                  // candidates (rows; -1 none)
   int* pidx = s_i + M;
-  int* st = s_i + 2 * M;            // s, stop, rank, Brow, nvalid
+  int* st = s_i + M + S;            // s, stop, rank, Brow
   double* cd = s_d;                 // candidates' residual diagonal (batch start)
   double* dpv = s_d + M;
-  double* misc = s_d + 2 * M;       // thr, Bv, tau value, then dnew (M)
+  double* dn = s_d + M + S;         // candidates' residual after the batch
+  double* misc = s_d + 2 * M + S;   // thr, Bv
   int j = 0;
   for (unsigned b = 1;; ++b) {
     const bool pr = prof != nullptr && tid == 0 && b <= 8192;
     // ---- every row's residual diagonal: all loads in flight, stale granules re-read ----
-    u32x4 g[SB_GR];
-#pragma unroll
-    for (int u = 0; u < SB_GR; ++u) {
-      const int row = min(tid + SB_THREADS * u, n - 1);
-      g[u] = sc_load_rec(ddg + row);
-    }
     double v[SB_GR];
     int rw[SB_GR];
+    unsigned tg[SB_GR];
+#pragma unroll
+    for (int u = 0; u < SB_GR; ++u) {
+      const u32x4 g = sc_load_rec(ddg + min(tid + SB_THREADS * u, n - 1));
+      v[u] = sb_dbl(g);
+      tg[u] = g.w;
+    }
     bool bad = false;
 #pragma unroll
     for (int u = 0; u < SB_GR; ++u) {
       const int row = tid + SB_THREADS * u;
+      double x = v[u];
       v[u] = -1e300;
       rw[u] = 0x7fffffff;
       if (row < n && !bad) {
-        if (sb_repoll(ddg + row, b, err, &g[u])) {
-          v[u] = sb_dbl(g[u]);
-          if (v[u] > -1e299) rw[u] = row;
-        } else {
-          bad = true;
+        u32x4 g;
+        g.w = tg[u];
+        if (tg[u] != b) {
+          g = sc_load_rec(ddg + row);
+          if (!sb_repoll(ddg + row, b, err, &g)) bad = true;
+          x = sb_dbl(g);
+        }
+        if (!bad && x > -1e299) {
+          v[u] = x;
+          rw[u] = row;
         }
       }
     }
     if (bad) s_bad = 1;
-    // ---- candidates: the M best (value desc, row asc) and the bound B (the (M+1)-th) ----
-    // each thread's best; tau = the (M+1)-th best of those: every key >= tau comes from a thread
-    // whose best is >= tau (at most M+1 threads x SB_GR keys), and the M+1 best keys are >= tau
-    double bv = -1e300;
-    int bi = 0x7fffffff;
+    // ---- candidates: each wave's SB_TW best keys; the bound B: the best key left out ----
+    // sorting network (19 compare-exchanges) puts each thread's 8 keys in order
+    sb_cx<0, 1>(v, rw); sb_cx<2, 3>(v, rw); sb_cx<4, 5>(v, rw); sb_cx<6, 7>(v, rw);
+    sb_cx<0, 2>(v, rw); sb_cx<1, 3>(v, rw); sb_cx<4, 6>(v, rw); sb_cx<5, 7>(v, rw);
+    sb_cx<1, 2>(v, rw); sb_cx<5, 6>(v, rw); sb_cx<0, 4>(v, rw); sb_cx<3, 7>(v, rw);
+    sb_cx<1, 5>(v, rw); sb_cx<2, 6>(v, rw);
+    sb_cx<1, 4>(v, rw); sb_cx<3, 6>(v, rw);
+    sb_cx<2, 4>(v, rw); sb_cx<3, 5>(v, rw);
+    sb_cx<3, 4>(v, rw);
+    for (int rd = 0; rd <= SB_TW; ++rd) {
+      double mv = v[0];
+      int mi = rw[0];
+      sb_wave_best(mv, mi);
+      if (rd < SB_TW) {
+        if (lane == 0) {
+          const bool valid = mi != 0x7fffffff;
+          cand[w * SB_TW + rd] = valid ? mi : -1;
+          cd[w * SB_TW + rd] = valid ? mv : -1e300;
+        }
+        if (mi != 0x7fffffff && rw[0] == mi) {  // the winner's lane moves on to its next key
 #pragma unroll
-    for (int u = 0; u < SB_GR; ++u)
-      if (sc_better(v[u], rw[u], bv, bi)) { bv = v[u]; bi = rw[u]; }
-    tv[tid] = bv;
-    ti[tid] = bi;
-    if (tid == 0) s_cnt = 0;
-    const int nvalid = __syncthreads_count(bi != 0x7fffffff);
+          for (int u = 0; u + 1 < SB_GR; ++u) {
+            v[u] = v[u + 1];
+            rw[u] = rw[u + 1];
+          }
+          v[SB_GR - 1] = -1e300;
+          rw[SB_GR - 1] = 0x7fffffff;
+        }
+      } else if (lane == 0) {
+        wbv[w] = mv;
+        wbi[w] = mi;
+      }
+    }
+    __syncthreads();
     if (s_bad) return;
     if (pr) prof[4L * (b - 1)] = __builtin_amdgcn_s_memrealtime();
-    if (bi != 0x7fffffff && nvalid > M) {
-      int rk = 0;
-      for (int t = 0; t < SB_THREADS; ++t) rk += sc_better(tv[t], ti[t], bv, bi) ? 1 : 0;
-      if (rk == M) {
-        misc[2] = bv;
-        st[3] = bi;
+    if (tid == 0) {
+      double bv = -1e300;
+      int bi = 0x7fffffff;
+      for (int q = 0; q < 8; ++q)
+        if (sc_better(wbv[q], wbi[q], bv, bi)) { bv = wbv[q]; bi = wbi[q]; }
+      misc[1] = bv;
+      st[3] = bi;
+      if (b == 1) {  // dpstrf's tolerance from the largest diagonal
+        double mx = -1e300;
+        for (int c = 0; c < M; ++c) mx = fmax(mx, cd[c]);
+        misc[0] = tol > 0 ? tol * mx : (double)n * 2.220446049250313e-16 * mx;
       }
     }
-    __syncthreads();
-    const double tau = nvalid > M ? misc[2] : -1e300;
-    const int taui = nvalid > M ? st[3] : 0x7fffffff;
-#pragma unroll
-    for (int u = 0; u < SB_GR; ++u)
-      if (rw[u] != 0x7fffffff && !sc_better(tau, taui, v[u], rw[u])) {
-        const int p = atomicAdd(&s_cnt, 1);
-        if (p < SB_LIST) {
-          lv[p] = v[u];
-          li[p] = rw[u];
-        }
-      }
-    __syncthreads();
-    const int cnt = min(s_cnt, SB_LIST);
-    if (tid <= M) {  // defaults: no candidate / no bound
-      if (tid < M) {
-        cand[tid] = -1;
-        cd[tid] = -1e300;
-      } else {
-        misc[1] = -1e300;
-        st[3] = 0x7fffffff;
-      }
-    }
-    __syncthreads();
-    if (tid < cnt) {
-      int rk = 0;
-      for (int t = 0; t < cnt; ++t) rk += sc_better(lv[t], li[t], lv[tid], li[tid]) ? 1 : 0;
-      if (rk < M) {
-        cand[rk] = li[tid];
-        cd[rk] = lv[tid];
-      } else if (rk == M) {
-        misc[1] = lv[tid];
-        st[3] = li[tid];
-      }
-    }
-    __syncthreads();
-    if (tid == 0 && b == 1)
-      misc[0] = tol > 0 ? tol * cd[0] : (double)n * 2.220446049250313e-16 * cd[0];
-    if (pr) prof[4L * (b - 1) + 1] = __builtin_amdgcn_s_memrealtime();
-    // ---- R = x4[C,C] - L[C,:j] L[C,:j]^T (FP64 MFMA, K over the 8 waves; A = B^T) ----
+    // ---- R = x4[C,C] - L[C,:j] L[C,:j]^T (FP64 MFMA: blocks 00, 01, 11; K over the waves) ----
     {
-      double xv = 0.0;
-      const int xa = (tid >> 4) & 15, xc = tid & 15;
-      if (tid < 256 && cand[xa] >= 0 && cand[xc] >= 0) xv = X2[(long)cand[xa] * n + cand[xc]].x;
       const int nks = (j + 3) >> 2;
-      const int ci = cand[i16];
-      const double* lgc = Lg + (long)max(ci, 0) * rmax;
-      double av[SB_KPW];
+      const int c0r = cand[i16], c1r = cand[16 + i16];
+      const double* l0 = Lg + (long)max(c0r, 0) * rmax;
+      const double* l1 = Lg + (long)max(c1r, 0) * rmax;
+      double xv[2] = {0.0, 0.0};
 #pragma unroll
-      for (int u = 0; u < SB_KPW; ++u) {
-        const int l = (w + 8 * u) * 4 + kq;
-        av[u] = 0.0;
-        if (w + 8 * u < nks) {
-          const double t = sb_ld_d(lgc + min(l, max(j - 1, 0)));
-          av[u] = (ci >= 0 && l < j) ? t : 0.0;
+      for (int h = 0; h < 2; ++h) {
+        const int e = tid + h * SB_THREADS, a = e >> 5, c = e & 31;
+        if (cand[a] >= 0 && cand[c] >= 0) xv[h] = X2[(long)cand[a] * n + cand[c]].x;
+      }
+      f64x4 D00 = {0, 0, 0, 0}, D01 = {0, 0, 0, 0}, D11 = {0, 0, 0, 0};
+      for (int k0 = 0; k0 < nks; k0 += 8 * SB_KCH) {
+        double a0[SB_KCH], a1[SB_KCH];
+#pragma unroll
+        for (int u = 0; u < SB_KCH; ++u) {
+          const int ks = k0 + w + 8 * u, l = ks * 4 + kq;
+          a0[u] = 0.0;
+          a1[u] = 0.0;
+          if (ks < nks) {
+            const double t0 = sb_ld_d(l0 + min(l, j - 1)), t1 = sb_ld_d(l1 + min(l, j - 1));
+            a0[u] = (c0r >= 0 && l < j) ? t0 : 0.0;
+            a1[u] = (c1r >= 0 && l < j) ? t1 : 0.0;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < SB_KCH; ++u) {
+          if (k0 + w + 8 * u < nks) {  // wave-uniform
+            D00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], a0[u], D00, 0, 0, 0);
+            D01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], a1[u], D01, 0, 0, 0);
+            D11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[u], a1[u], D11, 0, 0, 0);
+          }
         }
       }
-      f64x4 D = {0, 0, 0, 0};
 #pragma unroll
-      for (int u = 0; u < SB_KPW; ++u) {
-        if (w + 8 * u >= nks) break;
-        D = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], av[u], D, 0, 0, 0);
+      for (int r = 0; r < 4; ++r) {
+        const int o = (kq + 4 * r) * 16 + i16;
+        red[(0 * 8 + w) * 256 + o] = D00[r];
+        red[(1 * 8 + w) * 256 + o] = D01[r];
+        red[(2 * 8 + w) * 256 + o] = D11[r];
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[w * 256 + (kq + 4 * r) * 16 + i16] = D[r];
       __syncthreads();
-      if (tid < 256) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e = tid + h * SB_THREADS, a = e >> 5, c = e & 31;
+        // block of (a, c): 00, 01 (a < 16 <= c), 10 = 01^T, 11
+        const int blk = (a < 16) ? (c < 16 ? 0 : 1) : (c < 16 ? 1 : 2);
+        const int ra = (a < 16 || blk == 2) ? (a & 15) : (c & 15);
+        const int rc = (a < 16 || blk == 2) ? (c & 15) : (a & 15);
         double t = 0.0;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) t += red[q * 256 + tid];
-        Rs[tid] = xv * xv * scale - t;
+        for (int q = 0; q < 8; ++q) t += red[(blk * 8 + q) * 256 + ra * 16 + rc];
+        Rs[e] = xv[h] * xv[h] * scale - t;
       }
       __syncthreads();
     }
-    if (pr) prof[4L * (b - 1) + 2] = __builtin_amdgcn_s_memrealtime();
+    if (pr) prof[4L * (b - 1) + 1] = __builtin_amdgcn_s_memrealtime();
     // ---- the greedy steps on the candidates (wave 0; lane c < M holds candidate c's R row) ----
     if (w == 0) {
       const double thr = misc[0], Bv = misc[1];
@@ -1030,22 +1088,18 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
       int k = 0, stop = 0, rk = 0;
       for (;;) {
         if (j + k >= rmax) { stop = 1; rk = rmax; break; }
-        const double dv = (lane < M && !chosen) ? d : -1e300;
-        const int dr = (lane < M && !chosen) ? myrow : 0x7fffffff;
-        double mv = -1e300;
-        int mi = 0x7fffffff, pc = -1;
-#pragma unroll
-        for (int c = 0; c < M; ++c) {
-          const double vc = sb_readlane_d(dv, c);
-          const int ic = __builtin_amdgcn_readlane(dr, c);
-          if (sc_better(vc, ic, mv, mi)) { mv = vc; mi = ic; pc = c; }
-        }
+        if (k == S) break;  // the owners' MFMA block holds S pivots: next batch
+        double mv = (lane < M && !chosen) ? d : -1e300;
+        int mi = (lane < M && !chosen) ? myrow : 0x7fffffff;
+        sb_wave_best(mv, mi);
         if (mi == 0x7fffffff) {  // every candidate chosen
           if (Brow == 0x7fffffff) { stop = 1; rk = j + k; }  // ... and no other row left
           break;
         }
         if (!sc_better(mv, mi, Bv, Brow)) break;  // a non-candidate could win the next step
         if (!(mv > thr)) { stop = 1; rk = j + k; break; }  // the global max is below dpstrf's tol
+        const int pc = __builtin_amdgcn_readfirstlane(
+            __ffsll((long long)__ballot(lane < M && myrow == mi)) - 1);
         const double sq = sqrt(mv), inv = 1.0 / sq;
         double rp = 0.0;
 #pragma unroll
@@ -1053,25 +1107,31 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
         double l = 0.0;
         if (lane < M) {
           l = lane == pc ? sq : (chosen ? 0.0 : rp * inv);
-          Ldn[lane * M + k] = l;
+          Ldn[lane * S + k] = l;
+          Lb[lane] = l;
         }
         if (lane == 0) {
           pidx[k] = pc;
           dpv[k] = mv;
           piv[j + k] = mi;
         }
-        // rank-1 update of the candidates' residual block
+        __builtin_amdgcn_wave_barrier();
+        // rank-1 update of the candidates' residual block (every lane reads the column)
         const bool upd = lane < M && !chosen && lane != pc;
 #pragma unroll
-        for (int c = 0; c < M; ++c) {
-          const double lc = sb_readlane_d(l, c);
-          if (upd) Rr[c] -= l * lc;
+        for (int c = 0; c < M; c += 2) {
+          const double2 lc = *(const double2*)(Lb + c);
+          if (upd) {
+            Rr[c] -= l * lc.x;
+            Rr[c + 1] -= l * lc.y;
+          }
         }
         if (upd) d -= l * l;
         if (lane == pc) {
           chosen = true;
           d = -1e300;
         }
+        __builtin_amdgcn_wave_barrier();
         ++k;
       }
       if (k == 0 && !stop) {  // cannot happen (the top candidate beats B); never spin on it
@@ -1079,7 +1139,7 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
         rk = j;
         if (lane == 0) atomicExch(err, 1);
       }
-      if (lane < M) misc[3 + lane] = d;
+      if (lane < M) dn[lane] = d;
       if (lane == 0) {
         st[0] = k;
         st[1] = stop;
@@ -1088,24 +1148,29 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
       }
     }
     __syncthreads();
-    // ---- publish: one granule per thread (header included; readers re-read stale ones) ----
+    if (pr) prof[4L * (b - 1) + 2] = __builtin_amdgcn_s_memrealtime();
+    // ---- publish: the granules, header included (readers re-read stale ones) ----
     const int s = st[0], stop = st[1];
-    if (tid == 0) {
-      u32x4 h;
-      h.x = (unsigned)s;
-      h.y = (unsigned)stop;
-      h.z = (unsigned)st[2];
-      h.w = b;
-      sc_store_rec(pub, h);
-    } else if (tid < 1 + M) {
-      const int c = tid - 1;
-      sc_store_rec(pub + tid, sb_gran(misc[3 + c], (unsigned)cand[c], b));
-    } else if (tid < 1 + 2 * M) {
-      const int k = tid - 1 - M;
-      sc_store_rec(pub + tid, sb_gran(k < s ? dpv[k] : 1.0, k < s ? (unsigned)pidx[k] : 0u, b));
-    } else if (tid < SB_NPUB) {
-      const int e = tid - 1 - 2 * M;
-      sc_store_rec(pub + tid, sb_gran((e % M) < s ? Ldn[e] : 0.0, (unsigned)e, b));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = tid + h * SB_THREADS;
+      if (e >= SB_NPUB) break;
+      u32x4 gr;
+      if (e == 0) {
+        gr.x = (unsigned)s;
+        gr.y = (unsigned)stop;
+        gr.z = (unsigned)st[2];
+        gr.w = b;
+      } else if (e < 1 + M) {
+        gr = sb_gran(dn[e - 1], (unsigned)cand[e - 1], b);
+      } else if (e < 1 + M + S) {
+        const int k = e - 1 - M;
+        gr = sb_gran(k < s ? dpv[k] : 1.0, k < s ? (unsigned)pidx[k] : 0u, b);
+      } else {
+        const int q = e - 1 - M - S;
+        gr = sb_gran((q % S) < s ? Ldn[q] : 0.0, (unsigned)q, b);
+      }
+      sc_store_rec(pub + e, gr);
     }
     if (pr) prof[4L * (b - 1) + 3] = __builtin_amdgcn_s_memrealtime();
     j += s;
@@ -1473,7 +1538,7 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
                               const int** err_dev) {
   *handled = false;
   *err_dev = nullptr;
-  if (n < 2 * SB_M || n > SB_GR * SB_THREADS || rmax > 4 * 8 * SB_KPW) return 0;
+  if (n < 2 * SB_M || n > SB_GR * SB_THREADS || rmax > 4096) return 0;
   static const int ncu = [] {
     int dev = 0, v = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -1485,8 +1550,8 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
   const int G = (n + RW - 1) / RW;
   if (G + 1 > ncu) return 0;
   constexpr size_t kLds = 150 * 1024;
-  const size_t owner = sizeof(double) * (8 * 256 + 3 * 256 + (size_t)RW * rmax);
-  const size_t leader = sizeof(double) * (8 * 256 + 2 * SB_LIST + 2 * SB_THREADS + 2 * 256 + 64);
+  const size_t owner = sizeof(double) * (8 * 256 + SB_M * SB_S + 2 * 16 * SB_S + (size_t)RW * rmax);
+  const size_t leader = sizeof(double) * (3 * 8 * 256 + SB_M * SB_M + 64 + SB_M * SB_S + 16);
   const size_t lds = std::max(owner, leader);
   if (lds > kLds) return 0;
   // scratch in the caller's work area (n*n doubles): granules, publish area, global L, error flag
@@ -1542,15 +1607,15 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
       ++nb;
       if (b == 0 || !a[1] || !a[2] || !a[3]) continue;
       const unsigned long long prev = h[4 * (size_t)(b - 1) + 3];
-      ph[0] += (double)(a[0] - prev);  // published -> every row's residual gathered
-      ph[1] += (double)(a[1] - a[0]);  // candidate selection
-      ph[2] += (double)(a[2] - a[1]);  // candidates' residual block (MFMA Gram)
-      ph[3] += (double)(a[3] - a[2]);  // greedy steps + publish
+      ph[0] += (double)(a[0] - prev);  // published -> owners' update, gather, candidates
+      ph[1] += (double)(a[1] - a[0]);  // candidates' residual block (MFMA Gram)
+      ph[2] += (double)(a[2] - a[1]);  // greedy steps
+      ph[3] += (double)(a[3] - a[2]);  // publish
       ++cnt;
     }
     if (cnt)  // s_memrealtime: 100 MHz
-      fprintf(stderr, "select batch G=%d RW=%d: %d batches, per batch (us) owners+gather %.2f, "
-                      "select %.2f, gram %.2f, steps+publish %.2f\n",
+      fprintf(stderr, "select batch G=%d RW=%d: %d batches, per batch (us) owners+gather+select "
+                      "%.2f, gram %.2f, steps %.2f, publish %.2f\n",
               G, RW, nb, ph[0] / cnt / 100.0, ph[1] / cnt / 100.0, ph[2] / cnt / 100.0,
               ph[3] / cnt / 100.0);
   }
