@@ -683,17 +683,18 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
 //  * the leader publishes the batch (pivots, their d, the candidates' new L entries and
 //    residuals); each owner forms its rows' new columns with one MFMA pass against the pivot
 //    rows (acc = L[rows,:j] L[piv,:j]^T) plus the in-batch triangular part, and posts again.
-// Simulated on the C3 parent grid (n 3375, 600 pivots): 99 batches of 32 per-wave candidates
-// (100 with the exact top 16, 165 with 2 per wave).  Hand-offs: every handed-off byte is stored
+// Simulated on the C3 parent grid (n 3375, 600 pivots): 63 batches of 64 per-wave candidates
+// (99 with 32, 45 with 128; the exact top 16 / 32 / 64: 100 / 69 / 48).  Hand-offs: every handed-off byte is stored
 // sc1 (write-through) and loaded sc1; the owners' L stores wait (vmcnt) behind a barrier before
 // their next post; the published granules carry their batch and a stale one is re-read.  Every
 // wait is bounded: a stalled wait sets *err and the grid drains (the caller then falls back).
 constexpr int SB_THREADS = 512;
-constexpr int SB_TW = 4;                    // candidates per leader wave
+constexpr int SB_TW = 8;                    // candidates per leader wave
 constexpr int SB_M = 8 * SB_TW;             // candidates per batch
 constexpr int SB_S = 16;                    // pivots per batch at most (one MFMA N block)
 constexpr int SB_GR = 8;                    // granules per leader thread: n <= 8 * 512
-constexpr int SB_KCH = 20;                  // K steps (4 columns) per wave and load chunk
+constexpr int SB_KCH = 20;                  // K steps (4 columns) per wave and load chunk (owners)
+constexpr int SB_GCH = 6;                   // the same for the leader's Gram (4 row groups)
 constexpr int SB_NPUB = 1 + SB_M + SB_S + SB_M * SB_S;  // granules of one publish
 constexpr long SB_SPIN = 1L << 22;
 
@@ -811,17 +812,24 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
     for (unsigned b = 1;; ++b) {
       if (tid < nr) sc_store_rec(ddg + r0 + tid, sb_gran(dd, (unsigned)(r0 + tid), b));  // post
       // the leader's publish of this batch: every granule read in one round, stale ones re-read
-      u32x4 g0 = sc_load_rec(pub + tid), g1;
-      const bool two = tid + SB_THREADS < SB_NPUB;
-      if (two) g1 = sc_load_rec(pub + tid + SB_THREADS);
-      bool ok = sb_repoll(pub + tid, b, err, &g0);
-      if (two && ok) ok = sb_repoll(pub + tid + SB_THREADS, b, err, &g1);
+      constexpr int NH = (SB_NPUB + SB_THREADS - 1) / SB_THREADS;
+      u32x4 gq[NH];
+#pragma unroll
+      for (int h = 0; h < NH; ++h) gq[h] = sc_load_rec(pub + min(tid + h * SB_THREADS, SB_NPUB - 1));
+      bool ok = true;
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+        if (ok && tid + h * SB_THREADS < SB_NPUB && gq[h].w != b) {
+          u32x4 g = sc_load_rec(pub + tid + h * SB_THREADS);
+          ok = sb_repoll(pub + tid + h * SB_THREADS, b, err, &g);
+          gq[h] = g;
+        }
       if (!ok) s_bad = 1;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < NH; ++h) {
         const int e = tid + h * SB_THREADS;
-        if (h == 1 && !two) break;
-        const u32x4 g = h ? g1 : g0;
+        if (e >= SB_NPUB) break;
+        const u32x4 g = gq[h];
         const double v = sb_dbl(g);
         if (e == 0) {
           hdr[0] = (int)g.x;
@@ -921,9 +929,9 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
     }
   }
   // ======================= leader =======================
-  double* Rs = red + 3 * 8 * 256;   // M x M candidates' residual block
-  double* Lb = Rs + M * M;          // the step's column, broadcast through LDS
-  double* Ldn = Lb + 64;            // [c][k] the batch's columns of the candidates
+  double* Rs = red + M * M;         // M x M candidates' residual block (red: Gram scratch)
+  double* Lb = Rs + M * M;          // candidates' current residual, the step's column
+  double* Ldn = Lb + 2 * M;         // [c][k] the batch's columns of the candidates
   double* wbv = Ldn + M * S;        // per-wave bound (value, row)
   int* wbi = (int*)(wbv + 8);
   int* cand = s_i;                  // candidates (rows; -1 none)
@@ -1017,142 +1025,165 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
         misc[0] = tol > 0 ? tol * mx : (double)n * 2.220446049250313e-16 * mx;
       }
     }
-    // ---- R = x4[C,C] - L[C,:j] L[C,:j]^T (FP64 MFMA: blocks 00, 01, 11; K over the waves) ----
+    // ---- R = x4[C,C] - L[C,:j] L[C,:j]^T: FP64 MFMA on the 10 16 x 16 blocks of the upper
+    // triangle, K split over the 8 waves, the partials added into R in wave order (deterministic) ----
     {
       const int nks = (j + 3) >> 2;
-      const int c0r = cand[i16], c1r = cand[16 + i16];
-      const double* l0 = Lg + (long)max(c0r, 0) * rmax;
-      const double* l1 = Lg + (long)max(c1r, 0) * rmax;
-      double xv[2] = {0.0, 0.0};
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int e = tid + h * SB_THREADS, a = e >> 5, c = e & 31;
-        if (cand[a] >= 0 && cand[c] >= 0) xv[h] = X2[(long)cand[a] * n + cand[c]].x;
-      }
-      f64x4 D00 = {0, 0, 0, 0}, D01 = {0, 0, 0, 0}, D11 = {0, 0, 0, 0};
-      for (int k0 = 0; k0 < nks; k0 += 8 * SB_KCH) {
-        double a0[SB_KCH], a1[SB_KCH];
-#pragma unroll
-        for (int u = 0; u < SB_KCH; ++u) {
-          const int ks = k0 + w + 8 * u, l = ks * 4 + kq;
-          a0[u] = 0.0;
-          a1[u] = 0.0;
-          if (ks < nks) {
-            const double t0 = sb_ld_d(l0 + min(l, j - 1)), t1 = sb_ld_d(l1 + min(l, j - 1));
-            a0[u] = (c0r >= 0 && l < j) ? t0 : 0.0;
-            a1[u] = (c1r >= 0 && l < j) ? t1 : 0.0;
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < SB_KCH; ++u) {
-          if (k0 + w + 8 * u < nks) {  // wave-uniform
-            D00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], a0[u], D00, 0, 0, 0);
-            D01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], a1[u], D01, 0, 0, 0);
-            D11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[u], a1[u], D11, 0, 0, 0);
-          }
-        }
-      }
+      const double* lrow[4];
+      bool lok[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int o = (kq + 4 * r) * 16 + i16;
-        red[(0 * 8 + w) * 256 + o] = D00[r];
-        red[(1 * 8 + w) * 256 + o] = D01[r];
-        red[(2 * 8 + w) * 256 + o] = D11[r];
+        const int cr = cand[16 * r + i16];
+        lrow[r] = Lg + (long)max(cr, 0) * rmax;
+        lok[r] = cr >= 0;
+      }
+      f64x4 D[10];
+#pragma unroll
+      for (int q = 0; q < 10; ++q) D[q] = f64x4{0, 0, 0, 0};
+      for (int k0 = 0; k0 < nks; k0 += 8 * SB_GCH) {
+        double a[4][SB_GCH];
+#pragma unroll
+        for (int u = 0; u < SB_GCH; ++u) {
+          const int ks = k0 + w + 8 * u, l = ks * 4 + kq;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            a[r][u] = 0.0;
+            if (ks < nks) {
+              const double t = sb_ld_d(lrow[r] + min(l, j - 1));
+              a[r][u] = (lok[r] && l < j) ? t : 0.0;
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < SB_GCH; ++u) {
+          if (k0 + w + 8 * u < nks) {  // wave-uniform
+            int q = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int c = r; c < 4; ++c, ++q)
+                D[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[r][u], a[c][u], D[q], 0, 0, 0);
+          }
+        }
+      }
+      for (int wv = 0; wv < 8; ++wv) {
+        if (w == wv) {
+          int q = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = r; c < 4; ++c, ++q)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int o = (16 * r + kq + 4 * e) * M + 16 * c + i16;
+                Rs[o] = (wv == 0 ? 0.0 : Rs[o]) + D[q][e];
+              }
+        }
+        __syncthreads();
+      }
+      // R = x4 - Gram, the lower triangle mirrored from the upper
+      for (int e = tid; e < M * M; e += SB_THREADS) {
+        const int a = e / M, c = e % M;
+        const int lo = a < c ? a : c, hi = a < c ? c : a;
+        const bool up = (lo >> 4) <= (hi >> 4);
+        const double gm = Rs[(up ? lo : hi) * M + (up ? hi : lo)];
+        double x = 0.0;
+        if (cand[a] >= 0 && cand[c] >= 0) {
+          const double y = X2[(long)cand[a] * n + cand[c]].x;
+          x = y * y * scale;
+        }
+        red[e] = x - gm;  // R in the (free) partial area; copied back below
       }
       __syncthreads();
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int e = tid + h * SB_THREADS, a = e >> 5, c = e & 31;
-        // block of (a, c): 00, 01 (a < 16 <= c), 10 = 01^T, 11
-        const int blk = (a < 16) ? (c < 16 ? 0 : 1) : (c < 16 ? 1 : 2);
-        const int ra = (a < 16 || blk == 2) ? (a & 15) : (c & 15);
-        const int rc = (a < 16 || blk == 2) ? (c & 15) : (a & 15);
-        double t = 0.0;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) t += red[(blk * 8 + q) * 256 + ra * 16 + rc];
-        Rs[e] = xv[h] * xv[h] * scale - t;
-      }
+      for (int e = tid; e < M * M; e += SB_THREADS) Rs[e] = red[e];
       __syncthreads();
     }
     if (pr) prof[4L * (b - 1) + 1] = __builtin_amdgcn_s_memrealtime();
-    // ---- the greedy steps on the candidates (wave 0; lane c < M holds candidate c's R row) ----
-    if (w == 0) {
+    // ---- the greedy steps on the candidates: the arg-max by wave 0, the column and the rank-1
+    // update of R by the whole workgroup ----
+    {
+      double* dc = Lb;                  // candidates' current residual (-1e300: chosen/none)
+      double* lcol = Lb + M;            // the step's column l_c
+      int* ctl = st + 4;                // pc, go
+      if (tid < M) dc[tid] = cand[tid] >= 0 ? cd[tid] : -1e300;
+      __syncthreads();
       const double thr = misc[0], Bv = misc[1];
       const int Brow = st[3];
-      const int myrow = lane < M ? cand[lane] : -1;
-      double d = lane < M ? cd[lane] : -1e300;
-      bool chosen = myrow < 0;
-      double Rr[M];
-#pragma unroll
-      for (int c = 0; c < M; ++c) Rr[c] = lane < M ? Rs[lane * M + c] : 0.0;
       int k = 0, stop = 0, rk = 0;
       for (;;) {
-        if (j + k >= rmax) { stop = 1; rk = rmax; break; }
-        if (k == S) break;  // the owners' MFMA block holds S pivots: next batch
-        double mv = (lane < M && !chosen) ? d : -1e300;
-        int mi = (lane < M && !chosen) ? myrow : 0x7fffffff;
-        sb_wave_best(mv, mi);
-        if (mi == 0x7fffffff) {  // every candidate chosen
-          if (Brow == 0x7fffffff) { stop = 1; rk = j + k; }  // ... and no other row left
-          break;
-        }
-        if (!sc_better(mv, mi, Bv, Brow)) break;  // a non-candidate could win the next step
-        if (!(mv > thr)) { stop = 1; rk = j + k; break; }  // the global max is below dpstrf's tol
-        const int pc = __builtin_amdgcn_readfirstlane(
-            __ffsll((long long)__ballot(lane < M && myrow == mi)) - 1);
-        const double sq = sqrt(mv), inv = 1.0 / sq;
-        double rp = 0.0;
-#pragma unroll
-        for (int c = 0; c < M; ++c) rp = c == pc ? Rr[c] : rp;
-        double l = 0.0;
-        if (lane < M) {
-          l = lane == pc ? sq : (chosen ? 0.0 : rp * inv);
-          Ldn[lane * S + k] = l;
-          Lb[lane] = l;
-        }
-        if (lane == 0) {
-          pidx[k] = pc;
-          dpv[k] = mv;
-          piv[j + k] = mi;
-        }
-        __builtin_amdgcn_wave_barrier();
-        // rank-1 update of the candidates' residual block (every lane reads the column)
-        const bool upd = lane < M && !chosen && lane != pc;
-#pragma unroll
-        for (int c = 0; c < M; c += 2) {
-          const double2 lc = *(const double2*)(Lb + c);
-          if (upd) {
-            Rr[c] -= l * lc.x;
-            Rr[c + 1] -= l * lc.y;
+        if (w == 0) {
+          int go = 1;
+          if (j + k >= rmax) { go = 0; stop = 1; rk = rmax; }
+          else if (k == S) { go = 0; }  // the owners' MFMA block holds S pivots: next batch
+          double mv = -1e300;
+          int mi = 0x7fffffff;
+          if (go) {
+            mv = dc[lane];
+            mi = mv > -1e299 ? cand[lane] : 0x7fffffff;
+            sb_wave_best(mv, mi);
+            if (mi == 0x7fffffff) {  // every candidate chosen
+              go = 0;
+              if (Brow == 0x7fffffff) { stop = 1; rk = j + k; }  // ... and no other row left
+            } else if (!sc_better(mv, mi, Bv, Brow)) {
+              go = 0;  // a non-candidate could win the next step
+            } else if (!(mv > thr)) {
+              go = 0;  // the global max is below dpstrf's tolerance
+              stop = 1;
+              rk = j + k;
+            }
+          }
+          int pc = -1;
+          if (go)  // go is wave-uniform: every lane takes part in the ballot
+            pc = __builtin_amdgcn_readfirstlane(
+                __ffsll((long long)__ballot(lane < M && cand[lane] == mi)) - 1);
+          if (lane == 0) {
+            ctl[1] = go;
+            if (go) {
+              ctl[0] = pc;
+              pidx[k] = pc;
+              dpv[k] = mv;
+              piv[j + k] = mi;
+            }
           }
         }
-        if (upd) d -= l * l;
-        if (lane == pc) {
-          chosen = true;
-          d = -1e300;
+        __syncthreads();
+        if (!ctl[1]) break;
+        const int pc = ctl[0];
+        const double dp = dpv[k], sq = sqrt(dp), inv = 1.0 / sq;
+        if (tid < M) {
+          const bool live = dc[tid] > -1e299;
+          const double l = tid == pc ? sq : (live ? Rs[tid * M + pc] * inv : 0.0);
+          lcol[tid] = l;
+          Ldn[tid * S + k] = l;
         }
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
+        for (int e = tid; e < M * M; e += SB_THREADS) {
+          const int a = e / M, c = e % M;
+          Rs[e] -= lcol[a] * lcol[c];
+        }
+        if (tid < M && dc[tid] > -1e299) dc[tid] = tid == pc ? -1e300 : dc[tid] - lcol[tid] * lcol[tid];
+        __syncthreads();
         ++k;
       }
-      if (k == 0 && !stop) {  // cannot happen (the top candidate beats B); never spin on it
-        stop = 1;
-        rk = j;
-        if (lane == 0) atomicExch(err, 1);
-      }
-      if (lane < M) dn[lane] = d;
-      if (lane == 0) {
+      if (tid == 0) {
+        if (k == 0 && !stop) {  // cannot happen (the top candidate beats B); never spin on it
+          stop = 1;
+          rk = j;
+          atomicExch(err, 1);
+        }
         st[0] = k;
         st[1] = stop;
         st[2] = rk;
         if (stop) rank[0] = rk;
       }
+      if (tid < M) dn[tid] = dc[tid];
     }
     __syncthreads();
     if (pr) prof[4L * (b - 1) + 2] = __builtin_amdgcn_s_memrealtime();
     // ---- publish: the granules, header included (readers re-read stale ones) ----
     const int s = st[0], stop = st[1];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < (SB_NPUB + SB_THREADS - 1) / SB_THREADS; ++h) {
       const int e = tid + h * SB_THREADS;
       if (e >= SB_NPUB) break;
       u32x4 gr;
@@ -1551,7 +1582,7 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
   if (G + 1 > ncu) return 0;
   constexpr size_t kLds = 150 * 1024;
   const size_t owner = sizeof(double) * (8 * 256 + SB_M * SB_S + 2 * 16 * SB_S + (size_t)RW * rmax);
-  const size_t leader = sizeof(double) * (3 * 8 * 256 + SB_M * SB_M + 64 + SB_M * SB_S + 16);
+  const size_t leader = sizeof(double) * (2 * SB_M * SB_M + 2 * SB_M + SB_M * SB_S + 16);
   const size_t lds = std::max(owner, leader);
   if (lds > kLds) return 0;
   // scratch in the caller's work area (n*n doubles): granules, publish area, global L, error flag
