@@ -726,7 +726,7 @@ __device__ __forceinline__ double sb_ld_d(const double* a) {
 // re-read a granule until its batch word is `tag`; false on a stall or another workgroup's error
 __device__ __forceinline__ bool sb_repoll(const u32x4* gp, unsigned tag, int* err, u32x4* g) {
   for (long spins = 0; g->w != tag; ++spins) {
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(2);
     if (spins > SB_SPIN ||
         ((spins & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
       atomicExch(err, 1);
@@ -811,7 +811,15 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
     int j = 0;
     for (unsigned b = 1;; ++b) {
       if (tid < nr) sc_store_rec(ddg + r0 + tid, sb_gran(dd, (unsigned)(r0 + tid), b));  // post
-      // the leader's publish of this batch: every granule read in one round, stale ones re-read
+      // the leader's publish of this batch: one lane waits for the header (211 pollers, not
+      // 211 x 512: polling traffic slows everybody's loads), then every granule is read in one
+      // round and a stale one re-read
+      if (tid == 0) {
+        u32x4 h = sc_load_rec(pub);
+        if (!sb_repoll(pub, b, err, &h)) s_bad = 1;
+      }
+      __syncthreads();
+      if (s_bad) return;
       constexpr int NH = (SB_NPUB + SB_THREADS - 1) / SB_THREADS;
       u32x4 gq[NH];
 #pragma unroll
