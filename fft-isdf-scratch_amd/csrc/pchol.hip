@@ -694,7 +694,7 @@ constexpr int SB_M = 8 * SB_TW;             // candidates per batch
 constexpr int SB_S = 16;                    // pivots per batch at most (one MFMA N block)
 constexpr int SB_GR = 8;                    // granules per leader thread: n <= 8 * 512
 constexpr int SB_KCH = 20;                  // K steps (4 columns) per wave and load chunk (owners)
-constexpr int SB_GCH = 6;                   // the same for the leader's Gram (4 row groups)
+constexpr int SB_GCH = 4;                   // the same for the leader's Gram (4 row groups)
 constexpr int SB_NPUB = 1 + SB_M + SB_S + SB_M * SB_S;  // granules of one publish
 constexpr long SB_SPIN = 1L << 22;
 
@@ -937,8 +937,8 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
     }
   }
   // ======================= leader =======================
-  double* Rs = red + M * M;         // M x M candidates' residual block (red: Gram scratch)
-  double* Lb = Rs + M * M;          // candidates' current residual, the step's column
+  double* Rs = red + 2 * M * M;     // M x M candidates' residual block (red: 2 M^2 Gram scratch)
+  double* Lb = Rs + M * M;          // the step's column
   double* Ldn = Lb + 2 * M;         // [c][k] the batch's columns of the candidates
   double* wbv = Ldn + M * S;        // per-wave bound (value, row)
   int* wbi = (int*)(wbv + 8);
@@ -951,7 +951,7 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
   double* misc = s_d + 2 * M + S;   // thr, Bv
   int j = 0;
   for (unsigned b = 1;; ++b) {
-    const bool pr = prof != nullptr && tid == 0 && b <= 8192;
+    const bool pr = prof != nullptr && tid == 0 && b <= 4096;  // 8 slots of 4 x 8192
     // ---- every row's residual diagonal: all loads in flight, stale granules re-read ----
     double v[SB_GR];
     int rw[SB_GR];
@@ -1019,7 +1019,7 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
     }
     __syncthreads();
     if (s_bad) return;
-    if (pr) prof[4L * (b - 1)] = __builtin_amdgcn_s_memrealtime();
+    if (pr) prof[8L * (b - 1)] = __builtin_amdgcn_s_memrealtime();
     if (tid == 0) {
       double bv = -1e300;
       int bi = 0x7fffffff;
@@ -1034,8 +1034,24 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
       }
     }
     // ---- R = x4[C,C] - L[C,:j] L[C,:j]^T: FP64 MFMA on the 10 16 x 16 blocks of the upper
-    // triangle, K split over the 8 waves, the partials added into R in wave order (deterministic) ----
+    // triangle (block q <-> row group qr[q], column group qc[q]), K split over the 8 waves; the
+    // partials are summed in a fixed order (deterministic) in 3 rounds of 4 blocks ----
     {
+      constexpr int qr[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
+      constexpr int qc[10] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
+      // the x4 entries this thread's reduction writes, loaded first (they do not depend on L)
+      double xv[6];
+#pragma unroll
+      for (int rd = 0; rd < 3; ++rd)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = tid + h * SB_THREADS, q = 4 * rd + (e >> 8), idx = e & 255;
+          xv[2 * rd + h] = 0.0;
+          if (q < 10) {
+            const int a = cand[16 * qr[q] + (idx >> 4)], c = cand[16 * qc[q] + (idx & 15)];
+            if (a >= 0 && c >= 0) xv[2 * rd + h] = X2[(long)a * n + c].x;
+          }
+        }
       const int nks = (j + 3) >> 2;
       const double* lrow[4];
       bool lok[4];
@@ -1065,129 +1081,110 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
 #pragma unroll
         for (int u = 0; u < SB_GCH; ++u) {
           if (k0 + w + 8 * u < nks) {  // wave-uniform
-            int q = 0;
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-              for (int c = r; c < 4; ++c, ++q)
-                D[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[r][u], a[c][u], D[q], 0, 0, 0);
+            for (int q = 0; q < 10; ++q)
+              D[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[qr[q]][u], a[qc[q]][u], D[q], 0, 0, 0);
           }
         }
       }
-      for (int wv = 0; wv < 8; ++wv) {
-        if (w == wv) {
-          int q = 0;
+      if (pr) prof[8L * (b - 1) + 1] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
+      for (int rd = 0; rd < 3; ++rd) {
+        // round rd: blocks 4 rd .. 4 rd + 3 into red[(bq * 8 + wave) * 256 + idx]
 #pragma unroll
-            for (int c = r; c < 4; ++c, ++q)
+        for (int bq = 0; bq < 4; ++bq) {
+          const int q = 4 * rd + bq;
+          if (q < 10) {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const int o = (16 * r + kq + 4 * e) * M + 16 * c + i16;
-                Rs[o] = (wv == 0 ? 0.0 : Rs[o]) + D[q][e];
-              }
+            for (int e = 0; e < 4; ++e) red[(bq * 8 + w) * 256 + (kq + 4 * e) * 16 + i16] = D[q][e];
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = tid + h * SB_THREADS, bq = e >> 8, idx = e & 255, q = 4 * rd + bq;
+          if (q < 10) {
+            double t = 0.0;
+#pragma unroll
+            for (int wv = 0; wv < 8; ++wv) t += red[(bq * 8 + wv) * 256 + idx];
+            const double x = xv[2 * rd + h];
+            const double v = x * x * scale - t;
+            const int a = 16 * qr[q] + (idx >> 4), c = 16 * qc[q] + (idx & 15);
+            Rs[a * M + c] = v;
+            if (qr[q] != qc[q]) Rs[c * M + a] = v;  // the lower triangle mirrored
+          }
         }
         __syncthreads();
       }
-      // R = x4 - Gram, the lower triangle mirrored from the upper
-      for (int e = tid; e < M * M; e += SB_THREADS) {
-        const int a = e / M, c = e % M;
-        const int lo = a < c ? a : c, hi = a < c ? c : a;
-        const bool up = (lo >> 4) <= (hi >> 4);
-        const double gm = Rs[(up ? lo : hi) * M + (up ? hi : lo)];
-        double x = 0.0;
-        if (cand[a] >= 0 && cand[c] >= 0) {
-          const double y = X2[(long)cand[a] * n + cand[c]].x;
-          x = y * y * scale;
-        }
-        red[e] = x - gm;  // R in the (free) partial area; copied back below
-      }
-      __syncthreads();
-      for (int e = tid; e < M * M; e += SB_THREADS) Rs[e] = red[e];
-      __syncthreads();
     }
-    if (pr) prof[4L * (b - 1) + 1] = __builtin_amdgcn_s_memrealtime();
-    // ---- the greedy steps on the candidates: the arg-max by wave 0, the column and the rank-1
-    // update of R by the whole workgroup ----
-    {
-      double* dc = Lb;                  // candidates' current residual (-1e300: chosen/none)
-      double* lcol = Lb + M;            // the step's column l_c
-      int* ctl = st + 4;                // pc, go
-      if (tid < M) dc[tid] = cand[tid] >= 0 ? cd[tid] : -1e300;
-      __syncthreads();
+    if (pr) prof[8L * (b - 1) + 2] = __builtin_amdgcn_s_memrealtime();
+    if (pr) prof[8L * (b - 1) + 3] = __builtin_amdgcn_s_memrealtime();
+    if (pr) prof[8L * (b - 1) + 4] = __builtin_amdgcn_s_memrealtime();
+    // ---- the greedy steps on the candidates: wave 0, lane c updates candidate c's row of R
+    // (LDS); the step's column is broadcast through LDS ----
+    if (w == 0) {
       const double thr = misc[0], Bv = misc[1];
       const int Brow = st[3];
+      const int myrow = cand[lane];
+      double d = myrow >= 0 ? cd[lane] : -1e300;
+      double* Rr = Rs + lane * M;
       int k = 0, stop = 0, rk = 0;
       for (;;) {
-        if (w == 0) {
-          int go = 1;
-          if (j + k >= rmax) { go = 0; stop = 1; rk = rmax; }
-          else if (k == S) { go = 0; }  // the owners' MFMA block holds S pivots: next batch
-          double mv = -1e300;
-          int mi = 0x7fffffff;
-          if (go) {
-            mv = dc[lane];
-            mi = mv > -1e299 ? cand[lane] : 0x7fffffff;
-            sb_wave_best(mv, mi);
-            if (mi == 0x7fffffff) {  // every candidate chosen
-              go = 0;
-              if (Brow == 0x7fffffff) { stop = 1; rk = j + k; }  // ... and no other row left
-            } else if (!sc_better(mv, mi, Bv, Brow)) {
-              go = 0;  // a non-candidate could win the next step
-            } else if (!(mv > thr)) {
-              go = 0;  // the global max is below dpstrf's tolerance
-              stop = 1;
-              rk = j + k;
-            }
+        if (j + k >= rmax) { stop = 1; rk = rmax; break; }
+        if (k == S) break;  // the owners' MFMA block holds S pivots: next batch
+        const bool live = d > -1e299;
+        double mv = live ? d : -1e300;
+        int mi = live ? myrow : 0x7fffffff;
+        sb_wave_best(mv, mi);
+        if (mi == 0x7fffffff) {  // every candidate chosen
+          if (Brow == 0x7fffffff) { stop = 1; rk = j + k; }  // ... and no other row left
+          break;
+        }
+        if (!sc_better(mv, mi, Bv, Brow)) break;  // a non-candidate could win the next step
+        if (!(mv > thr)) { stop = 1; rk = j + k; break; }  // the global max is below dpstrf's tol
+        const int pc = __builtin_amdgcn_readfirstlane(
+            __ffsll((long long)__ballot(myrow == mi)) - 1);
+        const double sq = sqrt(mv), inv = 1.0 / sq;
+        const double rp = Rr[pc];
+        const double l = lane == pc ? sq : (live ? rp * inv : 0.0);
+        Ldn[lane * S + k] = l;
+        Lb[lane] = l;
+        if (lane == 0) {
+          pidx[k] = pc;
+          dpv[k] = mv;
+          piv[j + k] = mi;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const bool upd = live && lane != pc;
+        if (upd) {
+#pragma unroll 8
+          for (int c = 0; c < M; c += 2) {
+            const double2 lc = *(const double2*)(Lb + c);
+            double2 r = *(double2*)(Rr + c);
+            r.x -= l * lc.x;
+            r.y -= l * lc.y;
+            *(double2*)(Rr + c) = r;
           }
-          int pc = -1;
-          if (go)  // go is wave-uniform: every lane takes part in the ballot
-            pc = __builtin_amdgcn_readfirstlane(
-                __ffsll((long long)__ballot(lane < M && cand[lane] == mi)) - 1);
-          if (lane == 0) {
-            ctl[1] = go;
-            if (go) {
-              ctl[0] = pc;
-              pidx[k] = pc;
-              dpv[k] = mv;
-              piv[j + k] = mi;
-            }
-          }
         }
-        __syncthreads();
-        if (!ctl[1]) break;
-        const int pc = ctl[0];
-        const double dp = dpv[k], sq = sqrt(dp), inv = 1.0 / sq;
-        if (tid < M) {
-          const bool live = dc[tid] > -1e299;
-          const double l = tid == pc ? sq : (live ? Rs[tid * M + pc] * inv : 0.0);
-          lcol[tid] = l;
-          Ldn[tid * S + k] = l;
-        }
-        __syncthreads();
-        for (int e = tid; e < M * M; e += SB_THREADS) {
-          const int a = e / M, c = e % M;
-          Rs[e] -= lcol[a] * lcol[c];
-        }
-        if (tid < M && dc[tid] > -1e299) dc[tid] = tid == pc ? -1e300 : dc[tid] - lcol[tid] * lcol[tid];
-        __syncthreads();
+        d = lane == pc ? -1e300 : (upd ? d - l * l : d);
+        __builtin_amdgcn_wave_barrier();
         ++k;
       }
-      if (tid == 0) {
-        if (k == 0 && !stop) {  // cannot happen (the top candidate beats B); never spin on it
-          stop = 1;
-          rk = j;
-          atomicExch(err, 1);
-        }
+      if (k == 0 && !stop) {  // cannot happen (the top candidate beats B); never spin on it
+        stop = 1;
+        rk = j;
+        if (lane == 0) atomicExch(err, 1);
+      }
+      dn[lane] = d;
+      if (lane == 0) {
         st[0] = k;
         st[1] = stop;
         st[2] = rk;
         if (stop) rank[0] = rk;
       }
-      if (tid < M) dn[tid] = dc[tid];
     }
     __syncthreads();
-    if (pr) prof[4L * (b - 1) + 2] = __builtin_amdgcn_s_memrealtime();
+    if (pr) prof[8L * (b - 1) + 5] = __builtin_amdgcn_s_memrealtime();
     // ---- publish: the granules, header included (readers re-read stale ones) ----
     const int s = st[0], stop = st[1];
 #pragma unroll
@@ -1211,7 +1208,7 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
       }
       sc_store_rec(pub + e, gr);
     }
-    if (pr) prof[4L * (b - 1) + 3] = __builtin_amdgcn_s_memrealtime();
+    if (pr) prof[8L * (b - 1) + 6] = __builtin_amdgcn_s_memrealtime();
     j += s;
     if (stop) return;
     __syncthreads();  // the shared lists are rewritten by the next batch
@@ -1590,7 +1587,7 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
   if (G + 1 > ncu) return 0;
   constexpr size_t kLds = 150 * 1024;
   const size_t owner = sizeof(double) * (8 * 256 + SB_M * SB_S + 2 * 16 * SB_S + (size_t)RW * rmax);
-  const size_t leader = sizeof(double) * (2 * SB_M * SB_M + 2 * SB_M + SB_M * SB_S + 16);
+  const size_t leader = sizeof(double) * (3 * SB_M * SB_M + 2 * SB_M + SB_M * SB_S + 16);
   const size_t lds = std::max(owner, leader);
   if (lds > kLds) return 0;
   // scratch in the caller's work area (n*n doubles): granules, publish area, global L, error flag
@@ -1619,8 +1616,8 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
   if (want_prof && !prof[pdev])
     FISDF_HIP(hipMalloc(&prof[pdev], sizeof(unsigned long long) * 4 * kProfBatches));
   unsigned long long* profp = want_prof ? prof[pdev] : nullptr;
-  const int nb_cap = std::min(rmax, kProfBatches);
-  if (profp) FISDF_HIP(hipMemsetAsync(profp, 0, sizeof(unsigned long long) * 4 * nb_cap, s));
+  const int nb_cap = std::min(rmax, kProfBatches / 2);
+  if (profp) FISDF_HIP(hipMemsetAsync(profp, 0, sizeof(unsigned long long) * 8 * nb_cap, s));
   int rw = RW;
   void* args[] = {(void*)&X2,  (void*)&scale, (void*)&n,   (void*)&rmax, (void*)&tol,
                   (void*)&rw,  (void*)&piv,   (void*)&rank, (void*)&ddg, (void*)&pub,
@@ -1634,29 +1631,29 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
   *err_dev = err;
   *handled = true;
   if (profp) {
-    std::vector<unsigned long long> h(4 * (size_t)nb_cap);
+    std::vector<unsigned long long> h(8 * (size_t)nb_cap);
     FISDF_HIP(hipMemcpyAsync(h.data(), profp, sizeof(unsigned long long) * h.size(),
                              hipMemcpyDeviceToHost, s));
     FISDF_HIP(hipStreamSynchronize(s));
-    double ph[4] = {0, 0, 0, 0};
+    // leader timestamps per batch: 0 candidates chosen, 1 Gram MFMA done, 2 partials added,
+    // 3 x4 - Gram formed, 4 R ready, 5 steps done, 6 published
+    double ph[7] = {0, 0, 0, 0, 0, 0, 0};
     int cnt = 0, nb = 0;
     for (int b = 0; b < nb_cap; ++b) {
-      const unsigned long long* a = &h[4 * (size_t)b];
+      const unsigned long long* a = &h[8 * (size_t)b];
       if (!a[0]) break;
       ++nb;
-      if (b == 0 || !a[1] || !a[2] || !a[3]) continue;
-      const unsigned long long prev = h[4 * (size_t)(b - 1) + 3];
-      ph[0] += (double)(a[0] - prev);  // published -> owners' update, gather, candidates
-      ph[1] += (double)(a[1] - a[0]);  // candidates' residual block (MFMA Gram)
-      ph[2] += (double)(a[2] - a[1]);  // greedy steps
-      ph[3] += (double)(a[3] - a[2]);  // publish
+      if (b == 0 || !a[6]) continue;
+      ph[0] += (double)(a[0] - h[8 * (size_t)(b - 1) + 6]);
+      for (int q = 1; q < 7; ++q) ph[q] += (double)(a[q] - a[q - 1]);
       ++cnt;
     }
     if (cnt)  // s_memrealtime: 100 MHz
       fprintf(stderr, "select batch G=%d RW=%d: %d batches, per batch (us) owners+gather+select "
-                      "%.2f, gram %.2f, steps %.2f, publish %.2f\n",
+                      "%.2f, gram mfma %.2f, gram add %.2f, x4 %.2f, copy %.2f, steps %.2f, "
+                      "publish %.2f\n",
               G, RW, nb, ph[0] / cnt / 100.0, ph[1] / cnt / 100.0, ph[2] / cnt / 100.0,
-              ph[3] / cnt / 100.0);
+              ph[3] / cnt / 100.0, ph[4] / cnt / 100.0, ph[5] / cnt / 100.0, ph[6] / cnt / 100.0);
   }
   return 0;
 }
