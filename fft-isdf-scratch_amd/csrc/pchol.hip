@@ -683,18 +683,17 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
 //  * the leader publishes the batch (pivots, their d, the candidates' new L entries and
 //    residuals); each owner forms its rows' new columns with one MFMA pass against the pivot
 //    rows (acc = L[rows,:j] L[piv,:j]^T) plus the in-batch triangular part, and posts again.
-// Simulated on the C3 parent grid (n 3375, 600 pivots): 63 batches of 64 per-wave candidates
-// (99 with 32, 45 with 128; the exact top 16 / 32 / 64: 100 / 69 / 48).  Hand-offs: every handed-off byte is stored
+// Simulated on the C3 parent grid (n 3375, 600 pivots): 99 batches of 32 per-wave candidates
+// (100 with the exact top 16, 165 with 2 per wave).  Hand-offs: every handed-off byte is stored
 // sc1 (write-through) and loaded sc1; the owners' L stores wait (vmcnt) behind a barrier before
 // their next post; the published granules carry their batch and a stale one is re-read.  Every
 // wait is bounded: a stalled wait sets *err and the grid drains (the caller then falls back).
 constexpr int SB_THREADS = 512;
-constexpr int SB_TW = 8;                    // candidates per leader wave
+constexpr int SB_TW = 4;                    // candidates per leader wave
 constexpr int SB_M = 8 * SB_TW;             // candidates per batch
 constexpr int SB_S = 16;                    // pivots per batch at most (one MFMA N block)
 constexpr int SB_GR = 8;                    // granules per leader thread: n <= 8 * 512
-constexpr int SB_KCH = 20;                  // K steps (4 columns) per wave and load chunk (owners)
-constexpr int SB_GCH = 4;                   // the same for the leader's Gram (4 row groups)
+constexpr int SB_KCH = 20;                  // K steps (4 columns) per wave and load chunk
 constexpr int SB_NPUB = 1 + SB_M + SB_S + SB_M * SB_S;  // granules of one publish
 constexpr long SB_SPIN = 1L << 22;
 
@@ -820,24 +819,26 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
       }
       __syncthreads();
       if (s_bad) return;
-      constexpr int NH = (SB_NPUB + SB_THREADS - 1) / SB_THREADS;
-      u32x4 gq[NH];
-#pragma unroll
-      for (int h = 0; h < NH; ++h) gq[h] = sc_load_rec(pub + min(tid + h * SB_THREADS, SB_NPUB - 1));
+      u32x4 g0 = sc_load_rec(pub + tid), g1;
+      const bool two = tid + SB_THREADS < SB_NPUB;
+      if (two) g1 = sc_load_rec(pub + tid + SB_THREADS);
       bool ok = true;
-#pragma unroll
-      for (int h = 0; h < NH; ++h)
-        if (ok && tid + h * SB_THREADS < SB_NPUB && gq[h].w != b) {
-          u32x4 g = sc_load_rec(pub + tid + h * SB_THREADS);
-          ok = sb_repoll(pub + tid + h * SB_THREADS, b, err, &g);
-          gq[h] = g;
-        }
+      if (g0.w != b) {
+        u32x4 g = sc_load_rec(pub + tid);
+        ok = sb_repoll(pub + tid, b, err, &g);
+        g0 = g;
+      }
+      if (two && ok && g1.w != b) {
+        u32x4 g = sc_load_rec(pub + tid + SB_THREADS);
+        ok = sb_repoll(pub + tid + SB_THREADS, b, err, &g);
+        g1 = g;
+      }
       if (!ok) s_bad = 1;
 #pragma unroll
-      for (int h = 0; h < NH; ++h) {
+      for (int h = 0; h < 2; ++h) {
         const int e = tid + h * SB_THREADS;
-        if (e >= SB_NPUB) break;
-        const u32x4 g = gq[h];
+        if (h == 1 && !two) break;
+        const u32x4 g = h ? g1 : g0;
         const double v = sb_dbl(g);
         if (e == 0) {
           hdr[0] = (int)g.x;
@@ -937,9 +938,9 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
     }
   }
   // ======================= leader =======================
-  double* Rs = red + 2 * M * M;     // M x M candidates' residual block (red: 2 M^2 Gram scratch)
-  double* Lb = Rs + M * M;          // the step's column
-  double* Ldn = Lb + 2 * M;         // [c][k] the batch's columns of the candidates
+  double* Rs = red + 3 * 8 * 256;   // M x M candidates' residual block
+  double* Lb = Rs + M * M;          // the step's column, broadcast through LDS
+  double* Ldn = Lb + 64;            // [c][k] the batch's columns of the candidates
   double* wbv = Ldn + M * S;        // per-wave bound (value, row)
   int* wbi = (int*)(wbv + 8);
   int* cand = s_i;                  // candidates (rows; -1 none)
@@ -951,7 +952,7 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
   double* misc = s_d + 2 * M + S;   // thr, Bv
   int j = 0;
   for (unsigned b = 1;; ++b) {
-    const bool pr = prof != nullptr && tid == 0 && b <= 4096;  // 8 slots of 4 x 8192
+    const bool pr = prof != nullptr && tid == 0 && b <= 8192;
     // ---- every row's residual diagonal: all loads in flight, stale granules re-read ----
     double v[SB_GR];
     int rw[SB_GR];
@@ -1019,7 +1020,7 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
     }
     __syncthreads();
     if (s_bad) return;
-    if (pr) prof[8L * (b - 1)] = __builtin_amdgcn_s_memrealtime();
+    if (pr) prof[4L * (b - 1)] = __builtin_amdgcn_s_memrealtime();
     if (tid == 0) {
       double bv = -1e300;
       int bi = 0x7fffffff;
@@ -1033,108 +1034,80 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
         misc[0] = tol > 0 ? tol * mx : (double)n * 2.220446049250313e-16 * mx;
       }
     }
-    // ---- R = x4[C,C] - L[C,:j] L[C,:j]^T: FP64 MFMA on the 10 16 x 16 blocks of the upper
-    // triangle (block q <-> row group qr[q], column group qc[q]), K split over the 8 waves; the
-    // partials are summed in a fixed order (deterministic) in 3 rounds of 4 blocks ----
+    // ---- R = x4[C,C] - L[C,:j] L[C,:j]^T (FP64 MFMA: blocks 00, 01, 11; K over the waves) ----
     {
-      constexpr int qr[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
-      constexpr int qc[10] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
-      // the x4 entries this thread's reduction writes, loaded first (they do not depend on L)
-      double xv[6];
+      const int nks = (j + 3) >> 2;
+      const int c0r = cand[i16], c1r = cand[16 + i16];
+      const double* l0 = Lg + (long)max(c0r, 0) * rmax;
+      const double* l1 = Lg + (long)max(c1r, 0) * rmax;
+      double xv[2] = {0.0, 0.0};
 #pragma unroll
-      for (int rd = 0; rd < 3; ++rd)
+      for (int h = 0; h < 2; ++h) {
+        const int e = tid + h * SB_THREADS, a = e >> 5, c = e & 31;
+        if (cand[a] >= 0 && cand[c] >= 0) xv[h] = X2[(long)cand[a] * n + cand[c]].x;
+      }
+      f64x4 D00 = {0, 0, 0, 0}, D01 = {0, 0, 0, 0}, D11 = {0, 0, 0, 0};
+      for (int k0 = 0; k0 < nks; k0 += 8 * SB_KCH) {
+        double a0[SB_KCH], a1[SB_KCH];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int e = tid + h * SB_THREADS, q = 4 * rd + (e >> 8), idx = e & 255;
-          xv[2 * rd + h] = 0.0;
-          if (q < 10) {
-            const int a = cand[16 * qr[q] + (idx >> 4)], c = cand[16 * qc[q] + (idx & 15)];
-            if (a >= 0 && c >= 0) xv[2 * rd + h] = X2[(long)a * n + c].x;
+        for (int u = 0; u < SB_KCH; ++u) {
+          const int ks = k0 + w + 8 * u, l = ks * 4 + kq;
+          a0[u] = 0.0;
+          a1[u] = 0.0;
+          if (ks < nks) {
+            const double t0 = sb_ld_d(l0 + min(l, j - 1)), t1 = sb_ld_d(l1 + min(l, j - 1));
+            a0[u] = (c0r >= 0 && l < j) ? t0 : 0.0;
+            a1[u] = (c1r >= 0 && l < j) ? t1 : 0.0;
           }
         }
-      const int nks = (j + 3) >> 2;
-      const double* lrow[4];
-      bool lok[4];
+#pragma unroll
+        for (int u = 0; u < SB_KCH; ++u) {
+          if (k0 + w + 8 * u < nks) {  // wave-uniform
+            D00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], a0[u], D00, 0, 0, 0);
+            D01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], a1[u], D01, 0, 0, 0);
+            D11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[u], a1[u], D11, 0, 0, 0);
+          }
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int cr = cand[16 * r + i16];
-        lrow[r] = Lg + (long)max(cr, 0) * rmax;
-        lok[r] = cr >= 0;
+        const int o = (kq + 4 * r) * 16 + i16;
+        red[(0 * 8 + w) * 256 + o] = D00[r];
+        red[(1 * 8 + w) * 256 + o] = D01[r];
+        red[(2 * 8 + w) * 256 + o] = D11[r];
       }
-      f64x4 D[10];
+      __syncthreads();
 #pragma unroll
-      for (int q = 0; q < 10; ++q) D[q] = f64x4{0, 0, 0, 0};
-      for (int k0 = 0; k0 < nks; k0 += 8 * SB_GCH) {
-        double a[4][SB_GCH];
+      for (int h = 0; h < 2; ++h) {
+        const int e = tid + h * SB_THREADS, a = e >> 5, c = e & 31;
+        // block of (a, c): 00, 01 (a < 16 <= c), 10 = 01^T, 11
+        const int blk = (a < 16) ? (c < 16 ? 0 : 1) : (c < 16 ? 1 : 2);
+        const int ra = (a < 16 || blk == 2) ? (a & 15) : (c & 15);
+        const int rc = (a < 16 || blk == 2) ? (c & 15) : (a & 15);
+        double t = 0.0;
 #pragma unroll
-        for (int u = 0; u < SB_GCH; ++u) {
-          const int ks = k0 + w + 8 * u, l = ks * 4 + kq;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            a[r][u] = 0.0;
-            if (ks < nks) {
-              const double t = sb_ld_d(lrow[r] + min(l, j - 1));
-              a[r][u] = (lok[r] && l < j) ? t : 0.0;
-            }
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < SB_GCH; ++u) {
-          if (k0 + w + 8 * u < nks) {  // wave-uniform
-#pragma unroll
-            for (int q = 0; q < 10; ++q)
-              D[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[qr[q]][u], a[qc[q]][u], D[q], 0, 0, 0);
-          }
-        }
+        for (int q = 0; q < 8; ++q) t += red[(blk * 8 + q) * 256 + ra * 16 + rc];
+        Rs[e] = xv[h] * xv[h] * scale - t;
       }
-      if (pr) prof[8L * (b - 1) + 1] = __builtin_amdgcn_s_memrealtime();
-#pragma unroll
-      for (int rd = 0; rd < 3; ++rd) {
-        // round rd: blocks 4 rd .. 4 rd + 3 into red[(bq * 8 + wave) * 256 + idx]
-#pragma unroll
-        for (int bq = 0; bq < 4; ++bq) {
-          const int q = 4 * rd + bq;
-          if (q < 10) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) red[(bq * 8 + w) * 256 + (kq + 4 * e) * 16 + i16] = D[q][e];
-          }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int e = tid + h * SB_THREADS, bq = e >> 8, idx = e & 255, q = 4 * rd + bq;
-          if (q < 10) {
-            double t = 0.0;
-#pragma unroll
-            for (int wv = 0; wv < 8; ++wv) t += red[(bq * 8 + wv) * 256 + idx];
-            const double x = xv[2 * rd + h];
-            const double v = x * x * scale - t;
-            const int a = 16 * qr[q] + (idx >> 4), c = 16 * qc[q] + (idx & 15);
-            Rs[a * M + c] = v;
-            if (qr[q] != qc[q]) Rs[c * M + a] = v;  // the lower triangle mirrored
-          }
-        }
-        __syncthreads();
-      }
+      __syncthreads();
     }
-    if (pr) prof[8L * (b - 1) + 2] = __builtin_amdgcn_s_memrealtime();
-    if (pr) prof[8L * (b - 1) + 3] = __builtin_amdgcn_s_memrealtime();
-    if (pr) prof[8L * (b - 1) + 4] = __builtin_amdgcn_s_memrealtime();
-    // ---- the greedy steps on the candidates: wave 0, lane c updates candidate c's row of R
-    // (LDS); the step's column is broadcast through LDS ----
+    if (pr) prof[4L * (b - 1) + 1] = __builtin_amdgcn_s_memrealtime();
+    // ---- the greedy steps on the candidates (wave 0; lane c < M holds candidate c's R row) ----
     if (w == 0) {
       const double thr = misc[0], Bv = misc[1];
       const int Brow = st[3];
-      const int myrow = cand[lane];
-      double d = myrow >= 0 ? cd[lane] : -1e300;
-      double* Rr = Rs + lane * M;
+      const int myrow = lane < M ? cand[lane] : -1;
+      double d = lane < M ? cd[lane] : -1e300;
+      bool chosen = myrow < 0;
+      double Rr[M];
+#pragma unroll
+      for (int c = 0; c < M; ++c) Rr[c] = lane < M ? Rs[lane * M + c] : 0.0;
       int k = 0, stop = 0, rk = 0;
       for (;;) {
         if (j + k >= rmax) { stop = 1; rk = rmax; break; }
         if (k == S) break;  // the owners' MFMA block holds S pivots: next batch
-        const bool live = d > -1e299;
-        double mv = live ? d : -1e300;
-        int mi = live ? myrow : 0x7fffffff;
+        double mv = (lane < M && !chosen) ? d : -1e300;
+        int mi = (lane < M && !chosen) ? myrow : 0x7fffffff;
         sb_wave_best(mv, mi);
         if (mi == 0x7fffffff) {  // every candidate chosen
           if (Brow == 0x7fffffff) { stop = 1; rk = j + k; }  // ... and no other row left
@@ -1143,30 +1116,38 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
         if (!sc_better(mv, mi, Bv, Brow)) break;  // a non-candidate could win the next step
         if (!(mv > thr)) { stop = 1; rk = j + k; break; }  // the global max is below dpstrf's tol
         const int pc = __builtin_amdgcn_readfirstlane(
-            __ffsll((long long)__ballot(myrow == mi)) - 1);
+            __ffsll((long long)__ballot(lane < M && myrow == mi)) - 1);
         const double sq = sqrt(mv), inv = 1.0 / sq;
-        const double rp = Rr[pc];
-        const double l = lane == pc ? sq : (live ? rp * inv : 0.0);
-        Ldn[lane * S + k] = l;
-        Lb[lane] = l;
+        double rp = 0.0;
+#pragma unroll
+        for (int c = 0; c < M; ++c) rp = c == pc ? Rr[c] : rp;
+        double l = 0.0;
+        if (lane < M) {
+          l = lane == pc ? sq : (chosen ? 0.0 : rp * inv);
+          Ldn[lane * S + k] = l;
+          Lb[lane] = l;
+        }
         if (lane == 0) {
           pidx[k] = pc;
           dpv[k] = mv;
           piv[j + k] = mi;
         }
         __builtin_amdgcn_wave_barrier();
-        const bool upd = live && lane != pc;
-        if (upd) {
-#pragma unroll 8
-          for (int c = 0; c < M; c += 2) {
-            const double2 lc = *(const double2*)(Lb + c);
-            double2 r = *(double2*)(Rr + c);
-            r.x -= l * lc.x;
-            r.y -= l * lc.y;
-            *(double2*)(Rr + c) = r;
+        // rank-1 update of the candidates' residual block (every lane reads the column)
+        const bool upd = lane < M && !chosen && lane != pc;
+#pragma unroll
+        for (int c = 0; c < M; c += 2) {
+          const double2 lc = *(const double2*)(Lb + c);
+          if (upd) {
+            Rr[c] -= l * lc.x;
+            Rr[c + 1] -= l * lc.y;
           }
         }
-        d = lane == pc ? -1e300 : (upd ? d - l * l : d);
+        if (upd) d -= l * l;
+        if (lane == pc) {
+          chosen = true;
+          d = -1e300;
+        }
         __builtin_amdgcn_wave_barrier();
         ++k;
       }
@@ -1175,7 +1156,7 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
         rk = j;
         if (lane == 0) atomicExch(err, 1);
       }
-      dn[lane] = d;
+      if (lane < M) dn[lane] = d;
       if (lane == 0) {
         st[0] = k;
         st[1] = stop;
@@ -1184,11 +1165,11 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
       }
     }
     __syncthreads();
-    if (pr) prof[8L * (b - 1) + 5] = __builtin_amdgcn_s_memrealtime();
+    if (pr) prof[4L * (b - 1) + 2] = __builtin_amdgcn_s_memrealtime();
     // ---- publish: the granules, header included (readers re-read stale ones) ----
     const int s = st[0], stop = st[1];
 #pragma unroll
-    for (int h = 0; h < (SB_NPUB + SB_THREADS - 1) / SB_THREADS; ++h) {
+    for (int h = 0; h < 2; ++h) {
       const int e = tid + h * SB_THREADS;
       if (e >= SB_NPUB) break;
       u32x4 gr;
@@ -1208,7 +1189,7 @@ __global__ __launch_bounds__(SB_THREADS) void pchol_select_batch(
       }
       sc_store_rec(pub + e, gr);
     }
-    if (pr) prof[8L * (b - 1) + 6] = __builtin_amdgcn_s_memrealtime();
+    if (pr) prof[4L * (b - 1) + 3] = __builtin_amdgcn_s_memrealtime();
     j += s;
     if (stop) return;
     __syncthreads();  // the shared lists are rewritten by the next batch
@@ -1555,13 +1536,15 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
   return 0;
 }
 
-// FISDF_SEL_MODE (read per call: the GPU tests compare the paths): "batch" (default) tries the
+// FISDF_SEL_MODE (read per call: the GPU tests compare the paths): "batch" tries the
 // batched-candidate kernel, then the cooperative one; "coop" starts at the cooperative kernel;
-// "blocked" (or FISDF_SEL_COOP=0) runs the blocked single-CU path only
-int select_mode() {
+// "blocked" (or FISDF_SEL_COOP=0) runs the blocked single-CU path only.  Default: batch from
+// 800 pivots on (C4, 1000 pivots: 5.3 vs 6.4 ms), coop below (C3, 600: 4.36 vs 4.41 ms, a tie;
+// profiles/r05/selection/README.txt)
+int select_mode(int rmax) {
   const char* e = getenv("FISDF_SEL_MODE");
   if (!select_coop_enabled()) return 2;
-  if (!e) return 0;
+  if (!e) return rmax >= 800 ? 0 : 1;
   if (!strcmp(e, "coop")) return 1;
   if (!strcmp(e, "blocked")) return 2;
   return 0;
@@ -1587,7 +1570,7 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
   if (G + 1 > ncu) return 0;
   constexpr size_t kLds = 150 * 1024;
   const size_t owner = sizeof(double) * (8 * 256 + SB_M * SB_S + 2 * 16 * SB_S + (size_t)RW * rmax);
-  const size_t leader = sizeof(double) * (3 * SB_M * SB_M + 2 * SB_M + SB_M * SB_S + 16);
+  const size_t leader = sizeof(double) * (3 * 8 * 256 + SB_M * SB_M + 64 + SB_M * SB_S + 16);
   const size_t lds = std::max(owner, leader);
   if (lds > kLds) return 0;
   // scratch in the caller's work area (n*n doubles): granules, publish area, global L, error flag
@@ -1616,8 +1599,8 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
   if (want_prof && !prof[pdev])
     FISDF_HIP(hipMalloc(&prof[pdev], sizeof(unsigned long long) * 4 * kProfBatches));
   unsigned long long* profp = want_prof ? prof[pdev] : nullptr;
-  const int nb_cap = std::min(rmax, kProfBatches / 2);
-  if (profp) FISDF_HIP(hipMemsetAsync(profp, 0, sizeof(unsigned long long) * 8 * nb_cap, s));
+  const int nb_cap = std::min(rmax, kProfBatches);
+  if (profp) FISDF_HIP(hipMemsetAsync(profp, 0, sizeof(unsigned long long) * 4 * nb_cap, s));
   int rw = RW;
   void* args[] = {(void*)&X2,  (void*)&scale, (void*)&n,   (void*)&rmax, (void*)&tol,
                   (void*)&rw,  (void*)&piv,   (void*)&rank, (void*)&ddg, (void*)&pub,
@@ -1631,29 +1614,29 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
   *err_dev = err;
   *handled = true;
   if (profp) {
-    std::vector<unsigned long long> h(8 * (size_t)nb_cap);
+    std::vector<unsigned long long> h(4 * (size_t)nb_cap);
     FISDF_HIP(hipMemcpyAsync(h.data(), profp, sizeof(unsigned long long) * h.size(),
                              hipMemcpyDeviceToHost, s));
     FISDF_HIP(hipStreamSynchronize(s));
-    // leader timestamps per batch: 0 candidates chosen, 1 Gram MFMA done, 2 partials added,
-    // 3 x4 - Gram formed, 4 R ready, 5 steps done, 6 published
-    double ph[7] = {0, 0, 0, 0, 0, 0, 0};
+    double ph[4] = {0, 0, 0, 0};
     int cnt = 0, nb = 0;
     for (int b = 0; b < nb_cap; ++b) {
-      const unsigned long long* a = &h[8 * (size_t)b];
+      const unsigned long long* a = &h[4 * (size_t)b];
       if (!a[0]) break;
       ++nb;
-      if (b == 0 || !a[6]) continue;
-      ph[0] += (double)(a[0] - h[8 * (size_t)(b - 1) + 6]);
-      for (int q = 1; q < 7; ++q) ph[q] += (double)(a[q] - a[q - 1]);
+      if (b == 0 || !a[1] || !a[2] || !a[3]) continue;
+      const unsigned long long prev = h[4 * (size_t)(b - 1) + 3];
+      ph[0] += (double)(a[0] - prev);  // published -> owners' update, gather, candidates
+      ph[1] += (double)(a[1] - a[0]);  // candidates' residual block (MFMA Gram)
+      ph[2] += (double)(a[2] - a[1]);  // greedy steps
+      ph[3] += (double)(a[3] - a[2]);  // publish
       ++cnt;
     }
     if (cnt)  // s_memrealtime: 100 MHz
       fprintf(stderr, "select batch G=%d RW=%d: %d batches, per batch (us) owners+gather+select "
-                      "%.2f, gram mfma %.2f, gram add %.2f, x4 %.2f, copy %.2f, steps %.2f, "
-                      "publish %.2f\n",
+                      "%.2f, gram %.2f, steps %.2f, publish %.2f\n",
               G, RW, nb, ph[0] / cnt / 100.0, ph[1] / cnt / 100.0, ph[2] / cnt / 100.0,
-              ph[3] / cnt / 100.0, ph[4] / cnt / 100.0, ph[5] / cnt / 100.0, ph[6] / cnt / 100.0);
+              ph[3] / cnt / 100.0);
   }
   return 0;
 }
@@ -1664,7 +1647,7 @@ int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rm
   *handled = false;
   *coop_err = nullptr;
   if (rmax <= 0) return 0;
-  const int mode = select_mode();
+  const int mode = select_mode(rmax);
   if (allow_coop && mode == 0) {
     FISDF_TRY(pchol_select_batch_launch(s, X2, scale, n, rmax, tol, piv, rank, work, handled,
                                         coop_err));

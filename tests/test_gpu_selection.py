@@ -147,3 +147,26 @@ def test_selection_folded_gram_large_kmesh():
     for tr in (True, False):
         perm_g = gpu_select_km(x0, kmesh, nao, int(nao * c0), time_reversal=tr)
         _tie_certified(x4, perm_g, perm_l, f"toy666 time_reversal={tr}")
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c4", "toy222"])
+def test_selection_batch_equals_coop(cfg, monkeypatch):
+    """The batched-candidate kernel (FISDF_SEL_MODE=batch; the default from 800 pivots on) and
+    the cooperative one pick the same pivots — every batched step is the greedy pivot of the
+    whole matrix, so the sequences agree to the last pivot (ties aside: both break them by the
+    smaller row on equal values computed in the same order)."""
+    if cfg.startswith("toy"):
+        from cases import inputs
+        cell, kmesh, m0, c0, x0 = inputs(cfg)[:5]
+    else:
+        cell, kmesh, c0, x0 = _cell_x0(cfg)
+    nao = cell.nao_nr()
+    perms = {}
+    for mode in ("coop", "batch"):
+        monkeypatch.setenv("FISDF_SEL_MODE", mode)
+        perms[mode] = gpu_select(x0, nao, int(nao * c0))
+    same = perms["coop"] == perms["batch"]
+    print(f"{cfg}: coop {len(perms['coop'])} batch {len(perms['batch'])} pivots, identical "
+          f"{int(same.sum()) if len(same) else 0}")
+    assert np.array_equal(perms["coop"], perms["batch"])
