@@ -148,7 +148,7 @@ struct fisdf_ctx {
   // read back through tr_pinned when ev_tr completes
   unsigned long long* trmon = nullptr;
   unsigned long long* tr_pinned = nullptr;
-  hipEvent_t ev_tr = nullptr, ev_trfork = nullptr;
+  hipEvent_t ev_tr = nullptr;
   // timing
   bool timing = false;
   struct Ev { int stage; hipEvent_t a, b; int span; };
@@ -766,7 +766,6 @@ int fisdf_destroy(fisdf_ctx* c) {
   if (c->sel_pinned) (void)hipHostFree(c->sel_pinned);
   if (c->maximag) (void)hipFree(c->maximag);
   if (c->ev_tr) (void)hipEventSynchronize(c->ev_tr), (void)hipEventDestroy(c->ev_tr);
-  if (c->ev_trfork) (void)hipEventDestroy(c->ev_trfork);
   if (c->trmon) (void)hipFree(c->trmon);
   if (c->tr_pinned) (void)hipHostFree(c->tr_pinned);
   if (c->spans) (void)hipFree(c->spans);
@@ -2751,7 +2750,6 @@ int tr_alloc(fisdf_ctx* c) {
   FISDF_HIP(hipHostMalloc((void**)&c->tr_pinned, 4 * sizeof(unsigned long long),
                           hipHostMallocDefault));
   FISDF_HIP(hipEventCreateWithFlags(&c->ev_tr, hipEventDisableTiming));
-  FISDF_HIP(hipEventCreateWithFlags(&c->ev_trfork, hipEventDisableTiming));
   FISDF_HIP(hipEventRecord(c->ev_tr, c->stream));
   return 0;
 }
@@ -2899,36 +2897,22 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
     const char* e = getenv("FISDF_TR_CHECK");
     return !(e && e[0] == '0');
   }();
+  // the check runs on the side stream behind the factor chain, during the fit (beside the
+  // latency-bound selection it cost 0.7 ms/step, profiles/r05/tr_check/); a violation found when
+  // the build is complete restarts it with every q fitted
   const bool check_tr = tr && tr_check_on;
-  if (check_tr) {
-    FISDF_TRY(ensure_side(c));
-    FISDF_TRY(tr_alloc(c));
-    FISDF_HIP(hipEventRecord(c->ev_trfork, c->stream));
-    FISDF_HIP(hipStreamWaitEvent(c->side, c->ev_trfork, 0));
-    FISDF_TRY(tr_check_enqueue(c, c->side, (const cplx*)x0, ng0, (const cplx*)f, ngrid, nao,
-                               kmesh));
-  }
+  FISDF_TRY(fisdf_set_time_reversal(c, tr ? 1 : 0));
   // interpolation points (:33 -> :357-388), or the caller's
   std::vector<int> perm;
-  for (int attempt = 0;; ++attempt) {
-    FISDF_TRY(fisdf_set_time_reversal(c, tr ? 1 : 0));
-    if (o.perm) {
-      perm.assign(o.perm, o.perm + o.n_perm);
-    } else {
-      const int cap = o.nip_max > 0 ? std::min(o.nip_max, ng0) : ng0;
-      perm.assign(cap, 0);
-      int npiv = 0, full = 0;
-      FISDF_TRY(fisdf_select_points_km(c, x0, kmesh, ng0, nao, cap, o.select_tol, perm.data(),
-                                       &npiv, &full));
-      perm.resize(std::min(cap, npiv));                                           // :383
-    }
-    if (!check_tr || attempt > 0) break;
-    FISDF_TRY(tr_verdict(c, &tr_dev));
-    if (tr_dev <= kTrTol) break;
-    if (getenv("FISDF_VERBOSE"))
-      fprintf(stderr, "fisdf: build: AO inputs violate time reversal (max |a[-k] - conj(a[k])| / "
-                      "max |a| = %.3e): every q fitted\n", tr_dev);
-    tr = false;
+  if (o.perm) {
+    perm.assign(o.perm, o.perm + o.n_perm);
+  } else {
+    const int cap = o.nip_max > 0 ? std::min(o.nip_max, ng0) : ng0;
+    perm.assign(cap, 0);
+    int npiv = 0, full = 0;
+    FISDF_TRY(fisdf_select_points_km(c, x0, kmesh, ng0, nao, cap, o.select_tol, perm.data(),
+                                     &npiv, &full));
+    perm.resize(std::min(cap, npiv));                                             // :383
   }
   const int nip = (int)perm.size();
   FISDF_CHECK(nip > 0, "build: no interpolation points");
@@ -2954,12 +2938,30 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
                              qs.data(), nq, yT));                                  // :67-87
   FISDF_TRY(fisdf_factor_x4_async(c, x4, qs.data(), nq, nip, o.fit_tol,
                                   o.real_self_conjugate ? kmesh : nullptr));
+  if (check_tr) {  // behind the factor chain on the side stream (the inputs are ready)
+    FISDF_TRY(tr_alloc(c));
+    FISDF_TRY(tr_check_enqueue(c, c->side, (const cplx*)x0, ng0, (const cplx*)f, ngrid, nao,
+                               kmesh));
+  }
   void *Wq, *Ws;
   FISDF_TRY(build_alloc(c, BR_WQ, sizeof(cplx) * (size_t)nq * nn, &Wq));
   // the fit waits for the factor's verdict itself
   FISDF_TRY(fisdf_fit_coulomb_qs(c, qs.data(), nq, yT, nip, mesh, kmesh, a, Wq));   // :97-121
   std::vector<int> ranks(nq, 0);
   FISDF_TRY(fisdf_factor_x4_wait(c, ranks.data()));
+  if (check_tr) {
+    FISDF_TRY(tr_verdict(c, &tr_dev));
+    if (tr_dev > kTrTol) {  // the fold was wrong for these inputs: the reference's path instead
+      if (getenv("FISDF_VERBOSE"))
+        fprintf(stderr, "fisdf: build: AO inputs violate time reversal (max |a[-k] - conj(a[k])| "
+                        "/ max |a| = %.3e): rebuilt with every q fitted\n", tr_dev);
+      fisdf_build_opts o2 = o;
+      o2.time_reversal = 0;
+      FISDF_TRY(fisdf_build(c, x0, ng0, f, nao, kmesh, mesh, a, &o2, h_nip));
+      c->bld.tr_deviation = tr_dev;
+      return 0;
+    }
+  }
   int used = 0, ncod = 0;
   FISDF_TRY(fisdf_factor_info(c, &used));
   FISDF_TRY(fisdf_min_norm_info(c, &ncod));

@@ -11,6 +11,26 @@ __global__ void axpy(double* y, const double* x, double a, int n) {
   if (i < n) y[i] += a * x[i];
 }
 
+// D: the same work plus one cooperative launch (hipLaunchCooperativeKernel), the launch mode
+// of libfisdf's selection kernels
+__global__ void coop_touch(double* y, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] += 1.0;
+}
+
+extern "C" int control_coop(int n) {
+  double* y = nullptr;
+  if (hipMalloc(&y, sizeof(double) * n) != hipSuccess) return 1;
+  if (hipMemset(y, 0, sizeof(double) * n) != hipSuccess) return 1;
+  void* args[] = {(void*)&y, (void*)&n};
+  if (hipLaunchCooperativeKernel((const void*)coop_touch, dim3(64), dim3(256), args, 0, 0) != hipSuccess)
+    return 3;
+  double h = -1.0;
+  if (hipMemcpy(&h, y, sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  if (hipFree(y) != hipSuccess) return 1;
+  return h == 1.0 ? 0 : 2;
+}
+
 extern "C" int control_run(int n) {
   double *x = nullptr, *y = nullptr;
   if (hipMalloc(&x, sizeof(double) * n) != hipSuccess) return 1;
@@ -27,8 +47,12 @@ extern "C" int control_run(int n) {
 
 #ifdef CONTROL_MAIN
 int main(int argc, char** argv) {
-  const int rc = control_run(1 << 20);
+  int rc = control_run(1 << 20);
   printf("control_run rc=%d\n", rc);
+  if (argc > 2) {  // D: one cooperative launch too
+    rc = control_coop(1 << 14);
+    printf("control_coop rc=%d\n", rc);
+  }
   if (argc > 1) {  // the address map, to symbolize a crash in the exit handlers
     FILE* src = fopen("/proc/self/maps", "r");
     FILE* dst = fopen(argv[1], "w");

@@ -4,6 +4,7 @@
 #   A  ./control            C++ executable, one kernel, system HIP 7.2, no Python
 #   B  python3 ctl.py        Python + ctypes libcontrol.so (system HIP 7.2), no torch, no libfisdf
 #   C  python3 ctl.py --torch  Python + torch (its bundled HIP runtime), no libfisdf
+#   D  ./control MAPS coop   (run.sh TAG coop) A plus one hipLaunchCooperativeKernel
 # and the same three without the profiler.  Prints each exit status; the stderr tails and the
 # maps go to gpurun_out/$TAG.
 TAG=${1:-rocprof_control}
@@ -19,6 +20,11 @@ run() {  # name, command...
   [ $rc -eq 124 ] || [ $rc -eq 137 ] && return 1
   return 0
 }
+if [ "$2" = "coop" ]; then  # D only: a cooperative launch under the profiler
+  run D_plain $D/control $OUT/D_plain.maps coop || exit 1
+  run D_prof rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/D -o run -- $D/control $OUT/D_prof.maps coop || exit 1
+  exit 0
+fi
 run A_plain $D/control $OUT/A_plain.maps || exit 1
 run B_plain python3 $D/ctl.py $OUT/B_plain.maps || exit 1
 run C_plain python3 $D/ctl.py $OUT/C_plain.maps --torch || exit 1
