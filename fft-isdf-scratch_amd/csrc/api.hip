@@ -2742,8 +2742,10 @@ void tr_classes(const int km[3], bool on, std::vector<int>& reps, std::vector<in
 
 // time reversal of the AO inputs (what the fold over k <= -k of the selection Gram, x4 and y, and
 // W_{-q} = conj(W_q), rely on): a[-k] = conj(a[k]) holds for real basis functions on a k-mesh
-// containing -k (get_kpts order, no shift).  The check reads x0 and f once on stream `st` (about
-// 0.25 ms at C3) and lands in tr_pinned behind ev_tr; tr_verdict waits for it.
+// containing -k (get_kpts order, no shift).  The check reads all of x0 (the selection's input,
+// 45 MB at C3) and every 61st grid point of f (x0 and f come from one basis: the whole 1.24 GB of
+// f cost 0.7 ms/step beside the selection and the y build, profiles/r05/tr_check/) on stream `st`
+// and lands in tr_pinned behind ev_tr; tr_verdict waits for it.
 int tr_alloc(fisdf_ctx* c) {
   if (c->trmon) return 0;
   FISDF_HIP(hipMalloc(&c->trmon, 4 * sizeof(unsigned long long)));
@@ -2754,13 +2756,15 @@ int tr_alloc(fisdf_ctx* c) {
   return 0;
 }
 
+constexpr long kTrFStride = 61;  // grid-point sampling of f in the composite build's check
+
 int tr_check_enqueue(fisdf_ctx* c, hipStream_t st, const cplx* x0, long ng0, const cplx* f,
                      long ngrid, int nao, const int kmesh[3]) {
   FISDF_TRY(tr_alloc(c));
   FISDF_HIP(hipEventSynchronize(c->ev_tr));  // the pinned words are rewritten below
   FISDF_HIP(hipMemsetAsync(c->trmon, 0, 4 * sizeof(unsigned long long), st));
-  FISDF_TRY(tr_check(st, x0, ng0 * nao, ng0 * nao, kmesh, c->trmon));
-  if (f) FISDF_TRY(tr_check(st, f, ngrid * nao, ngrid * nao, kmesh, c->trmon + 2));
+  FISDF_TRY(tr_check(st, x0, ng0 * nao, ng0, nao, 1, kmesh, c->trmon));
+  if (f) FISDF_TRY(tr_check(st, f, ngrid * nao, ngrid, nao, kTrFStride, kmesh, c->trmon + 2));
   FISDF_HIP(hipMemcpyAsync(c->tr_pinned, c->trmon, 4 * sizeof(unsigned long long),
                            hipMemcpyDeviceToHost, st));
   FISDF_HIP(hipEventRecord(c->ev_tr, st));
@@ -2816,7 +2820,7 @@ int fisdf_check_time_reversal(fisdf_ctx* c, const void* d_a, long k_stride, long
   FISDF_TRY(tr_alloc(c));
   FISDF_HIP(hipEventSynchronize(c->ev_tr));
   FISDF_HIP(hipMemsetAsync(c->trmon, 0, 4 * sizeof(unsigned long long), c->stream));
-  FISDF_TRY(tr_check(c->stream, (const cplx*)d_a, k_stride, per_k, kmesh, c->trmon));
+  FISDF_TRY(tr_check(c->stream, (const cplx*)d_a, k_stride, per_k, 1, 1, kmesh, c->trmon));
   unsigned long long h[2];
   FISDF_HIP(hipMemcpyAsync(h, c->trmon, sizeof(h), hipMemcpyDeviceToHost, c->stream));
   FISDF_HIP(hipStreamSynchronize(c->stream));
@@ -2897,22 +2901,35 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
     const char* e = getenv("FISDF_TR_CHECK");
     return !(e && e[0] == '0');
   }();
-  // the check runs on the side stream behind the factor chain, during the fit (beside the
-  // latency-bound selection it cost 0.7 ms/step, profiles/r05/tr_check/); a violation found when
-  // the build is complete restarts it with every q fitted
+  // the check (~20 us) runs on the main stream ahead of the selection, whose read-back brings
+  // the verdict along; a violation redoes the selection without the fold and fits every q
   const bool check_tr = tr && tr_check_on;
-  FISDF_TRY(fisdf_set_time_reversal(c, tr ? 1 : 0));
+  if (check_tr) {
+    FISDF_TRY(tr_alloc(c));
+    FISDF_TRY(tr_check_enqueue(c, c->stream, (const cplx*)x0, ng0, (const cplx*)f, ngrid, nao,
+                               kmesh));
+  }
   // interpolation points (:33 -> :357-388), or the caller's
   std::vector<int> perm;
-  if (o.perm) {
-    perm.assign(o.perm, o.perm + o.n_perm);
-  } else {
-    const int cap = o.nip_max > 0 ? std::min(o.nip_max, ng0) : ng0;
-    perm.assign(cap, 0);
-    int npiv = 0, full = 0;
-    FISDF_TRY(fisdf_select_points_km(c, x0, kmesh, ng0, nao, cap, o.select_tol, perm.data(),
-                                     &npiv, &full));
-    perm.resize(std::min(cap, npiv));                                             // :383
+  for (int attempt = 0;; ++attempt) {
+    FISDF_TRY(fisdf_set_time_reversal(c, tr ? 1 : 0));
+    if (o.perm) {
+      perm.assign(o.perm, o.perm + o.n_perm);
+    } else {
+      const int cap = o.nip_max > 0 ? std::min(o.nip_max, ng0) : ng0;
+      perm.assign(cap, 0);
+      int npiv = 0, full = 0;
+      FISDF_TRY(fisdf_select_points_km(c, x0, kmesh, ng0, nao, cap, o.select_tol, perm.data(),
+                                       &npiv, &full));
+      perm.resize(std::min(cap, npiv));                                           // :383
+    }
+    if (!check_tr || attempt > 0) break;
+    FISDF_TRY(tr_verdict(c, &tr_dev));
+    if (tr_dev <= kTrTol) break;
+    if (getenv("FISDF_VERBOSE"))
+      fprintf(stderr, "fisdf: build: AO inputs violate time reversal (max |a[-k] - conj(a[k])| / "
+                      "max |a| = %.3e): every q fitted\n", tr_dev);
+    tr = false;
   }
   const int nip = (int)perm.size();
   FISDF_CHECK(nip > 0, "build: no interpolation points");
@@ -2938,30 +2955,14 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
                              qs.data(), nq, yT));                                  // :67-87
   FISDF_TRY(fisdf_factor_x4_async(c, x4, qs.data(), nq, nip, o.fit_tol,
                                   o.real_self_conjugate ? kmesh : nullptr));
-  if (check_tr) {  // behind the factor chain on the side stream (the inputs are ready)
-    FISDF_TRY(tr_alloc(c));
-    FISDF_TRY(tr_check_enqueue(c, c->side, (const cplx*)x0, ng0, (const cplx*)f, ngrid, nao,
-                               kmesh));
-  }
+
   void *Wq, *Ws;
   FISDF_TRY(build_alloc(c, BR_WQ, sizeof(cplx) * (size_t)nq * nn, &Wq));
   // the fit waits for the factor's verdict itself
   FISDF_TRY(fisdf_fit_coulomb_qs(c, qs.data(), nq, yT, nip, mesh, kmesh, a, Wq));   // :97-121
   std::vector<int> ranks(nq, 0);
   FISDF_TRY(fisdf_factor_x4_wait(c, ranks.data()));
-  if (check_tr) {
-    FISDF_TRY(tr_verdict(c, &tr_dev));
-    if (tr_dev > kTrTol) {  // the fold was wrong for these inputs: the reference's path instead
-      if (getenv("FISDF_VERBOSE"))
-        fprintf(stderr, "fisdf: build: AO inputs violate time reversal (max |a[-k] - conj(a[k])| "
-                        "/ max |a| = %.3e): rebuilt with every q fitted\n", tr_dev);
-      fisdf_build_opts o2 = o;
-      o2.time_reversal = 0;
-      FISDF_TRY(fisdf_build(c, x0, ng0, f, nao, kmesh, mesh, a, &o2, h_nip));
-      c->bld.tr_deviation = tr_dev;
-      return 0;
-    }
-  }
+
   int used = 0, ncod = 0;
   FISDF_TRY(fisdf_factor_info(c, &used));
   FISDF_TRY(fisdf_min_norm_info(c, &ncod));

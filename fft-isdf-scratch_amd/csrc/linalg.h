@@ -26,10 +26,11 @@ int set_identity(hipStream_t s, cplx* X, int n, int batch);
 // out[g][j*nao + m] = h_sc[j] * x0[h_k[j]][g][m] for the nsel listed k (any nsel)
 int permute_kgm_sel(hipStream_t s, const cplx* x0, const int* h_k, const double* h_sc, int nsel,
                     int ng, int nao, cplx* out);
-// time-reversal check of Bloch AO values a[k][.] (per_k elements, k stride ks, get_kpts order):
-// atomically maxes mon[0] with max |a[-k] - conj(a[k])| and mon[1] with max |a[k]| (double bits)
-int tr_check(hipStream_t s, const cplx* a, long ks, long per_k, const int kmesh[3],
-             unsigned long long* mon);
+// time-reversal check of Bloch AO values a[k][row][nao] (k stride ks elements, get_kpts order) on
+// every rstride-th row: atomically maxes mon[0] with max |a[-k] - conj(a[k])| and mon[1] with
+// max |a[k]| (double bits)
+int tr_check(hipStream_t s, const cplx* a, long ks, long rows, int nao, long rstride,
+             const int kmesh[3], unsigned long long* mon);
 // the time-reversal representatives k <= -k (ascending) and whether each is self-paired
 void kmesh_reps(const int kmesh[3], std::vector<int>* reps, std::vector<char>* self);
 int trsm_blocked(hipStream_t s, int lower, const cplx* Lp, long ldl, long sL, int r,

@@ -1624,15 +1624,17 @@ void kmesh_reps(const int kmesh[3], std::vector<int>* reps, std::vector<char>* s
 // time-reversal check of Bloch AO values a[k][r][m] (k stride ks): mon[0] = max over the
 // representatives k <= -k of |a[-k] - conj(a[k])| (2 |Im a[k]| on a self-paired k), mon[1] = max
 // |a[k]|, both as the ordered bit patterns of non-negative doubles.  Every pair is read once.
-__global__ void tr_check_kernel(const cplx* __restrict__ a, long ks, long per_k, int n0, int n1,
-                                int n2, unsigned long long* __restrict__ mon) {
+__global__ void tr_check_kernel(const cplx* __restrict__ a, long ks, long per_k, int nao,
+                                long rstride, int n0, int n1, int n2,
+                                unsigned long long* __restrict__ mon) {
   const int nk = n0 * n1 * n2;
   double dev = 0.0, mag = 0.0;
   const long tot = (long)nk * per_k;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot;
        e += (long)gridDim.x * blockDim.x) {
     const int k = (int)(e / per_k);
-    const long r = e - (long)k * per_k;
+    const long i = e - (long)k * per_k;  // sampled row i / nao (every rstride-th row), AO i % nao
+    const long r = (i / nao) * rstride * nao + i % nao;
     const int p = kmesh_partner(k, n0, n1, n2);
     if (p < k) continue;
     const cplx u = a[k * ks + r];
@@ -1650,13 +1652,15 @@ __global__ void tr_check_kernel(const cplx* __restrict__ a, long ks, long per_k,
   }
 }
 
-int tr_check(hipStream_t s, const cplx* a, long ks, long per_k, const int kmesh[3],
-             unsigned long long* mon) {
-  FISDF_CHECK(per_k > 0 && ks >= per_k && kmesh[0] > 0 && kmesh[1] > 0 && kmesh[2] > 0,
+int tr_check(hipStream_t s, const cplx* a, long ks, long rows, int nao, long rstride,
+             const int kmesh[3], unsigned long long* mon) {
+  FISDF_CHECK(rows > 0 && nao > 0 && rstride > 0 && ks >= rows * nao && kmesh[0] > 0 &&
+                  kmesh[1] > 0 && kmesh[2] > 0,
               "tr_check: bad sizes");
+  const long per_k = ((rows + rstride - 1) / rstride) * nao;
   const long n = (long)kmesh[0] * kmesh[1] * kmesh[2] * per_k;
   hipLaunchKernelGGL(tr_check_kernel, dim3(nblocks(n, 256, 4096)), dim3(256), 0, s, a, ks, per_k,
-                     kmesh[0], kmesh[1], kmesh[2], mon);
+                     nao, rstride, kmesh[0], kmesh[1], kmesh[2], mon);
   FISDF_HIP(hipGetLastError());
   return 0;
 }

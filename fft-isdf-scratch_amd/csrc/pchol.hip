@@ -472,7 +472,7 @@ __global__ __launch_bounds__(256) void syrk_real_update(double* __restrict__ W, 
 }
 
 // ---- cooperative left-looking variant (default for the selection) ----------------------
-// One pivot per step over a co-resident grid (hipLaunchCooperativeKernel): workgroup w owns
+// One pivot per step over a co-resident grid (launch_coresident): workgroup w owns
 // rows [w*RW, w*RW+RW) with their L rows in LDS (and a copy in the row-major global L) and
 // their residual diagonal.  Step j:
 //   post: the local arg-max of the residual diagonal as one 16-byte record {value, row, step}
@@ -1431,6 +1431,28 @@ bool select_coop_enabled() {
   return !(e && e[0] == '0');
 }
 
+// Launch of a grid whose workgroups wait on each other (the selection kernels): every workgroup
+// must be resident at once.  A plain launch after the occupancy check gives the same residency as
+// hipLaunchCooperativeKernel (MI355X_MICROARCH.md: the cooperative launch adds only that check)
+// and, unlike it, leaves no cooperative-queue state behind: a process that made one cooperative
+// launch SIGSEGVs in its exit handlers under rocprofv3 (ROCm 7.2; a one-kernel control program
+// reproduces it, profiles/r05/rocprof_exit/).  FISDF_COOP_LAUNCH=1 restores the cooperative
+// launch.  Returns hipErrorCooperativeLaunchTooLarge when the grid would not be co-resident.
+hipError_t launch_coresident(const void* fn, int grid, int threads, void** args, size_t lds,
+                             hipStream_t s, int ncu) {
+  static const bool coop = [] {
+    const char* e = getenv("FISDF_COOP_LAUNCH");
+    return e && e[0] == '1';
+  }();
+  if (coop)
+    return hipLaunchCooperativeKernel(fn, dim3(grid), dim3(threads), args, (unsigned)lds, s);
+  int per_cu = 0;
+  const hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds);
+  if (oe != hipSuccess) return oe;
+  if ((long)per_cu * ncu < grid) return hipErrorCooperativeLaunchTooLarge;
+  return hipLaunchKernel(fn, dim3(grid), dim3(threads), args, lds, s);
+}
+
 // launches pchol_select_coop when the owned L rows fit the LDS of a co-resident grid;
 // *handled = false (nothing enqueued that matters) otherwise or if the launch is refused.  No
 // host synchronisation: *err_dev receives the device address of the kernel's error flag (a
@@ -1504,8 +1526,8 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
   void* args[] = {(void*)&X2, (void*)&scale, (void*)&n,   (void*)&rmax, (void*)&tol, (void*)&RW,
                   (void*)&K,   (void*)&tpr,   (void*)&piv, (void*)&rank, (void*)&rec, (void*)&Lg,
                   (void*)&err, (void*)&profp};
-  const hipError_t e = hipLaunchCooperativeKernel((const void*)pchol_select_coop, dim3(G),
-                                                  dim3(SC_THREADS), args, (unsigned)lds, s);
+  const hipError_t e =
+      launch_coresident((const void*)pchol_select_coop, G, SC_THREADS, args, lds, s, ncu);
   if (e != hipSuccess) {  // refused (e.g. not co-resident): the caller's blocked path runs
     (void)hipGetLastError();
     return 0;
@@ -1605,8 +1627,8 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
   void* args[] = {(void*)&X2,  (void*)&scale, (void*)&n,   (void*)&rmax, (void*)&tol,
                   (void*)&rw,  (void*)&piv,   (void*)&rank, (void*)&ddg, (void*)&pub,
                   (void*)&Lg,  (void*)&err,   (void*)&profp};
-  const hipError_t e = hipLaunchCooperativeKernel((const void*)pchol_select_batch, dim3(G + 1),
-                                                  dim3(SB_THREADS), args, (unsigned)lds, s);
+  const hipError_t e =
+      launch_coresident((const void*)pchol_select_batch, G + 1, SB_THREADS, args, lds, s, ncu);
   if (e != hipSuccess) {  // refused (e.g. not co-resident): the caller's next path runs
     (void)hipGetLastError();
     return 0;
