@@ -1432,17 +1432,21 @@ bool select_coop_enabled() {
 }
 
 // Launch of a grid whose workgroups wait on each other (the selection kernels): every workgroup
-// must be resident at once.  A plain launch after the occupancy check gives the same residency as
-// hipLaunchCooperativeKernel (MI355X_MICROARCH.md: the cooperative launch adds only that check)
-// and, unlike it, leaves no cooperative-queue state behind: a process that made one cooperative
-// launch SIGSEGVs in its exit handlers under rocprofv3 (ROCm 7.2; a one-kernel control program
-// reproduces it, profiles/r05/rocprof_exit/).  FISDF_COOP_LAUNCH=1 restores the cooperative
-// launch.  Returns hipErrorCooperativeLaunchTooLarge when the grid would not be co-resident.
+// must be resident at once.  Default: hipLaunchCooperativeKernel.  FISDF_COOP_LAUNCH=0 launches
+// plainly after the occupancy check (the same residency, MI355X_MICROARCH.md).  Why both
+// (profiles/r05/rocprof_exit/README.txt):
+//  * a process that made one cooperative launch SIGSEGVs in its exit handlers under rocprofv3
+//    (ROCm 7.2; a one-kernel control program with one cooperative launch reproduces it, the same
+//    program without it exits cleanly) — the plain launch leaves profiled processes exiting 0;
+//  * but the plain launch moves the context's streams onto the 4 hardware queues differently: the
+//    two fit lanes then share one and serialise (C3 89.9 vs 81.0 ms/step on one box), so the
+//    cooperative launch stays the default and profiles are judged by their output files.
+// Returns hipErrorCooperativeLaunchTooLarge when the grid would not be co-resident.
 hipError_t launch_coresident(const void* fn, int grid, int threads, void** args, size_t lds,
                              hipStream_t s, int ncu) {
   static const bool coop = [] {
     const char* e = getenv("FISDF_COOP_LAUNCH");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   if (coop)
     return hipLaunchCooperativeKernel(fn, dim3(grid), dim3(threads), args, (unsigned)lds, s);
