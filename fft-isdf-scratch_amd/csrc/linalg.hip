@@ -774,186 +774,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
-// Warp-specialised fused y build (round 5; FISDF_YF_WS=0 keeps y_fused_kernel).  In
-// y_fused_kernel both resident workgroups of a CU run the same phase at the same time — the
-// operand-latency-bound MFMA phase, then the store-bound DFT phase — so neither hides the other
-// (full ~ MFMA phase + store phase).  Here one 512-thread workgroup per CU walks the
-// tiles persistently with two roles: waves 0-3 (producers) form fx of one k-plane chunk of a
-// tile on MFMA into an LDS buffer (the same yf_mfma_chunk), waves 4-7 (consumers) take each
-// chunk into registers (its in-plane 2-D DFTs) and, after a tile's last chunk, run the axis-0
-// DFTs, the square, the inverse DFTs and the stores — while the producers already fill the next
-// tile's chunks.  Chunks = k-planes (plane 0 and N0/2 at their in-plane representatives, plane 1
-// whole), two 16-slot buffers (128 KB); the roles hand buffers over through LDS counters.
-template <int N0, int N1, int N2>
-__global__ __launch_bounds__(512) void y_fused_ws_kernel(
-    const cplx* __restrict__ XT, int nip, int nao, const cplx* __restrict__ FT, int m, int nIt,
-    int nGt, YfPlan plan, unsigned long long qmask, cplx* __restrict__ yT, long qs, long Is,
-    long goff, int gpair, long ntiles) {
-  constexpr int P = N1 * N2, NK = N0 * P;
-  constexpr int R = yf_inplane_rank<N1, N2>(P);
-  constexpr int NC = (N0 - 1) / 2;
-  constexpr int NR = (N0 % 2 == 0 && N0 > 1) ? 2 : 1;
-  constexpr int NCH = NR + NC;      // chunks per tile: the self-paired planes, then plane 1
-  static_assert(N0 <= 4 && NC <= 1 && P <= 16, "y_fused_ws: k-mesh axis 0 <= 4, planes <= 16");
-  extern __shared__ cplx buf[];     // [2][16 slots][256]
-  __shared__ int prod_done, cons_done;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const bool producer = w < 4;
-  if (tid == 0) {
-    prod_done = 0;
-    cons_done = 0;
-  }
-  __syncthreads();
-  // tile index -> (I-tile, g-tile): XCD x (= virtual block & 7) walks its g-tiles in groups of
-  // gpair with the I-tiles slowest, as y_fused_kernel
-  auto tile_of = [&](long vb, int* I0, int* g0) {
-    const int xcd = (int)(vb & 7);
-    const long jj = vb >> 3;
-    const long grp = jj / ((long)nIt * gpair), rem = jj - grp * nIt * gpair;
-    const int it = (int)(rem / gpair), gt = (int)((grp * gpair + rem % gpair) * 8 + xcd);
-    *I0 = it * 16;
-    *g0 = gt < nGt ? gt * 16 : -1;
-  };
-  // chunk ch of a tile: its plan slots [sb, sb + ns) (plan order: plane 1 (nA), then the
-  // self-paired planes' representatives (R each))
-  auto chunk_slots = [&](int ch, int* sb, int* ns) {
-    if (ch < NR) {
-      *sb = plan.nA + ch * R;
-      *ns = R;
-    } else {
-      *sb = 0;
-      *ns = plan.nA;
-    }
-  };
-  long t = 0;  // global chunk sequence number of this workgroup
-  if (producer) {
-    for (long vb = blockIdx.x; vb < ntiles; vb += gridDim.x) {
-      int I0, g0;
-      tile_of(vb, &I0, &g0);
-#pragma unroll 1
-      for (int ch = 0; ch < NCH; ++ch, ++t) {
-        // buffer t & 1 is free once the consumers have taken chunk t - 2
-        if (t >= 2)
-          while (__hip_atomic_load(&cons_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * (t - 1))
-            __builtin_amdgcn_s_sleep(1);
-        if (g0 >= 0) {
-          int sb, ns;
-          chunk_slots(ch, &sb, &ns);
-          const int Ia = I0 + (lane & 15), ga = g0 + (lane & 15);
-          yf_mfma_chunk(XT, nip, nao, FT, m, sb, ns, Ia, Ia < nip, ga, ga < m, lane, w,
-                        buf + (t & 1) * 16 * 256);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_fetch_add(&prod_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-    return;
-  }
-  // ---- consumers: one thread per (I, g) column of the tile ----
-  const int ct = tid - 256;
-  cplx tw0[N0], tw1[N1], tw2[N2];
-#pragma unroll
-  for (int q = 0; q < N0; ++q) { double sn, cs; sincospi(2.0 * q / N0, &sn, &cs); tw0[q] = cmk(cs, sn); }
-#pragma unroll
-  for (int q = 0; q < N1; ++q) { double sn, cs; sincospi(2.0 * q / N1, &sn, &cs); tw1[q] = cmk(cs, sn); }
-#pragma unroll
-  for (int q = 0; q < N2; ++q) { double sn, cs; sincospi(2.0 * q / N2, &sn, &cs); tw2[q] = cmk(cs, sn); }
-  const double sc = 1.0 / sqrt((double)NK), sc2 = sc * sc;
-  for (long vb = blockIdx.x; vb < ntiles; vb += gridDim.x) {
-    int I0, g0;
-    tile_of(vb, &I0, &g0);
-    cplx tc[NC > 0 ? P : 1];
-    double tr[NR][P];
-#pragma unroll
-    for (int ch = 0; ch < NCH; ++ch, ++t) {
-      while (__hip_atomic_load(&prod_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * (t + 1))
-        __builtin_amdgcn_s_sleep(1);
-      const cplx* b = buf + (t & 1) * 16 * 256;
-      if (ch < NR) {
-        cplx u[P];
-#pragma unroll
-        for (int bc = 0; bc < P; ++bc)
-          if (bc <= yf_inplane_partner<N1, N2>(bc)) u[bc] = b[yf_inplane_rank<N1, N2>(bc) * 256 + ct];
-#pragma unroll
-        for (int bc = 0; bc < P; ++bc)
-          if (bc > yf_inplane_partner<N1, N2>(bc)) u[bc] = cconj(u[yf_inplane_partner<N1, N2>(bc)]);
-        reg_axis_dft<N1, N2, P>(u, tw1);
-        reg_axis_dft<N2, 1, P>(u, tw2);
-#pragma unroll
-        for (int bc = 0; bc < P; ++bc) tr[ch][bc] = u[bc].x;
-      } else if constexpr (NC > 0) {
-#pragma unroll
-        for (int bc = 0; bc < P; ++bc) tc[bc] = b[bc * 256 + ct];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the reads above are done
-      if (lane == 0) __hip_atomic_fetch_add(&cons_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    if (g0 < 0) continue;
-    if constexpr (NC > 0) {
-      reg_axis_dft<N1, N2, P>(tc, tw1);
-      reg_axis_dft<N2, 1, P>(tc, tw2);
-    }
-    // ---- per s: fx_s over axis 0, y_s = fx_s^2, r_qa = axis-0 DFT of y_s (as y_fused_kernel) ----
-    double rr[NR][P];
-    cplx rc[NC > 0 ? P : 1];
-#pragma unroll
-    for (int s = 0; s < P; ++s) {
-      double ys[N0];
-#pragma unroll
-      for (int a2 = 0; a2 < N0; ++a2) {
-        double f = tr[0][s];
-        if constexpr (NR == 2) f += (a2 & 1) ? -tr[1][s] : tr[1][s];
-        if constexpr (NC > 0) {
-          const cplx wv = tw0[a2 % N0];
-          f += 2.0 * (wv.x * tc[s].x - wv.y * tc[s].y);
-        }
-        ys[a2] = f * f * sc2;
-      }
-      double r0 = 0.0, rh = 0.0;
-      cplx r1 = cmk(0, 0);
-#pragma unroll
-      for (int a2 = 0; a2 < N0; ++a2) {
-        r0 += ys[a2];
-        if constexpr (NR == 2) rh += (a2 & 1) ? -ys[a2] : ys[a2];
-        if constexpr (NC > 0) r1 = cadd(r1, cscale(tw0[a2 % N0], ys[a2]));
-      }
-      rr[0][s] = r0;
-      if constexpr (NR == 2) rr[1][s] = rh;
-      if constexpr (NC > 0) rc[s] = r1;
-    }
-    const int I = I0 + (ct >> 4), g = g0 + (ct & 15);
-    if (I >= nip || g >= m) continue;
-    cplx* out = yT + (long)I * Is + goff + g;
-    auto put = [&](int q, cplx v) {
-      if ((qmask >> q) & 1ull) {
-        typedef double dv2 __attribute__((ext_vector_type(2)));
-        __builtin_nontemporal_store(dv2{v.x * sc, v.y * sc},
-                                    (dv2*)(out + (long)__popcll(qmask & ((1ull << q) - 1ull)) * qs));
-      }
-    };
-#pragma unroll
-    for (int pi = 0; pi < NR; ++pi) {
-      cplx u[P];
-#pragma unroll
-      for (int bc = 0; bc < P; ++bc) u[bc] = cmk(rr[pi][bc], 0.0);
-      reg_axis_dft<N1, N2, P>(u, tw1);
-      reg_axis_dft<N2, 1, P>(u, tw2);
-      const int qa = pi == 0 ? 0 : N0 / 2;
-#pragma unroll
-      for (int bc = 0; bc < P; ++bc) put(qa * P + bc, u[bc]);
-    }
-    if constexpr (NC > 0) {
-      reg_axis_dft<N1, N2, P>(rc, tw1);
-      reg_axis_dft<N2, 1, P>(rc, tw2);
-#pragma unroll
-      for (int bc = 0; bc < P; ++bc) {
-        put(P + bc, rc[bc]);
-        put((N0 - 1) * P + yf_inplane_partner<N1, N2>(bc), cconj(rc[bc]));
-      }
-    }
-  }
-}
-
 // pair densities at the interpolation points: P[I][i*n2 + j] = conj(A[I][i]) * B[I][j]
 __global__ void pair_product_kernel(const cplx* __restrict__ A, int n1, const cplx* __restrict__ B,
                                     int n2, int nip, cplx* __restrict__ P) {
@@ -1721,41 +1541,6 @@ int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long 
   const long grid = (long)nIt * ((nGt + 8 * gpair - 1) / (8 * gpair)) * gpair * 8;
   FISDF_CHECK(grid < (1L << 31), "y_fused: grid too large");
   static const int mode = getenv("FISDF_YF_MODE") ? atoi(getenv("FISDF_YF_MODE")) : 0;
-  // the warp-specialised kernel (default; FISDF_YF_WS=0: the two-phase kernel), for k-meshes
-  // whose planes fit one 16-slot buffer: one persistent workgroup per CU
-  static const bool ws = [] {
-    const char* e = getenv("FISDF_YF_WS");
-    return !(e && e[0] == '0');
-  }();
-  if (ws && mode == 0 && n1 * n2 <= 16) {
-    static const int ncu = [] {
-      int dev = 0, v = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 256;
-      return v;
-    }();
-    const size_t wlds = sizeof(cplx) * 2 * 16 * 256;
-    const long ntiles = grid;
-#define FISDF_YW(a, b, c)                                                                      \
-    if (n0 == a && n1 == b && n2 == c) {                                                       \
-      static bool wattr = false;                                                               \
-      if (!wattr) {                                                                            \
-        FISDF_HIP(hipFuncSetAttribute((const void*)y_fused_ws_kernel<a, b, c>,                 \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)wlds)); \
-        wattr = true;                                                                          \
-      }                                                                                        \
-      const unsigned wg = (unsigned)std::min<long>(ntiles, ncu);                               \
-      hipLaunchKernelGGL((y_fused_ws_kernel<a, b, c>), dim3(wg), dim3(512), wlds, s, XT, nip,  \
-                         nao, FT, m, nIt, nGt, plan, qmask, yT, qs, Is, goff, gpair, ntiles);   \
-      FISDF_HIP(hipGetLastError());                                                            \
-      *handled = true;                                                                         \
-      return 0;                                                                                \
-    }
-    FISDF_YW(1, 1, 1) FISDF_YW(1, 1, 2) FISDF_YW(2, 2, 2) FISDF_YW(3, 3, 1) FISDF_YW(3, 3, 3)
-    FISDF_YW(4, 4, 4) FISDF_YW(2, 2, 1) FISDF_YW(1, 2, 2) FISDF_YW(4, 4, 1) FISDF_YW(2, 2, 4)
-#undef FISDF_YW
-  }
 #define FISDF_YF(a, b, c)                                                                      \
   if (n0 == a && n1 == b && n2 == c) {                                                         \
     static bool attr = false;                                                                  \
