@@ -2901,7 +2901,7 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
     const char* e = getenv("FISDF_TR_CHECK");
     return !(e && e[0] == '0');
   }();
-  // the check (~20 us) runs on the main stream ahead of the selection, whose read-back brings
+  // the check (~25 us) runs on the main stream ahead of the selection, whose read-back brings
   // the verdict along; a violation redoes the selection without the fold and fits every q
   const bool check_tr = tr && tr_check_on;
   if (check_tr) {

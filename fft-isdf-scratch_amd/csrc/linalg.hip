@@ -1646,7 +1646,20 @@ __global__ void tr_check_kernel(const cplx* __restrict__ a, long ks, long per_k,
     dev = fmax(dev, __shfl_xor(dev, o, 64));
     mag = fmax(mag, __shfl_xor(mag, o, 64));
   }
+  // one pair of device atomics per workgroup: the per-wave atomics (32 k of them on two words,
+  // serialised in the memory fabric) cost ~0.9 ms per build at C3
+  __shared__ double red[2][4];
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
+    red[0][w] = dev;
+    red[1][w] = mag;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) {
+      dev = fmax(dev, red[0][i]);
+      mag = fmax(mag, red[1][i]);
+    }
     atomicMax(mon, (unsigned long long)__double_as_longlong(dev));
     atomicMax(mon + 1, (unsigned long long)__double_as_longlong(mag));
   }
@@ -1659,7 +1672,7 @@ int tr_check(hipStream_t s, const cplx* a, long ks, long rows, int nao, long rst
               "tr_check: bad sizes");
   const long per_k = ((rows + rstride - 1) / rstride) * nao;
   const long n = (long)kmesh[0] * kmesh[1] * kmesh[2] * per_k;
-  hipLaunchKernelGGL(tr_check_kernel, dim3(nblocks(n, 256, 4096)), dim3(256), 0, s, a, ks, per_k,
+  hipLaunchKernelGGL(tr_check_kernel, dim3(nblocks(n, 256, 1024)), dim3(256), 0, s, a, ks, per_k,
                      nao, rstride, kmesh[0], kmesh[1], kmesh[2], mon);
   FISDF_HIP(hipGetLastError());
   return 0;

@@ -33,7 +33,7 @@ if [ -n "$TESTS" ]; then
 fi
 run_variant() {  # $1 variant, $2 rep
   local v=$1 i=$2 name envs=() lib=""
-  name=$(echo "$v" | tr ',=:' '_-.')
+  name=$(echo "$v" | tr ',=:' '_.-')
   case $v in
     default) ;;
     lib:*) lib=${v#lib:} ;;
