@@ -170,7 +170,16 @@ struct fisdf_ctx {
     std::vector<int> perm, fit_qs, partner, ranks;
     std::vector<double> wt;
     void *X = nullptr, *x4 = nullptr, *Wq = nullptr, *Ws = nullptr;
+    // fisdf_build_sharded: this rank's share (W_s rows [row0, row1), W_0 broadcast) and the
+    // caller's collectives (get_jk all-reduces through them)
+    int shard_rank = 0, shard_size = 1, row0 = 0, row1 = 0;
+    void* W0 = nullptr;
+    bool sharded = false;
+    fisdf_comm comm{};
   } bld;
+  // stream of the sharded build's all-to-all (fisdf_build_sharded), forked from `stream`
+  hipStream_t comm_stream = nullptr;
+  hipEvent_t ev_comm = nullptr;
   // fisdf_set_allocator: device memory of the composite build's buffers from the caller (e.g. a
   // framework's caching allocator), else library-owned grow-only buffers
   fisdf_alloc_fn alloc_fn = nullptr;
@@ -759,6 +768,11 @@ int fisdf_destroy(fisdf_ctx* c) {
   for (hipEvent_t e : c->ev_q) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_free) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_ready) (void)hipEventDestroy(e);
+  if (c->comm_stream) {
+    (void)hipStreamSynchronize(c->comm_stream);
+    (void)hipStreamDestroy(c->comm_stream);
+    (void)hipEventDestroy(c->ev_comm);
+  }
   for (auto& kv : c->plane_cache) (void)hipFree(kv.second);
   if (c->arena) (void)hipFree(c->arena);
   if (c->ev_stage) (void)hipEventSynchronize(c->ev_stage), (void)hipEventDestroy(c->ev_stage);
@@ -1720,8 +1734,11 @@ int fisdf_set_fit_pipe(fisdf_ctx* c, int mode, int depth) {
   return 0;
 }
 
-int fisdf_mark_y_ready(fisdf_ctx* c, int j) {
-  FISDF_TRY(device_guard(c));
+}  // extern "C"
+
+namespace {
+// y of the next fit's j-th q has landed once the work enqueued so far on `st` is done
+int mark_y_ready_on(fisdf_ctx* c, int j, hipStream_t st) {
   FISDF_CHECK(j >= 0 && j < 4096, "mark_y_ready: bad index");
   while ((int)c->ev_ready.size() <= j) {
     hipEvent_t e;
@@ -1729,14 +1746,13 @@ int fisdf_mark_y_ready(fisdf_ctx* c, int j) {
     c->ev_ready.push_back(e);
   }
   if ((int)c->ready_marked.size() <= j) c->ready_marked.resize(j + 1, 0);
-  FISDF_HIP(hipEventRecord(c->ev_ready[j], c->stream));
+  FISDF_HIP(hipEventRecord(c->ev_ready[j], st));
   c->ready_marked[j] = 1;
   return 0;
 }
 
-int fisdf_set_y_slices(fisdf_ctx* c, int j, const void* recv, int nparts, const long* h_g0,
-                       const long* h_ng) {
-  FISDF_TRY(device_guard(c));
+int set_y_slices_on(fisdf_ctx* c, int j, const void* recv, int nparts, const long* h_g0,
+                    const long* h_ng, hipStream_t st) {
   FISDF_CHECK(recv != nullptr && nparts >= 1 && nparts <= 4096, "set_y_slices: bad piece");
   std::vector<long> sl;
   for (int p = 0; p < nparts; ++p) {
@@ -1750,7 +1766,21 @@ int fisdf_set_y_slices(fisdf_ctx* c, int j, const void* recv, int nparts, const 
   c->y_slices = sl;
   if ((int)c->y_piece.size() <= j) c->y_piece.resize(j + 1, nullptr);
   c->y_piece[j] = (const cplx*)recv;
-  return fisdf_mark_y_ready(c, j);
+  return mark_y_ready_on(c, j, st);
+}
+}  // namespace
+
+extern "C" {
+
+int fisdf_mark_y_ready(fisdf_ctx* c, int j) {
+  FISDF_TRY(device_guard(c));
+  return mark_y_ready_on(c, j, c->stream);
+}
+
+int fisdf_set_y_slices(fisdf_ctx* c, int j, const void* recv, int nparts, const long* h_g0,
+                       const long* h_ng) {
+  FISDF_TRY(device_guard(c));
+  return set_y_slices_on(c, j, recv, nparts, h_g0, h_ng, c->stream);
 }
 
 int fisdf_fit_info(fisdf_ctx* c, int* h_lanes, int* h_pipe_depth) {
@@ -2663,7 +2693,8 @@ int fisdf_get_k(fisdf_ctx* c, const void* Xv, const void* Wsv, const void* dmsv,
 
 namespace {
 
-enum BuildRole { BR_X = 0, BR_X4 = 1, BR_Y = 2, BR_WQ = 3, BR_WS = 4 };
+enum BuildRole { BR_X = 0, BR_X4 = 1, BR_Y = 2, BR_WQ = 3, BR_WS = 4, BR_SEND = 5, BR_WSB = 6,
+                 BR_W0 = 7 };
 
 // a buffer of the composite build: the caller's allocator, or a library-owned grow-only buffer
 int build_alloc(fisdf_ctx* c, int role, size_t bytes, void** out) {
@@ -2868,11 +2899,47 @@ int fisdf_build_release(fisdf_ctx* c) {
   return 0;
 }
 
-// ISDF.build() (fftisdf.py:308-325 -> build(df_obj), :22-128) on one GPU: the same stage sequence
-// the Python mirror's k-shard-capable build runs (fisdf/isdf.py build(), unsharded branch)
-int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, const int kmesh[3],
-                const int mesh[3], const double a[9], const fisdf_build_opts* opts_in, int* h_nip) {
-  FISDF_TRY(device_guard(c));
+}  // extern "C"
+
+namespace {
+
+// kshard.assign_q: longest-processing-time greedy over the fit positions (most expensive first,
+// each to the least loaded rank, ties to the lower rank), each rank's positions ascending
+std::vector<std::vector<int>> assign_q(const std::vector<double>& cost, int size) {
+  std::vector<int> order(cost.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
+  std::vector<double> load(size, 0.0);
+  std::vector<std::vector<int>> parts(size);
+  for (int i : order) {
+    int r = 0;
+    for (int t = 1; t < size; ++t)
+      if (load[t] < load[r]) r = t;
+    parts[r].push_back(i);
+    load[r] += cost[i];
+  }
+  for (auto& p : parts) std::sort(p.begin(), p.end());
+  return parts;
+}
+
+// kshard.shard_range: contiguous balanced [lo, hi) of `rank` among `size`
+void shard_range(long n, int rank, int size, long* lo, long* hi) {
+  const long base = n / size, rem = n % size;
+  *lo = rank * base + std::min<long>(rank, rem);
+  *hi = *lo + base + (rank < rem ? 1 : 0);
+}
+
+int comm_check(int rc, const char* what) {
+  FISDF_CHECK(rc == 0, std::string("build_sharded: the caller's ") + what + " failed");
+  return 0;
+}
+
+// fisdf_build (comm NULL) and fisdf_build_sharded: ISDF.build() (fftisdf.py:308-325 ->
+// build(df_obj), :22-128), the same stage sequence as the Python mirror's build (fisdf/isdf.py
+// build(): its unsharded branch, and its k-sharded branch with the caller's collectives)
+int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, const void* f,
+               int nao, const int kmesh[3], const int mesh[3], const double a[9],
+               const fisdf_build_opts* opts_in, int* h_nip) {
   fisdf_build_opts o;
   fisdf_build_opts_default(&o);
   if (opts_in) o = *opts_in;
@@ -2889,7 +2956,13 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
   const long ngrid = (long)mesh[0] * mesh[1] * mesh[2];
   FISDF_CHECK(ngrid < (1L << 31), "build: mesh too large");
-  FISDF_TRY(fisdf_set_factor_priority(c, 0));
+  const int NR = comm ? comm->size : 1, RK = comm ? comm->rank : 0;
+  if (comm)
+    FISDF_CHECK(NR >= 1 && RK >= 0 && RK < NR && comm->all_to_all && comm->reduce_scatter_f64 &&
+                    comm->allreduce_f64 && comm->broadcast,
+                "build_sharded: incomplete fisdf_comm");
+  // a k-shard's 1/N-grid y build is short, so its factor chain runs at the greatest priority
+  FISDF_TRY(fisdf_set_factor_priority(c, NR > 1 ? 1 : 0));
   // time reversal (X_{-k} = conj(X_k), real AOs): the selection Gram, x2_k (x4) and fx_k (y)
   // are formed for the representatives k <= -k only.  The inputs are checked on the side
   // stream beside the selection; a violation (complex basis, shifted k-mesh) is found when the
@@ -2943,40 +3016,147 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
   std::vector<double> wt;
   tr_classes(kmesh, tr, qs, partner, wt);
   const int nq = (int)qs.size();
-  // the factorisation (replaces zgelsy's QRCP, :108) on the side stream, overlapped with y
   FISDF_TRY(fisdf_set_pivoted_fit(c, o.pivoted_fit));
   FISDF_TRY(fisdf_set_fit_mode(c, o.fit_mode));
   FISDF_TRY(fisdf_set_half_grid(c, o.half_grid));
-  FISDF_TRY(fisdf_factor_x4_mark(c));
   FISDF_TRY(fisdf_set_omega(c, o.omega));
-  void* yT;
-  FISDF_TRY(build_alloc(c, BR_Y, sizeof(cplx) * (size_t)nq * nip * ngrid, &yT));
-  FISDF_TRY(fisdf_build_y_qs(c, f, ngrid * nao, 0, (int)ngrid, (int)ngrid, X, nip, nao, kmesh, a,
-                             qs.data(), nq, yT));                                  // :67-87
-  FISDF_TRY(fisdf_factor_x4_async(c, x4, qs.data(), nq, nip, o.fit_tol,
-                                  o.real_self_conjugate ? kmesh : nullptr));
-
-  void *Wq, *Ws;
-  FISDF_TRY(build_alloc(c, BR_WQ, sizeof(cplx) * (size_t)nq * nn, &Wq));
-  // the fit waits for the factor's verdict itself
-  FISDF_TRY(fisdf_fit_coulomb_qs(c, qs.data(), nq, yT, nip, mesh, kmesh, a, Wq));   // :97-121
-  std::vector<int> ranks(nq, 0);
-  FISDF_TRY(fisdf_factor_x4_wait(c, ranks.data()));
-
+  // this rank's q: the fitted q shared by cost, longest first (one GPU: all of them)
+  std::vector<double> cost(nq);
+  for (int i = 0; i < nq; ++i)
+    cost[i] = (o.real_self_conjugate && partner[qs[i]] == qs[i]) ? 0.6 : 1.0;
+  const std::vector<std::vector<int>> parts = assign_q(cost, NR);
+  std::vector<int> my_qs;
+  std::vector<double> my_wt;
+  for (int i : parts[RK]) my_qs.push_back(qs[i]), my_wt.push_back(wt[i]);
+  const int nmine = (int)my_qs.size();
+  void *Wq, *Ws, *W0;
+  std::vector<int> ranks(nmine, 0);
   int used = 0, ncod = 0;
-  FISDF_TRY(fisdf_factor_info(c, &used));
-  FISDF_TRY(fisdf_min_norm_info(c, &ncod));
-  // y is dead once the fit is enqueued: fit_coulomb_qs joined its lanes and FFT stream into
-  // c->stream, so the caller's stream-ordered free cannot overtake a reader
-  FISDF_TRY(build_return(c, yT));
-  FISDF_TRY(build_alloc(c, BR_WS, sizeof(double) * (size_t)nk * nn, &Ws));
-  FISDF_TRY(fisdf_build_ws_qs(c, Wq, qs.data(), wt.data(), nq, nip, kmesh, a, Ws)); // :204-207
+  long row0 = 0, row1 = nip;
+  if (!comm) {
+    // the factorisation (replaces zgelsy's QRCP, :108) on the side stream, overlapped with y
+    FISDF_TRY(fisdf_factor_x4_mark(c));
+    void* yT;
+    FISDF_TRY(build_alloc(c, BR_Y, sizeof(cplx) * (size_t)nq * nip * ngrid, &yT));
+    FISDF_TRY(fisdf_build_y_qs(c, f, ngrid * nao, 0, (int)ngrid, (int)ngrid, X, nip, nao, kmesh,
+                               a, qs.data(), nq, yT));                             // :67-87
+    FISDF_TRY(fisdf_factor_x4_async(c, x4, qs.data(), nq, nip, o.fit_tol,
+                                    o.real_self_conjugate ? kmesh : nullptr));
+    FISDF_TRY(build_alloc(c, BR_WQ, sizeof(cplx) * (size_t)nq * nn, &Wq));
+    // the fit waits for the factor's verdict itself
+    FISDF_TRY(fisdf_fit_coulomb_qs(c, qs.data(), nq, yT, nip, mesh, kmesh, a, Wq)); // :97-121
+    FISDF_TRY(fisdf_factor_x4_wait(c, ranks.data()));
+    FISDF_TRY(fisdf_factor_info(c, &used));
+    FISDF_TRY(fisdf_min_norm_info(c, &ncod));
+    // y is dead once the fit is enqueued: fit_coulomb_qs joined its lanes and FFT stream into
+    // c->stream (aux_join, checked by build_return), so a stream-ordered free cannot overtake a
+    // reader
+    FISDF_TRY(build_return(c, yT));
+    FISDF_TRY(build_alloc(c, BR_WS, sizeof(double) * (size_t)nk * nn, &Ws));
+    FISDF_TRY(fisdf_build_ws_qs(c, Wq, qs.data(), wt.data(), nq, nip, kmesh, a, Ws)); // :204-207
+    W0 = Wq;  // q = 0 is slot 0 (the smallest representative)
+  } else {
+    // y on this rank's plane-aligned grid slice for every fitted q (y_k = Phi^T (Phi fx_k)^2
+    // mixes all k at each grid point, :79-84), then one all-to-all per local q hands every rank
+    // its own q on the whole grid (kshard.exchange_y_chunked)
+    std::vector<long> g0s(NR), ngs(NR);
+    const long plane = (long)mesh[1] * mesh[2];
+    for (int r = 0; r < NR; ++r) {
+      long p0, p1;
+      shard_range(mesh[0], r, NR, &p0, &p1);
+      g0s[r] = p0 * plane;
+      ngs[r] = (p1 - p0) * plane;
+    }
+    const long ngme = ngs[RK];
+    if (nmine) FISDF_TRY(fisdf_factor_x4_mark(c));
+    void *send, *recv;
+    FISDF_TRY(build_alloc(c, BR_SEND, sizeof(cplx) * (size_t)nq * nip * std::max(ngme, 1L), &send));
+    if (ngme)
+      FISDF_TRY(fisdf_build_y_qs(c, (const cplx*)f + g0s[RK] * nao, ngrid * nao, 0, (int)ngme,
+                                 (int)ngme, X, nip, nao, kmesh, a, qs.data(), nq, send));
+    if (nmine)
+      FISDF_TRY(fisdf_factor_x4_async(c, x4, my_qs.data(), nmine, nip, o.fit_tol,
+                                      o.real_self_conjugate ? kmesh : nullptr));
+    FISDF_TRY(build_alloc(c, BR_Y, sizeof(cplx) * (size_t)std::max(nmine, 1) * nip * ngrid, &recv));
+    // the exchange runs on its own stream while this rank factorises and fits its earlier q
+    if (!c->comm_stream) {
+      FISDF_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+      FISDF_HIP(hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
+    }
+    FISDF_HIP(hipEventRecord(c->ev_comm, c->stream));
+    FISDF_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_comm, 0));
+    size_t nmax = 0;
+    for (const auto& p : parts) nmax = std::max(nmax, p.size());
+    std::vector<const void*> sp(NR);
+    std::vector<void*> rp(NR);
+    std::vector<size_t> sb(NR), rb(NR);
+    for (size_t j = 0; j < nmax; ++j) {
+      const bool mine = j < (size_t)nmine;
+      cplx* rj = (cplx*)recv + (long)j * nip * ngrid;
+      for (int r = 0; r < NR; ++r) {
+        const bool to_r = j < parts[r].size();
+        sp[r] = to_r ? (const cplx*)send + (long)parts[r][j] * nip * ngme : nullptr;
+        sb[r] = to_r ? sizeof(cplx) * (size_t)nip * ngme : 0;
+        // piece j = concat over ranks p of the (nip, ng_p) blocks: p's block at nip * g0_p
+        rp[r] = mine ? rj + (long)nip * g0s[r] : nullptr;
+        rb[r] = mine ? sizeof(cplx) * (size_t)nip * ngs[r] : 0;
+      }
+      FISDF_TRY(comm_check(comm->all_to_all(comm->user, sp.data(), sb.data(), rp.data(), rb.data(),
+                                            c->comm_stream), "all_to_all"));
+      if (mine)
+        FISDF_TRY(set_y_slices_on(c, (int)j, rj, NR, g0s.data(), ngs.data(), c->comm_stream));
+    }
+    FISDF_HIP(hipEventRecord(c->ev_comm, c->comm_stream));
+    FISDF_TRY(build_alloc(c, BR_WQ, sizeof(cplx) * (size_t)std::max(nmine, 1) * nn, &Wq));
+    if (nmine) {
+      // one call over the whole shard: its lanes start each q when that q's piece has landed
+      FISDF_TRY(fisdf_fit_coulomb_qs(c, my_qs.data(), nmine, nullptr, nip, mesh, kmesh, a, Wq));
+      FISDF_TRY(fisdf_factor_x4_wait(c, ranks.data()));
+      FISDF_TRY(fisdf_factor_info(c, &used));
+      FISDF_TRY(fisdf_min_norm_info(c, &ncod));
+    }
+    // the send and receive buffers stay the build's until the exchange is done
+    FISDF_HIP(hipStreamWaitEvent(c->stream, c->ev_comm, 0));
+    FISDF_TRY(build_return(c, recv));
+    FISDF_TRY(build_return(c, send));
+    // W_s = sqrt(nk) Re(sum_q Phi[R,q] W_q) (:204-207) mixes every rank's q: each rank forms every
+    // rank's interpolation-point row block of its partial sum, reduce-scattered by rows
+    std::vector<int> bounds(NR + 1);
+    long rmax = 0;
+    for (int r = 0; r < NR; ++r) {
+      long lo, hi;
+      shard_range(nip, r, NR, &lo, &hi);
+      bounds[r] = (int)lo;
+      bounds[r + 1] = (int)hi;
+      rmax = std::max(rmax, hi - lo);
+      if (r == RK) row0 = lo, row1 = hi;
+    }
+    const long chunk = (long)nk * std::max(rmax, 1L) * nip;
+    void* Wsb;
+    FISDF_TRY(build_alloc(c, BR_WSB, sizeof(double) * (size_t)chunk * NR, &Wsb));
+    FISDF_HIP(hipMemsetAsync(Wsb, 0, sizeof(double) * (size_t)chunk * NR, c->stream));
+    FISDF_TRY(fisdf_build_ws_blocks(c, Wq, my_qs.data(), my_wt.data(), nmine, nip, kmesh, a, NR,
+                                    bounds.data(), chunk, Wsb));
+    FISDF_TRY(build_alloc(c, BR_WS, sizeof(double) * (size_t)chunk, &Ws));
+    FISDF_TRY(comm_check(comm->reduce_scatter_f64(comm->user, (const double*)Wsb, (double*)Ws,
+                                                  (size_t)chunk, c->stream), "reduce_scatter_f64"));
+    FISDF_TRY(build_return(c, Wsb));
+    // W_0 for get_j (:159) from the rank fitting q = 0 (position 0 of the fit order, its slot 0)
+    int owner0 = 0;
+    for (int r = 0; r < NR; ++r)
+      if (!parts[r].empty() && parts[r][0] == 0) owner0 = r;
+    FISDF_TRY(build_alloc(c, BR_W0, sizeof(cplx) * (size_t)nn, &W0));
+    if (RK == owner0)
+      FISDF_HIP(hipMemcpyAsync(W0, Wq, sizeof(cplx) * nn, hipMemcpyDeviceToDevice, c->stream));
+    FISDF_TRY(comm_check(comm->broadcast(comm->user, W0, sizeof(cplx) * nn, owner0, c->stream),
+                         "broadcast"));
+  }
   B.valid = true;
   B.nk = nk;
   B.nip = nip;
   B.nao = nao;
   B.ng0 = ng0;
-  B.nfit = nq;
+  B.nfit = nmine;
   B.used_pivoted = used;
   B.min_norm = ncod;
   B.time_reversal = tr ? 1 : 0;
@@ -2984,16 +3164,41 @@ int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, c
   for (int i = 0; i < 3; ++i) B.kmesh[i] = kmesh[i], B.mesh[i] = mesh[i];
   for (int i = 0; i < 9; ++i) B.a[i] = a[i];
   B.perm = perm;
-  B.fit_qs = qs;
+  B.fit_qs = my_qs;
   B.partner = partner;
   B.ranks = ranks;
-  B.wt = wt;
+  B.wt = my_wt;
   B.X = X;
   B.x4 = x4;
   B.Wq = Wq;
   B.Ws = Ws;
+  B.W0 = W0;
+  B.sharded = comm != nullptr;
+  if (comm) B.comm = *comm;
+  B.shard_rank = RK;
+  B.shard_size = NR;
+  B.row0 = (int)row0;
+  B.row1 = (int)row1;
   if (h_nip) *h_nip = nip;
   return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fisdf_build(fisdf_ctx* c, const void* x0, int ng0, const void* f, int nao, const int kmesh[3],
+                const int mesh[3], const double a[9], const fisdf_build_opts* opts, int* h_nip) {
+  FISDF_TRY(device_guard(c));
+  return build_impl(c, nullptr, x0, ng0, f, nao, kmesh, mesh, a, opts, h_nip);
+}
+
+int fisdf_build_sharded(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0,
+                        const void* f, int nao, const int kmesh[3], const int mesh[3],
+                        const double a[9], const fisdf_build_opts* opts, int* h_nip) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(comm != nullptr, "build_sharded: comm is null (fisdf_build is the 1-GPU build)");
+  return build_impl(c, comm, x0, ng0, f, nao, kmesh, mesh, a, opts, h_nip);
 }
 
 int fisdf_build_get(fisdf_ctx* c, fisdf_build_result* out) {
@@ -3017,6 +3222,11 @@ int fisdf_build_get(fisdf_ctx* c, fisdf_build_result* out) {
   out->d_Ws = B.Ws;
   out->time_reversal = B.time_reversal;
   out->tr_deviation = B.tr_deviation;
+  out->shard_rank = B.shard_rank;
+  out->shard_size = B.shard_size;
+  out->row0 = B.row0;
+  out->row1 = B.row1;
+  out->d_W0 = B.W0;
   return 0;
 }
 
@@ -3031,13 +3241,15 @@ int fisdf_get_w0(fisdf_ctx* c, void* h_w0) {
   FISDF_TRY(device_guard(c));
   FISDF_CHECK(c->bld.valid && h_w0, "get_w0: no build or null output");
   const auto& B = c->bld;  // q = 0 is always fitted (slot 0: the smallest representative)
-  return fisdf_memcpy_dtoh(c, h_w0, B.Wq, sizeof(cplx) * (size_t)B.nip * B.nip);
+  return fisdf_memcpy_dtoh(c, h_w0, B.W0, sizeof(cplx) * (size_t)B.nip * B.nip);
 }
 
 int fisdf_get_wq(fisdf_ctx* c, void* h_wq) {
   FISDF_TRY(device_guard(c));
   FISDF_CHECK(c->bld.valid && h_wq, "get_wq: no build or null output");
   const auto& B = c->bld;
+  FISDF_CHECK(B.shard_size == 1, "get_wq: the W_q of a sharded build are distributed over the "
+                                 "ranks (fisdf_build_get: this rank's fit_qs and d_Wq)");
   const size_t nn = (size_t)B.nip * B.nip;
   cplx* h = (cplx*)h_wq;
   std::vector<int> slot(B.nk, -1);
@@ -3062,10 +3274,27 @@ int fisdf_get_jk(fisdf_ctx* c, const void* dms, int nset, int with_j, int with_k
   FISDF_CHECK(B.valid, "get_jk: no build (call fisdf_build first)");
   FISDF_CHECK(dms && nset > 0, "get_jk: no density matrices");
   FISDF_CHECK((!with_j || vj) && (!with_k || vk), "get_jk: missing output");
-  if (with_k)
-    FISDF_TRY(fisdf_get_k_rows(c, B.X, B.Ws, dms, nset, B.nip, B.nao, B.kmesh, B.a, 0, B.nip, vk));
-  if (with_j)
-    FISDF_TRY(fisdf_get_j_rows(c, B.X, B.Wq, dms, nset, B.nk, B.nip, B.nao, 0, B.nip, vj));
+  if (!B.sharded) {
+    if (with_k)
+      FISDF_TRY(fisdf_get_k_rows(c, B.X, B.Ws, dms, nset, B.nip, B.nao, B.kmesh, B.a, 0, B.nip, vk));
+    if (with_j)
+      FISDF_TRY(fisdf_get_j_rows(c, B.X, B.W0, dms, nset, B.nk, B.nip, B.nao, 0, B.nip, vj));
+    return 0;
+  }
+  // sharded: this rank's interpolation-point rows (its W_s rows), then the sums over the ranks
+  // (fftisdf.py:166,225 contract over all points)
+  const size_t nv = 2 * (size_t)nset * B.nk * B.nao * B.nao;
+  if (with_k) {
+    FISDF_TRY(fisdf_get_k_rows_local(c, B.X, B.Ws, dms, nset, B.nip, B.nao, B.kmesh, B.a, B.row0,
+                                     B.row1, vk));
+    FISDF_TRY(comm_check(B.comm.allreduce_f64(B.comm.user, (double*)vk, nv, c->stream),
+                         "allreduce_f64"));
+  }
+  if (with_j) {
+    FISDF_TRY(fisdf_get_j_rows(c, B.X, B.W0, dms, nset, B.nk, B.nip, B.nao, B.row0, B.row1, vj));
+    FISDF_TRY(comm_check(B.comm.allreduce_f64(B.comm.user, (double*)vj, nv, c->stream),
+                         "allreduce_f64"));
+  }
   return 0;
 }
 

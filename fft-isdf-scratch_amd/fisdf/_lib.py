@@ -108,10 +108,15 @@ _SIGS = {
     "fisdf_get_jk": ([_vp, _vp, _i, _i, _i, _vp, _vp], _i),
     "fisdf_set_allocator": ([_vp, _vp, _vp, _vp], _i),
     "fisdf_check_time_reversal": ([_vp, _vp, _l, _l, _ip, _dp], _i),
+    # k-sharded composite build with the caller's collectives
+    "fisdf_build_sharded": ([_vp, _vp, _vp, _i, _vp, _i, _ip, _ip, _dp, _vp, _ip], _i),
+    "fisdf_comm_rccl_unique_id": ([_vp], _i),
+    "fisdf_comm_rccl_init": ([_vp, _i, _i, _i, _vp], _i),
+    "fisdf_comm_rccl_destroy": ([_vp], _i),
 }
 
 # FISDF_ABI_VERSION of include/fisdf.h this binding's structs follow
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class BuildOpts(C.Structure):
@@ -126,7 +131,25 @@ class BuildResult(C.Structure):
     _fields_ = [("nk", _i), ("nip", _i), ("nao", _i), ("nfit", _i), ("used_pivoted_fit", _i),
                 ("min_norm_slots", _i), ("perm", _ip), ("fit_qs", _ip), ("ranks", _ip),
                 ("partner", _ip), ("d_X", _vp), ("d_x4", _vp), ("d_Wq", _vp), ("d_Ws", _vp),
-                ("time_reversal", _i), ("tr_deviation", _d)]
+                ("time_reversal", _i), ("tr_deviation", _d), ("shard_rank", _i),
+                ("shard_size", _i), ("row0", _i), ("row1", _i), ("d_W0", _vp)]
+
+
+# struct fisdf_comm: the caller's collectives of fisdf_build_sharded (device pointers, enqueued
+# stream-ordered on the hipStream_t they are given)
+ALL_TO_ALL_FN = C.CFUNCTYPE(_i, _vp, C.POINTER(_vp), C.POINTER(C.c_size_t), C.POINTER(_vp),
+                            C.POINTER(C.c_size_t), _vp)
+REDUCE_SCATTER_FN = C.CFUNCTYPE(_i, _vp, _vp, _vp, C.c_size_t, _vp)
+ALLREDUCE_FN = C.CFUNCTYPE(_i, _vp, _vp, C.c_size_t, _vp)
+BROADCAST_FN = C.CFUNCTYPE(_i, _vp, _vp, C.c_size_t, _i, _vp)
+COMM_ID_BYTES = 128
+
+
+class Comm(C.Structure):
+    """struct fisdf_comm (include/fisdf.h)."""
+    _fields_ = [("rank", _i), ("size", _i), ("user", _vp), ("all_to_all", ALL_TO_ALL_FN),
+                ("reduce_scatter_f64", REDUCE_SCATTER_FN), ("allreduce_f64", ALLREDUCE_FN),
+                ("broadcast", BROADCAST_FN)]
 
 
 # fisdf_alloc_fn / fisdf_free_fn

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FISDF_ABI_VERSION 3
+#define FISDF_ABI_VERSION 4
 
 typedef struct fisdf_ctx fisdf_ctx;
 
@@ -116,6 +116,13 @@ typedef struct fisdf_build_result {
   int time_reversal;          /* 1: one q of each (q, -q) pair fitted, W_{-q} = conj(W_q); 0: every
                                  q fitted (asked for, or the inputs failed the check below) */
   double tr_deviation;        /* max |a[-k] - conj(a[k])| / max |a| over x0 and f (0 unchecked) */
+  /* k-sharded build (fisdf_build_sharded): this rank's share.  nfit / fit_qs / ranks / d_Wq are
+   * the rank's own q; d_Ws holds only interpolation-point rows [row0, row1) of every W_s[R],
+   * (nk, row1 - row0, nip) float64; d_W0 is W_0 (broadcast from its owner).  One GPU: rank 0 of
+   * 1, rows [0, nip), d_W0 = slot 0 of d_Wq. */
+  int shard_rank, shard_size;
+  int row0, row1;
+  const void* d_W0;           /* (nip, nip) c128 */
 } fisdf_build_result;
 int fisdf_build_get(fisdf_ctx* ctx, fisdf_build_result* out);
 /* Time-reversal check of Bloch AO values d_a[k][per_k] (k stride k_stride elements, get_kpts
@@ -125,8 +132,53 @@ int fisdf_check_time_reversal(fisdf_ctx* ctx, const void* d_a, long k_stride, lo
                               const int kmesh[3], double* h_out);
 int fisdf_build_release(fisdf_ctx* ctx);
 
+/* ---- k-sharded composite build over several GPUs -----------------------------
+ * One process (or thread) per GPU, each with its own context, all calling fisdf_build_sharded
+ * with the same inputs and options (the Python mirror's torch.distributed build, fisdf/isdf.py
+ * build(), in C).  The fitted q are shared by cost, longest first (a self-conjugate q 0.6 of a
+ * complex one); the selection and x4 are replicated (identical pivots on every rank, no
+ * collective); y is built on the rank's plane-aligned grid slice for every fitted q and
+ * exchanged with one all-to-all per local q (each q's fit starts when its piece has landed);
+ * W_s row blocks are reduce-scattered; W_0 is broadcast from the rank fitting q = 0.  W_q of a
+ * rank equals the 1-GPU build's bit for bit.  fisdf_get_jk on a sharded build contracts the
+ * rank's interpolation-point rows and all-reduces J and K (every rank gets the whole result).
+ *
+ * The collectives come from the caller (MPI, RCCL, a framework's process group) through
+ * fisdf_comm; each is enqueued stream-ordered on `stream` (a hipStream_t): it may return before
+ * the transfer is done, as long as work enqueued on `stream` afterwards sees the result.  Device
+ * pointers throughout; zero-byte entries are allowed.  Return 0, or non-zero on failure. */
+typedef struct fisdf_comm {
+  int rank, size;
+  void* user;
+  /* send d_send[r] (send_bytes[r]) to rank r and receive d_recv[r] (recv_bytes[r]) from rank r,
+   * for every r (self included) */
+  int (*all_to_all)(void* user, const void* const* d_send, const size_t* send_bytes,
+                    void* const* d_recv, const size_t* recv_bytes, void* stream);
+  /* d_recv[i] = sum over ranks of d_send[rank * count + i], i < count */
+  int (*reduce_scatter_f64)(void* user, const double* d_send, double* d_recv, size_t count,
+                            void* stream);
+  /* in place: d_buf[i] = sum over ranks of d_buf[i] */
+  int (*allreduce_f64)(void* user, double* d_buf, size_t count, void* stream);
+  /* in place: d_buf of rank `root` to every rank */
+  int (*broadcast)(void* user, void* d_buf, size_t bytes, int root, void* stream);
+} fisdf_comm;
+/* The build of one rank.  `comm` must stay valid while the build's results are used
+ * (fisdf_get_jk all-reduces through it).  Arguments otherwise as fisdf_build. */
+int fisdf_build_sharded(fisdf_ctx* ctx, const fisdf_comm* comm, const void* d_x0, int ng0,
+                        const void* d_f, int nao, const int kmesh[3], const int mesh[3],
+                        const double a[9], const fisdf_build_opts* opts, int* h_nip);
+/* A fisdf_comm over RCCL (librccl, loaded at run time): rank 0 makes the id, the caller hands it
+ * to every rank (MPI_Bcast, a file, a TCP store), each rank then joins on its own GPU.  The
+ * collectives run on the stream they are given, over xGMI within a node. */
+#define FISDF_COMM_ID_BYTES 128
+int fisdf_comm_rccl_unique_id(unsigned char h_id[FISDF_COMM_ID_BYTES]);
+int fisdf_comm_rccl_init(const unsigned char h_id[FISDF_COMM_ID_BYTES], int rank, int size,
+                         int device, fisdf_comm* out);
+int fisdf_comm_rccl_destroy(fisdf_comm* comm);
+
 /* Host copies of the reference's attributes (fftisdf.py:125-128): h_x (nk, nip, nao) = _x,
- * h_w0 (nip, nip) = _w0, h_wq (nk, nip, nip) = _wq (unfitted q filled as conj(W_{-q})).
+ * h_w0 (nip, nip) = _w0, h_wq (nk, nip, nip) = _wq (unfitted q filled as conj(W_{-q}); not on a
+ * sharded build of several ranks, whose W_q are distributed: fisdf_build_get per rank).
  * synchronous. */
 int fisdf_get_x(fisdf_ctx* ctx, void* h_x);
 int fisdf_get_w0(fisdf_ctx* ctx, void* h_w0);
@@ -135,6 +187,8 @@ int fisdf_get_wq(fisdf_ctx* ctx, void* h_wq);
 /* get_jk of the last build (fftisdf.py:390-408 -> get_k_kpts :173-228, then get_j_kpts
  * :133-171): d_dms (nset, nk, nao, nao) c128 device; d_vj / d_vk same shape (either may be NULL
  * when with_j / with_k is 0).  J is complex: a Gamma-only caller takes .real (:169-170).
+ * After fisdf_build_sharded every rank calls it with the same d_dms: each contracts its own
+ * interpolation-point rows and J / K are all-reduced through the build's fisdf_comm.
  * asynchronous. */
 int fisdf_get_jk(fisdf_ctx* ctx, const void* d_dms, int nset, int with_j, int with_k, void* d_vj,
                  void* d_vk);

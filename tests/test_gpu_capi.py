@@ -59,3 +59,52 @@ def test_capi_build_get_jk_torch_free(name):
     for q in range(nk):
         if partner[q] != q:
             assert np.array_equal(o["wq"][partner[q]], o["wq"][q].conj())
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode,size,name", [("host", 2, "toy222"), ("host", 3, "toy331_fr"),
+                                            ("rccl", 1, "toy222")])
+def test_capi_build_sharded(mode, size, name):
+    """fisdf_build_sharded (SURVEY §8(e) through the C-ABI, no torch): SIZE ranks on GPU 0
+    (tests/capi_shard_worker.py), the collectives from the caller (host: a file mailbox per
+    collective, uneven q shares at 3 ranks; rccl: the library's RCCL fisdf_comm on a 1-rank
+    communicator).  Every rank's W_q equal the 1-GPU build's bit for bit, every rank holds W_0,
+    the W_s row blocks are the 1-GPU W_s rows, and the all-reduced J/K of every rank equal the
+    1-GPU get_jk to rounding."""
+    with tempfile.TemporaryDirectory() as tmp:
+        procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "capi_shard_worker.py"), name,
+                                   str(r), str(size), tmp, mode]) for r in range(size)]
+        rcs = []
+        for p in procs:
+            try:
+                rcs.append(p.wait(timeout=240))
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+        assert rcs == [0] * size, rcs
+        outs = [dict(np.load(os.path.join(tmp, f"rank{r}.npz"))) for r in range(size)]
+    ref = outs[0]
+    qs = np.concatenate([o["fit_qs"] for o in outs])
+    assert sorted(qs.tolist()) == ref["ref_fit_qs"].tolist()
+    slot = {int(q): i for i, q in enumerate(ref["ref_fit_qs"])}
+    lo = 0
+    for r, o in enumerate(outs):
+        assert np.array_equal(o["perm"], ref["perm"])              # replicated selection
+        for i, q in enumerate(o["fit_qs"]):
+            assert np.array_equal(o["wq"][i], ref["ref_wq"][slot[int(q)]]), (r, q)
+        assert np.array_equal(o["w0"], ref["ref_wq"][0])
+        i0, i1 = o["rows"]
+        assert i0 == lo
+        lo = i1
+        dws = abs(o["ws_rows"] - ref["ref_ws"][:, i0:i1]).max()
+        assert dws < 1e-12 * max(1.0, abs(ref["ref_ws"]).max()), dws
+        dj, dk = abs(o["vj"] - ref["ref_vj"]).max(), abs(o["vk"] - ref["ref_vk"]).max()
+        print(f"\n{name} {mode} rank {r}/{size}: q {o['fit_qs'].tolist()} rows [{i0}, {i1}) "
+              f"|dWs| {dws:.1e} |dJ| {dj:.1e} |dK| {dk:.1e} vs the 1-GPU build")
+        assert dj < 1e-11 and dk < 1e-11
+        assert np.array_equal(o["vj"], outs[0]["vj"]) and np.array_equal(o["vk"], outs[0]["vk"])
+        if mode == "host":   # a2a per local q, one reduce-scatter, one broadcast, J + K
+            n_a2a = max(len(x["fit_qs"]) for x in outs)
+            assert o["calls"].tolist() == [n_a2a, 2, 1, 1], o["calls"]  # sorted names
+    assert lo == ref["perm"].size

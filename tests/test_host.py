@@ -28,7 +28,7 @@ def test_library_exports_header_symbols():
         assert hasattr(lib, s), s
     # and the ctypes signature table covers the whole header
     assert set(syms) == set(_lib._SIGS), set(syms) ^ set(_lib._SIGS)
-    assert lib.fisdf_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.fisdf_abi_version() == _lib.ABI_VERSION == 4
     # no GPU here: fisdf_create fails and its message is the thread's last error (ctx NULL)
     import ctypes as C
     import torch
