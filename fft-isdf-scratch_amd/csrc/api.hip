@@ -43,6 +43,14 @@ LaunchEvents& launch_events() {
 
 using namespace fisdf;
 
+// default relative pivot cut of the x4_q factorisation (fisdf_build_opts.fit_tol, the rank of a
+// rank-deficient x4_q): 4.2e-15 ~ 19 eps is where the pivoted Cholesky's ranks reproduce gelsy's
+// (fftisdf.py:108: QRCP + incremental condition estimate at rcond = eps) in the reference demo's
+// regime (C2 at c0 = 1e4, every x4_q rank-deficient): per-q ranks 0-13 from gelsy's, J/K within
+// 0.78 / 0.71 of gelsy's own rcond band; the round-4 cut 1e-14 sat 27-37 ranks below it, at
+// 1.38 / 0.97 of the band (tests/experiments/rank_rule_c2.py, profiles/r05/rank_regime/)
+constexpr double kFitTolDefault = 4.2e-15;
+
 struct fisdf_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -76,7 +84,7 @@ struct fisdf_ctx {
   int* f_fail_pinned = nullptr;  // unpivoted path: per-slot failure flags (host, pinned)
   int* f_qr_pinned = nullptr;    // factored q-list + real flags (2 nk ints, pinned) and device copy
   int* f_qr_dev = nullptr;
-  double f_tol = 1e-14;
+  double f_tol = kFitTolDefault;
   bool f_check_fail = false, f_used_pivoted = false;
   int f_cap_nk = 0, f_cap_nip = 0;  // shape the factor buffers were allocated for
   int force_pivoted = -1;  // fisdf_set_pivoted_fit; -1: environment FISDF_PIVOTED_FIT
@@ -2868,7 +2876,7 @@ void fisdf_build_opts_default(fisdf_build_opts* o) {
   o->perm = nullptr;
   o->n_perm = 0;
   o->fit_mode = FISDF_FIT_LSTSQ;
-  o->fit_tol = 1e-14;
+  o->fit_tol = kFitTolDefault;
   o->pivoted_fit = -1;
   o->half_grid = -1;
   o->time_reversal = 1;

@@ -115,7 +115,8 @@ class InterpolativeSeparableDensityFitting:
     _w0 = None
     _wq = None
     blksize = 8000          # fftisdf.py:300
-    fit_tol = 1e-14         # relative pivot cut of the x4_q factorisation
+    fit_tol = 4.2e-15       # relative pivot cut of the x4_q factorisation: where
+                            # its ranks reproduce gelsy's at rcond = eps (fftisdf.py:108)
     select_tol = -1.0       # dpstrf default tolerance (ng0*eps*max diag)
     # cap on the number of interpolation points; None -> int(nao * c0) (fftisdf.py:383);
     # the get_coul drivers set it directly (fftdf-with-k-lstsq.py:71, fftdf-with-k.py:64)

@@ -78,7 +78,8 @@ typedef struct fisdf_build_opts {
   const int* perm;         /* host, n_perm parent-grid indices: use these points, no selection */
   int n_perm;              /*   (ISDF.set_interpolation_points / a refit on the same points)     */
   int fit_mode;            /* FISDF_FIT_LSTSQ (gelsy semantics, default), _SVD, _BASIC */
-  double fit_tol;          /* relative pivot cut of the x4_q factorisation (1e-14) */
+  double fit_tol;          /* relative pivot cut of the x4_q factorisation (4.2e-15: gelsy's rank
+                              decision at rcond = eps, fftisdf.py:108) */
   int pivoted_fit;         /* -1 default (fisdf_set_pivoted_fit), 0, 1 */
   int half_grid;           /* -1 default (fisdf_set_half_grid), 0, 1 */
   int time_reversal;       /* 1: fit one q of each (q, -q) pair, W_{-q} = conj(W_q) (default);

@@ -6,6 +6,7 @@ the Cholesky cuts and a condition-number rule on the Cholesky factor, then J/K o
 at (a) gelsy's own per-q rank and (b) each rule, against gelsy at its default rcond.  CPU only.
 
   python tests/experiments/rank_rule_c2.py
+  python tests/experiments/rank_rule_c2.py --gpu OUT.npz   (tools/rank_regime_gpu.py's builds)
 """
 import os
 import sys
@@ -61,7 +62,50 @@ def cond_rank(L, bound, lo, hi):
     return lo
 
 
+def gpu_compare(path):
+    """J/K of GPU builds at several fit_tol cuts (tools/rank_regime_gpu.py) against gelsy at its
+    default rcond and gelsy's own rcond band (4 eps, eps / 4), on the GPU's points."""
+    g = dict(np.load(path))
+    cell, kmesh, m0, c0, x0, chi, dm = bench.setup("c2")
+    dms = dm[None]
+    perm = g["perm"]
+    xip = x0[:, perm]
+    kpts = R.get_kpts(cell.a, kmesh)
+    phase = R.get_phase(cell.a, kpts, kmesh)
+    x4 = R.build_x4(xip, phase)
+    coords = cell.gen_uniform_grids(cell.mesh)
+    mesh, vol, N = cell.mesh, cell.vol, coords.shape[0]
+    Gv = R.get_Gv(cell.a, mesh)
+    y_all = np.empty((len(kpts), N, len(perm)), complex)
+    for g0 in range(0, N, 8000):
+        y_all[:, g0:g0 + 8000] = R.build_y(chi[:, g0:g0 + 8000], xip, phase)
+    res = {}
+    for tag, cond in (("gelsy", None), ("gelsy x4", 4 * EPS), ("gelsy /4", EPS / 4)):
+        ws, rs = [], []
+        for q, vq in enumerate(kpts):
+            fq = np.exp(-1j * coords @ vq)
+            z, _, r, _ = sl.lstsq(x4[q], y_all[q].T, cond=cond, lapack_driver="gelsy")
+            zeta = R.fft(z * fq, mesh) * R.get_coulG(cell.a, vq, mesh, Gv=Gv) * (vol / N)
+            ws.append((R.ifft(zeta, mesh) * fq.conj()) @ z.conj().T)
+            rs.append(r)
+        w = np.asarray(ws)
+        res[tag] = (R.get_j_kpts(xip, w[0], dms)[0], R.get_k_kpts(xip, w, dms, phase)[0], rs)
+        print(f"  {tag:9s} ranks {rs}", flush=True)
+    vj0, vk0, _ = res["gelsy"]
+    bj = max(abs(res[t][0] - vj0).max() for t in ("gelsy x4", "gelsy /4"))
+    bk = max(abs(res[t][1] - vk0).max() for t in ("gelsy x4", "gelsy /4"))
+    print(f"  gelsy's own rcond band |dJ| {bj:.2e} |dK| {bk:.2e}  (nip {len(perm)})")
+    for tol in g["tols"]:
+        tag = f"{tol:.1e}"
+        ej = abs(g[f"vj_{tag}"] - vj0).max()
+        ek = abs(g[f"vk_{tag}"] - vk0).max()
+        print(f"  GPU fit_tol {tag} ranks {g[f'ranks_{tag}'].tolist()}: vs gelsy |dJ| {ej:.2e} "
+              f"({ej / bj:.2f} band) |dK| {ek:.2e} ({ek / bk:.2f} band)", flush=True)
+
+
 def main():
+    if len(sys.argv) > 2 and sys.argv[1] == "--gpu":
+        return gpu_compare(sys.argv[2])
     cell, kmesh, m0, c0, x0, chi, dm = bench.setup("c2")
     dms = dm[None]
     perm, rank, nip, _ = R.select_interpolation_points(x0, cell.nao_nr(), 1e4)

@@ -196,8 +196,11 @@ def test_min_norm_fit_full_size_rank_regime():
     §3.4).  Here the reference's own answer is only defined to the level its solver moves under
     a change of rcond: gelsy at 4x and 1/4x its default rcond differs from itself by ~1.5e-7 Ha
     (J) / ~2.5e-8 (K) (tests/experiments/rank_regime_c2.py, profiles/r03_rank_regime_c2.log),
-    above the 1e-8 bar.  Asserted: the GPU's J/K sit within 2x of that band around gelsy at its
-    default rcond, on the GPU's points."""
+    above the 1e-8 bar.  The fit's rank cut (fit_tol 4.2e-15) is the one whose ranks follow
+    gelsy's here (tests/experiments/rank_rule_c2.py).  Asserted: the GPU's J/K sit inside that band
+    around gelsy at its default rcond (1x; round 4's 1e-14 cut needed 1.4x), on the GPU's points;
+    the measured |dJ| / |dK| are printed against the 1e-8 bar, which no solver other than gelsy
+    itself meets in this regime."""
     df, cell, kmesh, x0, chi, dm, vj, vk, mi = _gpu_build("c2", c0=1e4)
     ng0 = x0.shape[1]
     print(f"\nc2 rank regime: nip {df.nip} (parent grid {ng0}), x4_q ranks "
@@ -217,10 +220,10 @@ def test_min_norm_fit_full_size_rank_regime():
               f"(ranks {min(r0)}-{max(r0)}): |dJ| {abs(vj1 - vj0).max():.2e} "
               f"|dK| {abs(vk1 - vk0).max():.2e}", flush=True)
     ej, ek = abs(vj - vj0).max(), abs(vk - vk0).max()
-    print(f"c2 rank regime: GPU vs gelsy: |dJ| {ej:.2e} |dK| {ek:.2e}; gelsy's own rcond band "
-          f"|dJ| {band_j:.2e} |dK| {band_k:.2e} (margins {2 * band_j / ej:.1f}x / "
-          f"{2 * band_k / ek:.1f}x; oracle {time.perf_counter() - t0:.1f} s)", flush=True)
-    assert ej <= 2 * band_j and ek <= 2 * band_k
+    print(f"c2 rank regime: GPU vs gelsy: |dJ| {ej:.2e} |dK| {ek:.2e} (bar 1e-8); gelsy's own "
+          f"rcond band |dJ| {band_j:.2e} |dK| {band_k:.2e} (GPU at {ej / band_j:.2f} / "
+          f"{ek / band_k:.2f} of the band; oracle {time.perf_counter() - t0:.1f} s)", flush=True)
+    assert ej <= band_j and ek <= band_k
 
 
 # C2 / C3 with the second C moved off its symmetric site (Angstrom): no symmetry maps the parent
