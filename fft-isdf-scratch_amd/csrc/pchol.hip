@@ -616,8 +616,10 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
     const double dp = s_dp;
     if (pr) prof[4L * j + 1] = __builtin_amdgcn_s_memrealtime();
     // ---- gather ----
+#ifndef FISDF_EXP_NOGATHER  // timing experiment only (stale pivot row)
     for (int c = tid; c < j; c += SC_THREADS)
       Lp[c] = __hip_atomic_load(&Lg[(long)p * rmax + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     for (int r = tid; r < nr; r += SC_THREADS) {
       const double x = X2[(long)p * n + r0 + r].x;
       w0[r] = x * x * scale;
@@ -657,7 +659,9 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
           }
           if (j < K) Lr[(long)r * K + j] = l;
           __hip_atomic_store(&Lg[(long)i * rmax + j], l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifndef FISDF_EXP_NOSTOREWAIT  // timing experiment only (breaks the hand-off)
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         }
       }
     }
@@ -1480,7 +1484,9 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
   const int kcap = ek ? atoi(ek) : 0;
   constexpr size_t kLds = 150 * 1024;
   // 128 workgroups: the per-pivot time is flat from 128 to 256 (cross-XCD round trips)
-  int G = std::min({128, ncu, (n + 7) / 8});
+  // FISDF_SEL_WGS=g caps the grid (experiments: the exchange's cost against its poller count)
+  const char* eg = getenv("FISDF_SEL_WGS");
+  int G = std::min({eg ? std::max(1, atoi(eg)) : 128, ncu, (n + 7) / 8});
   if (G < 1) return 0;
   int RW = (n + G - 1) / G;
   G = (n + RW - 1) / RW;

@@ -19,5 +19,5 @@ for s in api zgemm zgemm_wide fft pchol linalg ao; do
     OBJS="$OBJS $s.o"
   fi
 done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OBJS -o ../fisdf/libfisdf_$NAME.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OBJS -ldl -o ../fisdf/libfisdf_$NAME.so
 echo "built fisdf/libfisdf_$NAME.so ($FL on $SRCS)"

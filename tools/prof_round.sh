@@ -4,10 +4,11 @@
 # step is left out, so the CSV's per-step kernel time matches the bench's roofline), and
 # FETCH_SIZE / WRITE_SIZE passes (separate runs) for the roofline kernels' HBM traffic.
 #   bash tools/prof_round.sh TAG
-# rocprofv3-profiled processes may SIGSEGV in their exit handlers after the tool has written its
-# files: torch's bundled libamdhip64 tears down into the system libhsa-runtime64 that
-# rocprofiler-sdk loaded (symbolized in profiles/r03_prof_v5/exit_crash_stack.txt).
-# Each pass is therefore judged by its output files; a timeout (124/137) still stops the script.
+# rocprofv3-profiled processes SIGSEGV in their exit handlers after the tool has written its
+# files: ROCm 7.2's teardown of the state a cooperative launch (the selection kernel) leaves,
+# under rocprofiler-sdk — a HIP program with one cooperative launch and nothing else does the same
+# (profiles/r05/rocprof_exit/README.txt).  Each pass is therefore judged by its output
+# files; a timeout (124/137) still stops the script.
 set -o pipefail
 TAG=${1:-prof}
 OUT=gpurun_out/$TAG
