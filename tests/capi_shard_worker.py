@@ -9,7 +9,9 @@ its stream, moves its pieces through host files and uploads what it receives (ra
 GPU, as a test; RCCL refuses two ranks on one device).  "rccl": the library's own RCCL
 fisdf_comm (fisdf_comm_rccl_*), rank 0 writing the unique id to DIR/id.bin.
 
-usage: python capi_shard_worker.py CASE RANK SIZE DIR host|rccl
+usage: python capi_shard_worker.py CASE RANK SIZE DIR host|rccl [VARIANT]
+  VARIANT: "" (defaults), "svd" (fit_mode FISDF_FIT_SVD: the minimum-norm operator on every q),
+  "notr" (time_reversal 0: every q fitted, weights 1)
 """
 import ctypes as C
 import os
@@ -128,7 +130,7 @@ class FileComm:
         return c
 
 
-def main(case, rank, size, d, mode):
+def main(case, rank, size, d, mode, variant=""):
     from cases import inputs
     cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(case)
     nao = cell.nao_nr()
@@ -170,6 +172,12 @@ def main(case, rank, size, d, mode):
     opts = _lib.BuildOpts()
     lib.fisdf_build_opts_default(C.byref(opts))
     opts.nip_max = int(nao * c0)                                           # fftisdf.py:383
+    if variant == "svd":
+        opts.fit_mode = 1
+    elif variant == "notr":
+        opts.time_reversal = 0
+    elif variant:
+        raise ValueError(variant)
 
     if mode == "rccl":
         idf = os.path.join(d, "id.bin")
@@ -244,4 +252,5 @@ def main(case, rank, size, d, mode):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5])
+    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5],
+         sys.argv[6] if len(sys.argv) > 6 else "")

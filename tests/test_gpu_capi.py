@@ -62,18 +62,20 @@ def test_capi_build_get_jk_torch_free(name):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("mode,size,name", [("host", 2, "toy222"), ("host", 3, "toy331_fr"),
-                                            ("rccl", 1, "toy222")])
-def test_capi_build_sharded(mode, size, name):
+@pytest.mark.parametrize("mode,size,name,variant", [
+    ("host", 2, "toy222", ""), ("host", 3, "toy331_fr", ""), ("rccl", 1, "toy222", ""),
+    ("host", 2, "toy331_fr", "svd"), ("host", 3, "toy222", "notr")])
+def test_capi_build_sharded(mode, size, name, variant):
     """fisdf_build_sharded (SURVEY §8(e) through the C-ABI, no torch): SIZE ranks on GPU 0
     (tests/capi_shard_worker.py), the collectives from the caller (host: a file mailbox per
     collective, uneven q shares at 3 ranks; rccl: the library's RCCL fisdf_comm on a 1-rank
     communicator).  Every rank's W_q equal the 1-GPU build's bit for bit, every rank holds W_0,
     the W_s row blocks are the 1-GPU W_s rows, and the all-reduced J/K of every rank equal the
-    1-GPU get_jk to rounding."""
+    1-GPU get_jk to rounding.  Variants: fit="svd" (the minimum-norm operator on every q) and
+    time reversal off (all nk q fitted and shared)."""
     with tempfile.TemporaryDirectory() as tmp:
         procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "capi_shard_worker.py"), name,
-                                   str(r), str(size), tmp, mode]) for r in range(size)]
+                                   str(r), str(size), tmp, mode, variant]) for r in range(size)]
         rcs = []
         for p in procs:
             try:
@@ -100,7 +102,8 @@ def test_capi_build_sharded(mode, size, name):
         dws = abs(o["ws_rows"] - ref["ref_ws"][:, i0:i1]).max()
         assert dws < 1e-12 * max(1.0, abs(ref["ref_ws"]).max()), dws
         dj, dk = abs(o["vj"] - ref["ref_vj"]).max(), abs(o["vk"] - ref["ref_vk"]).max()
-        print(f"\n{name} {mode} rank {r}/{size}: q {o['fit_qs'].tolist()} rows [{i0}, {i1}) "
+        print(f"\n{name} {mode}{' ' + variant if variant else ''} rank {r}/{size}: "
+              f"q {o['fit_qs'].tolist()} rows [{i0}, {i1}) "
               f"|dWs| {dws:.1e} |dJ| {dj:.1e} |dK| {dk:.1e} vs the 1-GPU build")
         assert dj < 1e-11 and dk < 1e-11
         assert np.array_equal(o["vj"], outs[0]["vj"]) and np.array_equal(o["vk"], outs[0]["vk"])
