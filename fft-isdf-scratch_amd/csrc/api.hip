@@ -2059,6 +2059,16 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       rfmax = nip;
       ++ncod;
     }
+  // every q full rank (the production regime): each q's W_PP = L^-H G L^-1 and its scatter run
+  // in its lane right after its HERK, overlapped with the other q's fit, instead of as a batched
+  // tail after the lanes join (the same kernels with batch 1: W_q unchanged bit for bit);
+  // FISDF_LANE_WPP=0 keeps the batched tail
+  static const bool lane_wpp_env = [] {
+    const char* e = getenv("FISDF_LANE_WPP");
+    return !(e && e[0] == '0');
+  }();
+  bool lane_wpp = lane_wpp_env && rmax == nip && ncod == 0;
+  for (int lq = 0; lq < nq && lane_wpp; ++lq) lane_wpp = c->f_rank[s0 + lq] == nip;
   // split-K of each q's HERK from its own rank (not the call's largest), so a q's arithmetic
   // does not depend on which other q share the call (1-GPU vs sharded builds agree bitwise)
   const int ncu = num_cus(c->device);
@@ -2287,6 +2297,16 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       FISDF_HIP(hipEventRecord(c->ev_free[lq % D], st));
       FISDF_TRY(enqueue_fft(lq + D));
     }
+    if (lane_wpp) {  // W_PP = L^-H G L^-1 of this q (S = L^-H G, W_PP = L^-H S^H), scattered
+      StageTimer tm(c, FISDF_ST_SMALL, st);
+      const cplx* Lf = c->f_Li + (long)sl * nn;
+      FISDF_TRY(zgemm(st, OP_C, OP_N, nip, nip, nip, ONE, Lf, nip, 0, G + lq * rr, rmax, 0, ZERO,
+                      S + lq * rr, rmax, 0, 1, 1, nullptr, EPI_NONE, nullptr, GEMM_A_UPPER));
+      FISDF_TRY(zgemm(st, OP_C, OP_C, nip, nip, nip, ONE, Lf, nip, 0, S + lq * rr, rmax, 0, ZERO,
+                      T + lq * rr, rmax, 0, 1, 1, nullptr, EPI_NONE, nullptr, GEMM_A_UPPER));
+      FISDF_TRY(scatter_w(st, T + lq * rr, rmax, rr, rmax, c->f_piv + (long)sl * nip,
+                          c->f_rank_dev + sl, Wq + lq * nn, nip, 1));
+    }
   }
   // join the lanes (and the FFT stream: that keeps the arena reuse ordered) before the batched
   // small stage on the main stream
@@ -2295,7 +2315,7 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   for (int i = 0; i < 3; ++i)
     if (aux_used[i]) FISDF_TRY(aux_join(c, i));
   FISDF_TRY(join_factors(c));
-  {
+  if (!lane_wpp) {
     StageTimer tm(c, FISDF_ST_SMALL);
     // W_PP = L^{-H} G L^{-1} for all q of the shard at once (L padded with identity, G with
     // zeros beyond each rank):  T = L^{-H} G ; S = L^{-H} T^H ; W_PP = S^H ; scatter by pivots
