@@ -2059,15 +2059,19 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       rfmax = nip;
       ++ncod;
     }
-  // every q full rank (the production regime): each q's W_PP = L^-H G L^-1 and its scatter run
-  // in its lane right after its HERK, overlapped with the other q's fit, instead of as a batched
-  // tail after the lanes join (the same kernels with batch 1: W_q unchanged bit for bit);
-  // FISDF_LANE_WPP=0 keeps the batched tail
-  static const bool lane_wpp_env = [] {
+  // every q full rank (the production regime) and many q in the call: each q's W_PP =
+  // L^-H G L^-1 and its scatter run in its lane right after its HERK, overlapped with the other
+  // q's fit, instead of as a batched tail after the lanes join (the same kernel per output, batch
+  // 1: W_q unchanged bit for bit).  C3 on one GPU (36 q): 79.89 vs 80.21 ms/step; a k-shard's 4-5
+  // q: +0.6 ms per rank (the last q of each lane then waits for its own small GEMMs), so below
+  // kLaneWppMinQ q the batched tail stays.  FISDF_LANE_WPP: 0 never, 1 always
+  constexpr int kLaneWppMinQ = 12;
+  static const int lane_wpp_env = [] {
     const char* e = getenv("FISDF_LANE_WPP");
-    return !(e && e[0] == '0');
+    return e ? atoi(e) : -1;
   }();
-  bool lane_wpp = lane_wpp_env && rmax == nip && ncod == 0;
+  bool lane_wpp = (lane_wpp_env < 0 ? nq >= kLaneWppMinQ : lane_wpp_env != 0) && rmax == nip &&
+                  ncod == 0;
   for (int lq = 0; lq < nq && lane_wpp; ++lq) lane_wpp = c->f_rank[s0 + lq] == nip;
   // split-K of each q's HERK from its own rank (not the call's largest), so a q's arithmetic
   // does not depend on which other q share the call (1-GPU vs sharded builds agree bitwise)
