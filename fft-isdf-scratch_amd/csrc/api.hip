@@ -588,7 +588,14 @@ int env_fit_pipe() {
   return v;
 }
 
-int default_pipe_depth(int lanes) { return lanes + 2; }
+// the FFT ring's depth when fisdf_set_fit_pipe gave none: FISDF_PIPE_DEPTH, else lanes + 2
+int default_pipe_depth(int lanes) {
+  static const int env = [] {
+    const char* e = getenv("FISDF_PIPE_DEPTH");
+    return e ? std::max(0, std::min(64, atoi(e))) : 0;
+  }();
+  return env > 0 ? env : lanes + 2;
+}
 
 int num_cus(int device) {
   int n = 0;
