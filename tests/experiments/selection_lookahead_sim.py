@@ -2,7 +2,7 @@
 column, if d'_q > T then q is the next greedy pivot without another exchange."""
 import sys, time
 import numpy as np
-sys.path.insert(0, "/root/repo"); sys.path.insert(0, "/root/repo/fft-isdf-scratch_amd")
+import os; _R = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))); sys.path[:0] = [_R, os.path.join(_R, "fft-isdf-scratch_amd")]
 from fisdf import cell as C
 import bench
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"

@@ -2,7 +2,7 @@
 order while the next candidate's updated residual beats the bound (the (k+2)-th current value)."""
 import sys
 import numpy as np
-sys.path.insert(0, "/root/repo"); sys.path.insert(0, "/root/repo/fft-isdf-scratch_amd")
+import os; _R = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))); sys.path[:0] = [_R, os.path.join(_R, "fft-isdf-scratch_amd")]
 from fisdf import cell as C
 import bench
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
