@@ -2773,12 +2773,17 @@ int build_return(fisdf_ctx* c, void* p) {
 
 void build_return_all(fisdf_ctx* c) {
   // an earlier call that failed between a fork and its join may have left an aux stream with
-  // work: drain it before the caller's allocator gets the buffers back
+  // work: drain it before the caller's allocator gets the buffers back (likewise the sharded
+  // build's collective stream, whose exchange reads and writes the build's y buffers)
   for (int i = 0; i < 3; ++i)
     if (c->aux_joined[i] != c->aux_use[i]) {
       if (c->aux[i]) (void)hipStreamSynchronize(c->aux[i]);
       c->aux_joined[i] = c->aux_use[i];
     }
+  if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
+  // y-readiness marks left by a build that failed before its fit consumed them
+  c->ready_marked.assign(c->ready_marked.size(), 0);
+  c->y_piece.clear();
   std::vector<void*> l;
   l.swap(c->lent);
   if (c->free_fn)
