@@ -2178,6 +2178,23 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     for (int i = 0; i < 3; ++i) kd[i] = g.a[i][0] * kq[0] + g.a[i][1] * kq[1] + g.a[i][2] * kq[2];
     const double* wt = nullptr;
     FISDF_TRY(weight_q(st, lq, &wt));
+    // a half-grid q: its transform pairs G with -G - m (m = 2 k_q, the phase exp(-i k_q.r) times
+    // a real input), so the FFT writes the prefix planes only and moves half of its intermediate
+    // (fft3d herm); m from the phase actually applied must match the pairing the weights use
+    int herm_m[3];
+    bool herm = half_of(sl);
+    if (herm) {
+      int m[3];
+      self_conjugate_m(kmesh, h_qs[lq], m);
+      for (int d = 0; d < 3; ++d) {
+        const double t = kd[d] / M_PI;
+        const long tm2 = std::lround(t);
+        herm = herm && std::fabs(t - (double)tm2) < 1e-9 &&
+               ((tm2 % mesh[d]) + mesh[d]) % mesh[d] == m[d] % mesh[d];
+        herm_m[d] = m[d];
+      }
+    }
+    const int* hm = herm ? herm_m : nullptr;
     StageTimer tm(c, FISDF_ST_FFT, st);
     const cplx* pc = piece_of(lq);
     FISDF_CHECK(pc || yT, "fit_coulomb: q without y");
@@ -2197,11 +2214,12 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       }
       pc = nullptr;
       FISDF_TRY(fft3d(st, yb, ngrid, c->f_piv + (long)sl * nip, Yh, ngrid, r, mesh[0], mesh[1],
-                      mesh[2], kd, wt, nullptr, nullptr));
+                      mesh[2], kd, wt, nullptr, nullptr, hm));
       return 0;
     }
     FISDF_TRY(fft3d(st, pc ? pc : yT + (long)lq * nip * ngrid, ngrid, c->f_piv + (long)sl * nip, Yh,
-                    ngrid, r, mesh[0], mesh[1], mesh[2], kd, wt, nullptr, pc ? planes : nullptr));
+                    ngrid, r, mesh[0], mesh[1], mesh[2], kd, wt, nullptr, pc ? planes : nullptr,
+                    hm));
     return 0;
   };
   // FFT of q lq into its ring slot, after the lane that read the slot's previous q is done

@@ -380,7 +380,8 @@ __global__ __launch_bounds__(64) void fft_plane_reg(const cplx* __restrict__ in,
                                                     long out_ld, int rows, int n0,
                                                     const cplx* __restrict__ W, double kd0,
                                                     double kd1, double kd2, int use_phase,
-                                                    const PlaneRef* __restrict__ planes) {
+                                                    const PlaneRef* __restrict__ planes,
+                                                    int nrow_out) {
   constexpr int P = NN * NN, LD = NN + 1;
   __shared__ cplx img[NN * LD];
   __shared__ cplx ph1[NN], ph2[NN];
@@ -435,10 +436,12 @@ __global__ __launch_bounds__(64) void fft_plane_reg(const cplx* __restrict__ in,
     for (int p = 0; p < NN; ++p) img[p * LD + lane] = x[p];
   }
   __syncthreads();
+  // lines j1 < nrow_out only (all of them, or the Hermitian prefix: fft_axis0_herm)
+  const int Pout = nrow_out * NN;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int e = lane + 64 * u;
-    if (e < P) {
+    if (e < Pout) {
       const int i1 = e / NN, i2 = e - i1 * NN;
       dst[e] = img[i1 * LD + i2];
     }
@@ -473,19 +476,95 @@ __global__ __launch_bounds__(256) void fft_axis0_reg(const cplx* in, long in_ld,
     __builtin_nontemporal_store(fft_dv2{x[p].x, x[p].y}, (fft_dv2*)(dst + (long)p * P));
 }
 
+constexpr int herm_prefix(int n, int m) {
+  int nH = 0;
+  for (int i = 0; i < n; ++i)
+    if (i <= ((-i - m) % n + n) % n) nH = i + 1;
+  return nH;
+}
+
+// axis 0 of a Hermitian-paired transform (a self-conjugate q: out(j') = conj(out(j)),
+// j' = -j - m): the plane pass wrote only the lines j1 < n1H.  A column (j1', j2') on a line it
+// skipped is the partner of a stored column (j1, j2) = (-j1' - m1, -j2' - m2), and
+//   T(i0, j1', j2') = e^{-2 pi i m0 i0 / n0} conj(T(i0, j1, j2))
+// (the axis-0 phase squared).  Lanes l and l + 32 of a wave take one stored column and its
+// partner: both read the stored column (the same addresses, one fetch), the partner lane
+// conjugates and twiddles, each transforms its column and stores its prefix planes j0 < NH.
+// The transform is in place: the wave's loads all complete before its first store, and no other
+// wave touches the pair, so reading a column another lane overwrites is race-free.  Columns of
+// the self-paired lines (both members stored) take one lane each (blocks past npb).  Per lane
+// the same registers as fft_axis0_reg; moves n1H / n1 of its intermediate and NH / n0 of its
+// output.
+template <int N0, int M0>
+__global__ __launch_bounds__(256) void fft_axis0_herm(const cplx* in, long in_ld, cplx* out,
+                                                      long out_ld, int rows, int n1, int n2,
+                                                      int m1, int m2, int lo, int hi, int sl0,
+                                                      int sl1, int npb,
+                                                      const cplx* __restrict__ W,
+                                                      const double* __restrict__ weight) {
+  constexpr int NH = herm_prefix(N0, M0);
+  const int P = n1 * n2;
+  const int lane = threadIdx.x & 63;
+  int row, c, d;
+  bool flip = false;
+  if ((int)blockIdx.x < npb) {  // pair region: 32 stored columns and their partners per wave
+    const long npr = (long)(hi - lo) * n2;
+    const long k = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + (lane & 31);
+    if (k >= (long)rows * npr) return;
+    row = (int)(k / npr);
+    const int kk = (int)(k - (long)row * npr);
+    const int j1 = lo + kk / n2, j2 = kk - (kk / n2) * n2;
+    c = j1 * n2 + j2;
+    flip = lane >= 32;
+    d = flip ? (((-j1 - m1) % n1 + n1) % n1) * n2 + ((-j2 - m2) % n2 + n2) % n2 : c;
+  } else {  // self-paired lines sl0, sl1 (-1: none)
+    const int nsl = (sl0 >= 0) + (sl1 >= 0);
+    const long nsr = (long)nsl * n2;
+    const long s = (long)(blockIdx.x - npb) * 256 + threadIdx.x;
+    if (s >= (long)rows * nsr) return;
+    row = (int)(s / nsr);
+    const int ss = (int)(s - (long)row * nsr);
+    const int li = ss / n2;
+    const int j1 = (li == 0 && sl0 >= 0) ? sl0 : sl1;
+    c = d = j1 * n2 + (ss - li * n2);
+  }
+  const cplx* src = in + (long)row * in_ld + c;
+  cplx* dst = out + (long)row * out_ld + d;
+  cplx x[N0];
+#pragma unroll
+  for (int p = 0; p < N0; ++p) x[p] = src[(long)p * P];
+  if (flip) {
+#pragma unroll
+    for (int p = 0; p < N0; ++p) {
+      x[p].y = -x[p].y;
+      if constexpr (M0 != 0) x[p] = cmul(x[p], W[(p * M0) % N0]);
+    }
+  }
+  fft_rec<N0, N0>(x, W);
+  if (weight) {
+#pragma unroll
+    for (int p = 0; p < NH; ++p) x[p] = cscale(x[p], weight[(long)p * P + d]);
+  }
+  // same non-temporal stores as fft_axis0_reg
+#pragma unroll
+  for (int p = 0; p < NH; ++p)
+    __builtin_nontemporal_store(fft_dv2{x[p].x, x[p].y}, (fft_dv2*)(dst + (long)p * P));
+}
+
 // meshes with register kernels (cubic n^3 for the plane kernel; any n0 for axis 0)
 #define FISDF_REG_SIZES(X) X(8) X(12) X(13) X(15) X(16) X(18) X(20) X(24) X(25) X(27) X(30) X(32) X(36) X(40) X(45) X(48)
 
 int fft_plane_reg_launch(hipStream_t s, int n, const cplx* in, long in_ld, const int* rowidx,
                          cplx* out, long out_ld, int rows, int n0, const cplx* W, const double* kd,
-                         const PlaneRef* planes, bool* done) {
+                         const PlaneRef* planes, int nrow_out, bool* done) {
   *done = false;
   const double k0 = kd ? kd[0] : 0, k1 = kd ? kd[1] : 0, k2 = kd ? kd[2] : 0;
   const long nplanes = (long)rows * n0;
 #define FISDF_PL(N)                                                                            \
   if (n == N) {                                                                                \
     hipLaunchKernelGGL(fft_plane_reg<N>, dim3((unsigned)nplanes), dim3(64), 0, s, in, in_ld,    \
-                       rowidx, out, out_ld, rows, n0, W, k0, k1, k2, kd ? 1 : 0, planes);       \
+                       rowidx, out, out_ld, rows, n0, W, k0, k1, k2, kd ? 1 : 0, planes,        \
+                       nrow_out);                                                             \
     *done = true;                                                                              \
   }
   FISDF_REG_SIZES(FISDF_PL)
@@ -507,6 +586,40 @@ int fft_axis0_reg_launch(hipStream_t s, int n0, const cplx* in, long in_ld, cplx
   }
   FISDF_REG_SIZES(FISDF_AX)
 #undef FISDF_AX
+  if (*done) FISDF_HIP(hipGetLastError());
+  return 0;
+}
+
+int fft_axis0_herm_launch(hipStream_t s, int n0, const cplx* in, long in_ld, cplx* out,
+                          long out_ld, int rows, int n1, int n2, int n1H, const int m[3],
+                          const cplx* W, const double* weight, bool* done) {
+  *done = false;
+  auto partner1 = [&](int j) { return ((-j - m[1]) % n1 + n1) % n1; };
+  // stored lines: [lo, hi) pair with skipped lines; sl0 / sl1 are self-paired (or -1)
+  const int sl0 = partner1(0) == 0 ? 0 : -1;
+  const int sl1 = (n1H - 1 > 0 && partner1(n1H - 1) == n1H - 1) ? n1H - 1 : -1;
+  const int lo = sl0 >= 0 ? 1 : 0, hi = sl1 >= 0 ? n1H - 1 : n1H;
+  for (int j = lo; j < hi; ++j)
+    FISDF_CHECK(partner1(j) >= n1H, "fft: Hermitian line pairing");
+  const long pairs = (long)rows * (hi - lo) * n2;
+  const long npb = (pairs + 127) / 128;  // 4 waves x 32 pairs per block
+  const long nself = (long)rows * ((sl0 >= 0) + (sl1 >= 0)) * n2;
+  const long blocks = npb + (nself + 255) / 256;
+  FISDF_CHECK(blocks < (1L << 31), "fft: too many blocks");
+#define FISDF_AXH(N)                                                                           \
+  if (n0 == N) {                                                                               \
+    if (m[0] == 0)                                                                             \
+      hipLaunchKernelGGL((fft_axis0_herm<N, 0>), dim3((unsigned)blocks), dim3(256), 0, s, in,    \
+                         in_ld, out, out_ld, rows, n1, n2, m[1], m[2], lo, hi, sl0, sl1,       \
+                         (int)npb, W, weight);                                                 \
+    else                                                                                       \
+      hipLaunchKernelGGL((fft_axis0_herm<N, 1>), dim3((unsigned)blocks), dim3(256), 0, s, in,    \
+                         in_ld, out, out_ld, rows, n1, n2, m[1], m[2], lo, hi, sl0, sl1,       \
+                         (int)npb, W, weight);                                                 \
+    *done = true;                                                                              \
+  }
+  FISDF_REG_SIZES(FISDF_AXH)
+#undef FISDF_AXH
   if (*done) FISDF_HIP(hipGetLastError());
   return 0;
 }
@@ -628,9 +741,18 @@ bool fft3d_reads_slices(int n0, int n1, int n2) {
   return reg_mesh(n0, n1, n2) || plane_kernel_lds(n1, n2) <= 96 * 1024;
 }
 
+// FISDF_FFT_HERM=0: the self-conjugate q's transform runs the full two passes (A/B)
+bool fft_herm_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FISDF_FFT_HERM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* out, long out_ld,
           int rows, int n0, int n1, int n2, const double* kd, const double* weight, cplx* /*work*/,
-          const PlaneRef* planes) {
+          const PlaneRef* planes, const int* herm) {
   if (rows == 0) return 0;
   FISDF_CHECK(in != out || rowidx == nullptr, "fft: in-place pass cannot gather rows");
   FISDF_CHECK(!planes || fft3d_reads_slices(n0, n1, n2), "fft: sliced input needs a plane kernel");
@@ -640,9 +762,21 @@ int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* ou
     FISDF_TRY(get_twiddles(n0, &W0));
     bool ok1 = false, ok0 = false;
     FISDF_CHECK((long)rows * n0 < (1L << 31) && (long)rows * n1 * n2 < (1L << 38), "fft: too large");
+    if (herm && (herm[0] == 0 || herm[0] == 1) && fft_herm_enabled()) {
+      // Hermitian-paired input: the plane pass stores the lines j1 < n1H, the axis-0 pass
+      // completes their partners and writes the prefix planes only
+      const int m[3] = {herm[0], ((herm[1] % n1) + n1) % n1, ((herm[2] % n2) + n2) % n2};
+      const int n1H = herm_prefix(n1, m[1]);
+      FISDF_TRY(fft_plane_reg_launch(s, n1, in, in_ld, rowidx, out, out_ld, rows, n0, W12, kd,
+                                     planes, n1H, &ok1));
+      FISDF_TRY(fft_axis0_herm_launch(s, n0, out, out_ld, out, out_ld, rows, n1, n2, n1H, m, W0,
+                                      weight, &ok0));
+      FISDF_CHECK(ok1 && ok0, "fft: register kernel dispatch failed");
+      return 0;
+    }
     {
       FISDF_TRY(fft_plane_reg_launch(s, n1, in, in_ld, rowidx, out, out_ld, rows, n0, W12, kd,
-                                     planes, &ok1));
+                                     planes, n1, &ok1));
       FISDF_TRY(fft_axis0_reg_launch(s, n0, out, out_ld, out, out_ld, rows, n1 * n2, W0, weight, &ok0));
       FISDF_CHECK(ok1 && ok0, "fft: register kernel dispatch failed");
       return 0;
