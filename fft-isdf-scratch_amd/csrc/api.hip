@@ -128,6 +128,10 @@ struct fisdf_ctx {
   std::vector<char> ready_marked;
   // fisdf_set_y_slices: y of local q j read in place from its all-to-all piece (grid slices)
   std::vector<const cplx*> y_piece;
+  // the composite 1-GPU build stores the self-conjugate q's y real (y_real_store, set around
+  // its y build and fit); y_real_slot[i]: slot i of the last fisdf_build_y_qs holds doubles
+  bool y_real_store = false;
+  std::vector<char> y_real_slot;
   std::vector<long> y_slices;  // (g0, ng) pairs of the pieces' layout, shared by every piece
   std::map<std::vector<long>, PlaneRef*> plane_cache;  // device plane tables per (slices, mesh, rows)
   int* f_piv = nullptr;     // (nk, nip)
@@ -1368,6 +1372,7 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
   // time reversal (fisdf_set_time_reversal): fx_k only for the representatives k <= -k, the
   // others are conj(fx_{-k}) inside kmesh_y — 36 of 64 k at 4x4x4
   const bool half = c->time_reversal;
+  c->y_real_slot.assign(nq, 0);
 #ifdef FISDF_EXP_NOY  // timing experiment only (wrong results)
   return 0;
 #endif
@@ -1375,13 +1380,26 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
     // fused fx + k-mesh DFT where the k-mesh allows it: no fx round trip through HBM
     bool done = false;
     const size_t yw = y_fused_workspace(kmesh, nip, nao, nblk);
+    // self-conjugate q stored real (half their bytes) when the caller's fit reads them so:
+    // the composite build on the whole grid (c->y_real_store)
+    unsigned long long rmask = 0;
+    if (c->y_real_store && g0 == 0 && nblk == ngrid)
+      for (int i = 0; i < nq; ++i) {
+        const int q = h_qs[i];
+        const int i2 = q % kmesh[2], i1 = (q / kmesh[2]) % kmesh[1], i0 = q / (kmesh[1] * kmesh[2]);
+        if ((2 * i0) % kmesh[0] == 0 && (2 * i1) % kmesh[1] == 0 && (2 * i2) % kmesh[2] == 0)
+          rmask |= 1ull << q;
+      }
     if (yw) {
       void* wb = nullptr;
       FISDF_TRY(arena_get(c, yw, &wb));
       FISDF_TRY(y_fused(c->stream, X, nip, nao, f, f_kstride, nblk, kmesh, h_qs, nq, yT,
-                        (long)nip * ngrid, ngrid, g0, c->maximag + 1, (cplx*)wb, yw, &done));
+                        (long)nip * ngrid, ngrid, g0, c->maximag + 1, (cplx*)wb, yw, rmask, &done));
     }
-    if (done) return 0;
+    if (done) {
+      for (int i = 0; i < nq; ++i) c->y_real_slot[i] = (rmask >> h_qs[i]) & 1ull ? 1 : 0;
+      return 0;
+    }
   }
   const int nks = half ? kmesh_half_count(kmesh) : nk;
   std::vector<int> runs = {0, nk};
@@ -2195,6 +2213,8 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       }
     }
     const int* hm = herm ? herm_m : nullptr;
+    // y of this q stored real by the composite build's y kernel (fisdf_build_y_qs)
+    const bool y_real = yT != nullptr && lq < (int)c->y_real_slot.size() && c->y_real_slot[lq];
     StageTimer tm(c, FISDF_ST_FFT, st);
     const cplx* pc = piece_of(lq);
     FISDF_CHECK(pc || yT, "fit_coulomb: q without y");
@@ -2217,9 +2237,10 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
                       mesh[2], kd, wt, nullptr, nullptr, hm));
       return 0;
     }
+    FISDF_CHECK(!(pc && y_real), "fit_coulomb: a real y slot with a y piece");
     FISDF_TRY(fft3d(st, pc ? pc : yT + (long)lq * nip * ngrid, ngrid, c->f_piv + (long)sl * nip, Yh,
                     ngrid, r, mesh[0], mesh[1], mesh[2], kd, wt, nullptr, pc ? planes : nullptr,
-                    hm));
+                    hm, y_real));
     return 0;
   };
   // FFT of q lq into its ring slot, after the lane that read the slot's previous q is done
@@ -3100,6 +3121,16 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
     FISDF_TRY(fisdf_factor_x4_mark(c));
     void* yT;
     FISDF_TRY(build_alloc(c, BR_Y, sizeof(cplx) * (size_t)nq * nip * ngrid, &yT));
+    // the self-conjugate q's y real (half their y writes and FFT reads); FISDF_Y_REAL=0: off
+    static const bool y_real_env = [] {
+      const char* e = getenv("FISDF_Y_REAL");
+      return !(e && e[0] == '0');
+    }();
+    struct YRealScope {  // the mode is this build's only: reset on every exit
+      fisdf_ctx* c;
+      ~YRealScope() { c->y_real_store = false; c->y_real_slot.clear(); }
+    } y_real_scope{c};
+    c->y_real_store = y_real_env && o.real_self_conjugate && fft3d_reads_real(mesh[0], mesh[1], mesh[2]);
     FISDF_TRY(fisdf_build_y_qs(c, f, ngrid * nao, 0, (int)ngrid, (int)ngrid, X, nip, nao, kmesh,
                                a, qs.data(), nq, yT));                             // :67-87
     FISDF_TRY(fisdf_factor_x4_async(c, x4, qs.data(), nq, nip, o.fit_tol,

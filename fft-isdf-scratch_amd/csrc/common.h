@@ -146,12 +146,15 @@ struct PlaneRef {
 // herm (3 ints or null): the input is real up to the phase, so its transform pairs up as
 // out(j') = conj(out(j)) with j' = -j - herm (mod mesh) (a self-conjugate q, m = 2 k_q); only the
 // prefix planes j0 < half_prefix_planes(n0, herm[0]) of out are written (the half-grid fit reads
-// nothing else) and the register path moves half of the intermediate planes
+// nothing else) and the register path moves half of the intermediate planes.
+// in_real: the input rows are doubles (in cast to double*, same in_ld and plane offsets)
 int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* out, long out_ld,
           int rows, int n0, int n1, int n2, const double* kd /*3 or null*/,
           const double* weight /*ngrid or null*/, cplx* work, const PlaneRef* planes = nullptr,
-          const int* herm = nullptr);
+          const int* herm = nullptr, bool in_real = false);
 // whether fft3d takes sliced input for this mesh (its first pass is a per-plane kernel)
 bool fft3d_reads_slices(int n0, int n1, int n2);
+// whether fft3d takes real input (in_real: rows of doubles at the same strides) for this mesh
+bool fft3d_reads_real(int n0, int n1, int n2);
 
 }  // namespace fisdf

@@ -381,7 +381,7 @@ __global__ __launch_bounds__(64) void fft_plane_reg(const cplx* __restrict__ in,
                                                     const cplx* __restrict__ W, double kd0,
                                                     double kd1, double kd2, int use_phase,
                                                     const PlaneRef* __restrict__ planes,
-                                                    int nrow_out) {
+                                                    int nrow_out, int in_real) {
   constexpr int P = NN * NN, LD = NN + 1;
   __shared__ cplx img[NN * LD];
   __shared__ cplx ph1[NN], ph2[NN];
@@ -393,10 +393,19 @@ __global__ __launch_bounds__(64) void fft_plane_reg(const cplx* __restrict__ in,
   cplx* dst = out + (long)row * out_ld + (long)i0 * P;
   constexpr int U = (P + 63) / 64;
   cplx v[U];
+  if (in_real) {  // real rows (a self-conjugate q's y): doubles at the same offsets
+    const double* srr = (const double*)in + r * in_ld + (long)i0 * P;
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int e = lane + 64 * u;
-    v[u] = src[e < P ? e : 0];
+    for (int u = 0; u < U; ++u) {
+      const int e = lane + 64 * u;
+      v[u] = cmk(srr[e < P ? e : 0], 0.0);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = lane + 64 * u;
+      v[u] = src[e < P ? e : 0];
+    }
   }
   if (use_phase && lane < NN) {
     double s0, c0, s, c;
@@ -556,7 +565,7 @@ __global__ __launch_bounds__(256) void fft_axis0_herm(const cplx* in, long in_ld
 
 int fft_plane_reg_launch(hipStream_t s, int n, const cplx* in, long in_ld, const int* rowidx,
                          cplx* out, long out_ld, int rows, int n0, const cplx* W, const double* kd,
-                         const PlaneRef* planes, int nrow_out, bool* done) {
+                         const PlaneRef* planes, int nrow_out, bool in_real, bool* done) {
   *done = false;
   const double k0 = kd ? kd[0] : 0, k1 = kd ? kd[1] : 0, k2 = kd ? kd[2] : 0;
   const long nplanes = (long)rows * n0;
@@ -564,7 +573,7 @@ int fft_plane_reg_launch(hipStream_t s, int n, const cplx* in, long in_ld, const
   if (n == N) {                                                                                \
     hipLaunchKernelGGL(fft_plane_reg<N>, dim3((unsigned)nplanes), dim3(64), 0, s, in, in_ld,    \
                        rowidx, out, out_ld, rows, n0, W, k0, k1, k2, kd ? 1 : 0, planes,        \
-                       nrow_out);                                                             \
+                       nrow_out, in_real ? 1 : 0);                                            \
     *done = true;                                                                              \
   }
   FISDF_REG_SIZES(FISDF_PL)
@@ -737,6 +746,8 @@ bool reg_mesh(int n0, int n1, int n2) {
 
 size_t plane_kernel_lds(int n1, int n2) { return sizeof(cplx) * (4 * MAXN + 2 * (size_t)n1 * n2); }
 
+bool fft3d_reads_real(int n0, int n1, int n2) { return reg_mesh(n0, n1, n2); }
+
 bool fft3d_reads_slices(int n0, int n1, int n2) {
   return reg_mesh(n0, n1, n2) || plane_kernel_lds(n1, n2) <= 96 * 1024;
 }
@@ -752,8 +763,10 @@ bool fft_herm_enabled() {
 
 int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* out, long out_ld,
           int rows, int n0, int n1, int n2, const double* kd, const double* weight, cplx* /*work*/,
-          const PlaneRef* planes, const int* herm) {
+          const PlaneRef* planes, const int* herm, bool in_real) {
   if (rows == 0) return 0;
+  FISDF_CHECK(!in_real || (reg_mesh(n0, n1, n2) && !planes && in != out),
+              "fft: real input needs the register path and unsliced, out-of-place rows");
   FISDF_CHECK(in != out || rowidx == nullptr, "fft: in-place pass cannot gather rows");
   FISDF_CHECK(!planes || fft3d_reads_slices(n0, n1, n2), "fft: sliced input needs a plane kernel");
   if (reg_mesh(n0, n1, n2)) {  // register kernels: square (i1, i2) planes of a listed size, listed n0
@@ -768,7 +781,7 @@ int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* ou
       const int m[3] = {herm[0], ((herm[1] % n1) + n1) % n1, ((herm[2] % n2) + n2) % n2};
       const int n1H = herm_prefix(n1, m[1]);
       FISDF_TRY(fft_plane_reg_launch(s, n1, in, in_ld, rowidx, out, out_ld, rows, n0, W12, kd,
-                                     planes, n1H, &ok1));
+                                     planes, n1H, in_real, &ok1));
       FISDF_TRY(fft_axis0_herm_launch(s, n0, out, out_ld, out, out_ld, rows, n1, n2, n1H, m, W0,
                                       weight, &ok0));
       FISDF_CHECK(ok1 && ok0, "fft: register kernel dispatch failed");
@@ -776,7 +789,7 @@ int fft3d(hipStream_t s, const cplx* in, long in_ld, const int* rowidx, cplx* ou
     }
     {
       FISDF_TRY(fft_plane_reg_launch(s, n1, in, in_ld, rowidx, out, out_ld, rows, n0, W12, kd,
-                                     planes, n1, &ok1));
+                                     planes, n1, in_real, &ok1));
       FISDF_TRY(fft_axis0_reg_launch(s, n0, out, out_ld, out, out_ld, rows, n1 * n2, W0, weight, &ok0));
       FISDF_CHECK(ok1 && ok0, "fft: register kernel dispatch failed");
       return 0;

@@ -94,9 +94,11 @@ int kmesh_half_count(const int kmesh[3]);
 // or nk > 64 (the two-kernel path then runs).
 // workspace bytes of y_fused for this shape (0: the fused kernel does not apply)
 size_t y_fused_workspace(const int kmesh[3], int nip, int nao, int m);
+// rmask: q (bits) stored real, as doubles in the first half of their slot (self-conjugate q)
 int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long fks, int m,
             const int kmesh[3], const int* h_qs, int nq, cplx* yT, long qs, long Is, long goff,
-            unsigned long long* mon, cplx* work, size_t work_bytes, bool* handled);
+            unsigned long long* mon, cplx* work, size_t work_bytes, unsigned long long rmask,
+            bool* handled);
 int kmesh_rep_runs(const int kmesh[3], std::vector<int>* runs);
 // Bloch AO values (ao.hip): F (nimg, ng, nao) f64 workspace, scratch for the small tables;
 // nkb > 0: at the nkb band k-points h_kband (any k) instead of the k-mesh, F (nT, ng, nao)

@@ -648,8 +648,8 @@ __global__ __launch_bounds__(256) void yf_transpose_kernel(const cplx* __restric
 template <int N0, int N1, int N2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void y_fused_kernel(
     const cplx* __restrict__ XT, int nip, int nao, const cplx* __restrict__ FT, int m,
-    int nIt, int nGt, YfPlan plan, unsigned long long qmask, cplx* __restrict__ yT, long qs,
-    long Is, long goff, int mode, int gpair) {
+    int nIt, int nGt, YfPlan plan, unsigned long long qmask, unsigned long long rmask,
+    cplx* __restrict__ yT, long qs, long Is, long goff, int mode, int gpair) {
   constexpr int P = N1 * N2, NK = N0 * P;
   constexpr int R = yf_inplane_rank<N1, N2>(P);         // in-plane representatives
   constexpr int NC = (N0 - 1) / 2;                        // complex planes 1..NC (N0 <= 4: 0 or 1)
@@ -747,9 +747,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       // non-temporal: y (GBs, read back by the fit's FFTs much later) streams past L2, so the
       // X / f operand lines of the MFMA phase stay cached (y -0.22 ms, the factor beside it
       // -0.4 ms at C3, profiles/r03_ab/gemm_pipe.log)
-      typedef double dv2 __attribute__((ext_vector_type(2)));
-      __builtin_nontemporal_store(dv2{v.x * sc, v.y * sc},
-                                  (dv2*)(out + (long)__popcll(qmask & ((1ull << q) - 1ull)) * qs));
+      const long so = (long)__popcll(qmask & ((1ull << q) - 1ull)) * qs;
+      if ((rmask >> q) & 1ull) {
+        // a self-conjugate q (rmask): y_q is real (its DFT twiddles at these frequencies are
+        // +-1, so the imaginary part is exactly zero) and is stored as doubles in the first
+        // half of its slot, [I][g] with the same strides: half the bytes (fft3d in_real)
+        __builtin_nontemporal_store(v.x * sc, (double*)(yT + so) + ((long)I * Is + goff + g));
+      } else {
+        typedef double dv2 __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store(dv2{v.x * sc, v.y * sc}, (dv2*)(out + so));
+      }
     }
   };
 #pragma unroll
@@ -1491,7 +1498,8 @@ size_t y_fused_workspace(const int kmesh[3], int nip, int nao, int m) {
 
 int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long fks, int m,
             const int kmesh[3], const int* h_qs, int nq, cplx* yT, long qs, long Is, long goff,
-            unsigned long long* mon, cplx* work, size_t work_bytes, bool* handled) {
+            unsigned long long* mon, cplx* work, size_t work_bytes, unsigned long long rmask,
+            bool* handled) {
   (void)mon;  // fx_s is real by construction here (t_{-a} = conj(t_a)); nothing to monitor
   *handled = false;
   const int n0 = kmesh[0], n1 = kmesh[1], n2 = kmesh[2];
@@ -1550,7 +1558,8 @@ int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long 
       attr = true;                                                                             \
     }                                                                                          \
     hipLaunchKernelGGL((y_fused_kernel<a, b, c>), dim3((unsigned)grid), dim3(256), lds, s, XT,  \
-                       nip, nao, FT, m, nIt, nGt, plan, qmask, yT, qs, Is, goff, mode, gpair);   \
+                       nip, nao, FT, m, nIt, nGt, plan, qmask, rmask & qmask, yT, qs, Is, goff, \
+                       mode, gpair);                                                          \
     FISDF_HIP(hipGetLastError());                                                              \
     *handled = true;                                                                           \
     return 0;                                                                                  \
