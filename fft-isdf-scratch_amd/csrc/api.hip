@@ -947,6 +947,16 @@ int fisdf_fft3d(fisdf_ctx* c, const void* in, void* out, int rows, const int mes
                mesh[2], nullptr, nullptr, nullptr);
 }
 
+int fisdf_fft3d_paired(fisdf_ctx* c, const void* in, void* out, int rows, const int mesh[3],
+                       const double kd[3], const int m[3], int in_real) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(in && out && mesh && rows >= 0, "fft3d_paired: bad arguments");
+  FISDF_CHECK(!in_real || in != out, "fft3d_paired: real input needs an output buffer of its own");
+  long ng = (long)mesh[0] * mesh[1] * mesh[2];
+  return fft3d(c->stream, (const cplx*)in, ng, nullptr, (cplx*)out, ng, rows, mesh[0], mesh[1],
+               mesh[2], kd, nullptr, nullptr, nullptr, m, in_real != 0);
+}
+
 int fisdf_coulg(fisdf_ctx* c, const int mesh[3], const double a[9], const double k[3],
                 double scale, int take_sqrt, double* w) {
   FISDF_TRY(device_guard(c));

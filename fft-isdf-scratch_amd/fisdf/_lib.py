@@ -93,6 +93,7 @@ _SIGS = {
                           _l, _i, _i], _i),
     "fisdf_herk": ([_vp, _i, _i, _d, _vp, _l, _vp, _l, _i], _i),
     "fisdf_fft3d": ([_vp, _vp, _vp, _i, _ip], _i),
+    "fisdf_fft3d_paired": ([_vp, _vp, _vp, _i, _ip, _dp, _ip, _i], _i),
     "fisdf_coulg": ([_vp, _ip, _dp, _dp, _d, _i, _vp], _i),
     "fisdf_pivoted_cholesky": ([_vp, _vp, _i, _i, _i, _d, _ip, _ip], _i),
     "fisdf_cholesky": ([_vp, _vp, _i, _i, _d, _ip], _i),

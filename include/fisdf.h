@@ -468,6 +468,14 @@ int fisdf_herk(fisdf_ctx* ctx, int n, int K, double alpha, const void* d_A, long
                long ldc, int ksplit);
 /* forward 3-D FFT (numpy fftn sign, unnormalised) of `rows` rows of n0*n1*n2 points */
 int fisdf_fft3d(fisdf_ctx* ctx, const void* d_in, void* d_out, int rows, const int mesh[3]);
+/* the fit's transform of a self-conjugate q: rows pre-multiplied by exp(-i f.kd) (f: fftfreq
+ * fractions; kd may be NULL), m (or NULL) = 2 k_q in mesh units: the input is real up to that
+ * phase, out(j') = conj(out(j)) for j' = -j - m, and only the prefix planes
+ * j0 < #{i0 : i0 <= (-i0 - m0) mod n0} of d_out are written (register meshes; other meshes
+ * write every plane).  in_real: d_in holds rows of doubles (same strides), d_in != d_out,
+ * register meshes only (an error otherwise) */
+int fisdf_fft3d_paired(fisdf_ctx* ctx, const void* d_in, void* d_out, int rows, const int mesh[3],
+                       const double kd[3], const int m[3], int in_real);
 /* sqrt(coulG(k+G) * scale) (or without sqrt), PySCF get_coulG(exxdiv=None) restated */
 int fisdf_coulg(fisdf_ctx* ctx, const int mesh[3], const double a[9], const double k[3],
                 double scale, int take_sqrt, double* d_w);

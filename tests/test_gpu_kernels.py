@@ -113,6 +113,42 @@ def test_fft3d(env, mesh):
     assert err < 1e-14
 
 
+def _prefix_planes(n0, m0):
+    """Restates half_prefix_planes (linalg.hip): planes i0 with i0 <= their partner -i0 - m0."""
+    return max(i0 for i0 in range(n0) if i0 <= (-i0 - m0) % n0) + 1
+
+
+@pytest.mark.parametrize("mesh", [(8, 8, 8), (12, 12, 12), (15, 15, 15), (36, 36, 36)])
+@pytest.mark.parametrize("m", [(0, 0, 0), (1, 1, 1), (1, 0, 1), (0, 1, 0)])
+def test_fft3d_paired(env, mesh, m):
+    """The self-conjugate q's transform (fisdf_fft3d_paired: Hermitian half of the plane pass,
+    the partner lines rebuilt in the axis-0 pass, real input rows) equals numpy's fftn of the
+    phased real input on the prefix planes the half-grid fit reads, for both parities of m and an
+    odd mesh."""
+    torch, L, ctx = env
+    rng = np.random.default_rng(sum(mesh) + 7 * sum(m))
+    rows = 3
+    y = rng.standard_normal((rows, int(np.prod(mesh))))
+    kd = np.pi * np.array(m, dtype=float)
+    f = [np.fft.fftfreq(n) for n in mesh]
+    ph = np.exp(-1j * (f[0][:, None, None] * kd[0] + f[1][None, :, None] * kd[1]
+                       + f[2][None, None, :] * kd[2]))
+    ref = np.fft.fftn(y.reshape(rows, *mesh) * ph, axes=(1, 2, 3)).reshape(rows, -1)
+    ncol = _prefix_planes(mesh[0], m[0]) * mesh[1] * mesh[2]
+    ma, mp = L.iarr(mesh)  # the arrays stay alive as long as their pointers
+    ka, kp = L.darr(kd)
+    ha, hp = L.iarr(m)
+    for in_real in (0, 1):
+        dx = (torch.from_numpy(y).to("cuda") if in_real
+              else dev(torch, y.astype(np.complex128)))
+        dy = torch.full((rows, int(np.prod(mesh))), complex(7.0, 7.0), dtype=torch.complex128,
+                        device="cuda")
+        ctx.call("fisdf_fft3d_paired", L.ptr(dx), L.ptr(dy), rows, mp, kp, hp, in_real)
+        out = dy.cpu().numpy()
+        err = abs(out[:, :ncol] - ref[:, :ncol]).max() / abs(ref).max()
+        assert err < 1e-14, (in_real, err)
+
+
 def test_coulg(env):
     torch, L, ctx = env
     from fisdf.cell import diamond_cell, make_kpts
