@@ -18,6 +18,7 @@ Differences from the reference, all deliberate:
 from __future__ import annotations
 
 import logging
+import os
 import time
 
 import numpy as np
@@ -99,6 +100,18 @@ class _Device:
         t = self.torch
         a = np.ascontiguousarray(arr)
         return t.from_numpy(a).to(self.dev, non_blocking=False)
+
+    def to_host(self, x):
+        """Read back through pinned memory: the copy is enqueued right behind the kernels that
+        produce x and the host then waits for the stream.  A pageable ``.cpu()`` first drains the
+        stream and only then stages its copy — about 0.2 ms of idle GPU at the end of every
+        get_jk (kernel trace, profiles/r05/prof_v2).  FISDF_PINNED_D2H=0: ``.cpu()``."""
+        if os.environ.get("FISDF_PINNED_D2H", "1") == "0":
+            return x.cpu().numpy()
+        h = self.torch.empty(tuple(x.shape), dtype=x.dtype, pin_memory=True)
+        h.copy_(x, non_blocking=True)
+        self.stream.synchronize()
+        return h.numpy()
 
     def to_dev_async(self, arr):
         """Upload through pinned memory without a host wait on the stream (small per-call inputs
@@ -316,9 +329,9 @@ class InterpolativeSeparableDensityFitting:
             vj = _get_j_dev(self, ddms, band)
         if vk is not None and vj is not None and vk.shape == vj.shape:
             # one device-to-host copy (and one synchronisation) for both
-            vk, vj = self.device.torch.stack((vk, vj)).cpu().numpy()
+            vk, vj = self.device.to_host(self.device.torch.stack((vk, vj)))
         if vk is not None:
-            vk = _format_band(vk if isinstance(vk, np.ndarray) else vk.cpu().numpy(), dm,
+            vk = _format_band(vk if isinstance(vk, np.ndarray) else self.device.to_host(vk), dm,
                               kpts_band, kpts)
         if vj is not None:
             vj = _finish_j(vj, dm, kpts, kpts_band)
