@@ -3075,6 +3075,15 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
     FISDF_TRY(tr_check_enqueue(c, c->stream, (const cplx*)x0, ng0, (const cplx*)f, ngrid, nao,
                                kmesh));
   }
+  // X and x4 at their upper bound (the point cap) taken now, while the check runs: the caller's
+  // allocator (a Python callback in the mirror, ~40 us each) then no longer sits in the idle gap
+  // between the selection's read-back and the gather
+  const int nip_ub = o.perm ? o.n_perm : (o.nip_max > 0 ? std::min(o.nip_max, ng0) : 0);
+  void *X = nullptr, *x4 = nullptr;
+  if (nip_ub > 0) {
+    FISDF_TRY(build_alloc(c, BR_X, sizeof(cplx) * (size_t)nk * nip_ub * nao, &X));
+    FISDF_TRY(build_alloc(c, BR_X4, sizeof(cplx) * (size_t)nk * nip_ub * nip_ub, &x4));
+  }
   // interpolation points (:33 -> :357-388), or the caller's
   std::vector<int> perm;
   for (int attempt = 0;; ++attempt) {
@@ -3100,10 +3109,10 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
   const int nip = (int)perm.size();
   FISDF_CHECK(nip > 0, "build: no interpolation points");
   const long nn = (long)nip * nip;
-  void *X, *x4;
-  FISDF_TRY(build_alloc(c, BR_X, sizeof(cplx) * (size_t)nk * nip * nao, &X));
+  FISDF_CHECK(nip_ub == 0 || nip <= nip_ub, "build: more points than the cap");
+  if (!X) FISDF_TRY(build_alloc(c, BR_X, sizeof(cplx) * (size_t)nk * nip * nao, &X));
   FISDF_TRY(fisdf_gather_points(c, x0, nk, ng0, nao, perm.data(), nip, X));        // :388
-  FISDF_TRY(build_alloc(c, BR_X4, sizeof(cplx) * (size_t)nk * nn, &x4));
+  if (!x4) FISDF_TRY(build_alloc(c, BR_X4, sizeof(cplx) * (size_t)nk * nn, &x4));
   FISDF_TRY(fisdf_build_x4(c, X, nip, nao, kmesh, a, x4));                         // :38-48
   std::vector<int> qs, partner;
   std::vector<double> wt;
