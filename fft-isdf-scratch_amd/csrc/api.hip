@@ -3041,9 +3041,8 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
               "build: bad k-mesh or mesh");
   FISDF_CHECK(o.fit_mode >= FISDF_FIT_LSTSQ && o.fit_mode <= FISDF_FIT_BASIC, "build: bad fit_mode");
   FISDF_CHECK(o.perm == nullptr || o.n_perm > 0, "build: perm given without n_perm");
-  // the previous build's buffers go back first (its factor chain may still read x4)
+  // the previous build's factor chain may still read x4: wait for it before anything else
   if (c->f_pending) FISDF_TRY(fisdf_factor_x4_wait(c, nullptr));
-  build_return_all(c);
   StageSettings keep(c);
   fisdf_ctx::Build& B = c->bld;
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
@@ -3075,6 +3074,9 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
     FISDF_TRY(tr_check_enqueue(c, c->stream, (const cplx*)x0, ng0, (const cplx*)f, ngrid, nao,
                                kmesh));
   }
+  // the previous build's buffers go back to the caller's allocator now, while the check runs
+  // (in the mirror each is a Python callback: done first, they left the GPU idle between steps)
+  build_return_all(c);
   // X and x4 at their upper bound (the point cap) taken now, while the check runs: the caller's
   // allocator (a Python callback in the mirror, ~40 us each) then no longer sits in the idle gap
   // between the selection's read-back and the gather
