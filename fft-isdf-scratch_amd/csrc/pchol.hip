@@ -17,6 +17,8 @@
 #include <cstring>
 #include <vector>
 
+#include <mutex>
+
 #include "common.h"
 
 namespace fisdf {
@@ -1452,8 +1454,13 @@ hipError_t launch_coresident(const void* fn, int grid, int threads, void** args,
     const char* e = getenv("FISDF_COOP_LAUNCH");
     return !(e && e[0] == '0');
   }();
-  if (coop)
+  if (coop) {
+    // one cooperative launch at a time in the process: concurrent ones from several host threads
+    // (fisdf_group's ranks) left the runtime crashing in its exit handlers
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
     return hipLaunchCooperativeKernel(fn, dim3(grid), dim3(threads), args, (unsigned)lds, s);
+  }
   int per_cu = 0;
   const hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds);
   if (oe != hipSuccess) return oe;

@@ -114,6 +114,12 @@ _SIGS = {
     "fisdf_comm_rccl_unique_id": ([_vp], _i),
     "fisdf_comm_rccl_init": ([_vp, _i, _i, _i, _vp], _i),
     "fisdf_comm_rccl_destroy": ([_vp], _i),
+    "fisdf_group_create": ([_i, _ip, _i, _vp], _i),
+    "fisdf_group_destroy": ([_vp], _i),
+    "fisdf_group_ctx": ([_vp, _i], _vp),
+    "fisdf_group_last_error": ([_vp], C.c_char_p),
+    "fisdf_group_build": ([_vp, _vp, _i, _vp, _i, _ip, _ip, _dp, _vp, _vp], _i),
+    "fisdf_group_get_jk": ([_vp, _vp, _i, _i, _i, _vp, _vp], _i),
 }
 
 # FISDF_ABI_VERSION of include/fisdf.h this binding's structs follow
@@ -144,6 +150,7 @@ REDUCE_SCATTER_FN = C.CFUNCTYPE(_i, _vp, _vp, _vp, C.c_size_t, _vp)
 ALLREDUCE_FN = C.CFUNCTYPE(_i, _vp, _vp, C.c_size_t, _vp)
 BROADCAST_FN = C.CFUNCTYPE(_i, _vp, _vp, C.c_size_t, _i, _vp)
 COMM_ID_BYTES = 128
+GROUP_COPY, GROUP_RCCL = 0, 1
 
 
 class Comm(C.Structure):

@@ -177,6 +177,27 @@ int fisdf_comm_rccl_init(const unsigned char h_id[FISDF_COMM_ID_BYTES], int rank
                          int device, fisdf_comm* out);
 int fisdf_comm_rccl_destroy(fisdf_comm* comm);
 
+/* ---- one process, several GPUs (SURVEY §8(b)'s fisdf_create(ndev, dev_ids)) -----------------
+ * A group of n ranks, rank r on devices[r] with a context and a stream of its own, joined by
+ * RCCL (FISDF_GROUP_RCCL: distinct devices) or by device copies between the ranks' buffers
+ * (FISDF_GROUP_COPY: any devices, a device may repeat).  fisdf_group_build / _get_jk run
+ * fisdf_build_sharded / fisdf_get_jk on every rank at once, one host thread per rank; the per-rank
+ * arrays hold each rank's device pointers (the same AO values on every rank).  Results: through
+ * fisdf_group_ctx(g, r) and the single-rank entries (fisdf_build_get, ...); every rank's J/K are
+ * the full, all-reduced matrices.  On failure the message is fisdf_group_last_error(g). */
+#define FISDF_GROUP_COPY 0
+#define FISDF_GROUP_RCCL 1
+typedef struct fisdf_group fisdf_group;
+int fisdf_group_create(int n, const int* devices, int kind, fisdf_group** out);
+int fisdf_group_destroy(fisdf_group* g);
+fisdf_ctx* fisdf_group_ctx(fisdf_group* g, int rank);
+const char* fisdf_group_last_error(fisdf_group* g);
+int fisdf_group_build(fisdf_group* g, const void* const* d_x0, int ng0, const void* const* d_f,
+                      int nao, const int kmesh[3], const int mesh[3], const double a[9],
+                      const fisdf_build_opts* opts, int* h_nip);
+int fisdf_group_get_jk(fisdf_group* g, const void* const* d_dms, int nset, int with_j,
+                       int with_k, void* const* d_vj, void* const* d_vk);
+
 /* Host copies of the reference's attributes (fftisdf.py:125-128): h_x (nk, nip, nao) = _x,
  * h_w0 (nip, nip) = _w0, h_wq (nk, nip, nip) = _wq (unfitted q filled as conj(W_{-q}); not on a
  * sharded build of several ranks, whose W_q are distributed: fisdf_build_get per rank).

@@ -9,7 +9,9 @@ its stream, moves its pieces through host files and uploads what it receives (ra
 GPU, as a test; RCCL refuses two ranks on one device).  "rccl": the library's own RCCL
 fisdf_comm (fisdf_comm_rccl_*), rank 0 writing the unique id to DIR/id.bin.
 
-usage: python capi_shard_worker.py CASE RANK SIZE DIR host|rccl [VARIANT]
+"group": every rank in one process through fisdf_group (FISDF_GROUP_COPY; RANK ignored).
+
+usage: python capi_shard_worker.py CASE RANK SIZE DIR host|rccl|group [VARIANT]
   VARIANT: "" (defaults), "svd" (fit_mode FISDF_FIT_SVD: the minimum-norm operator on every q),
   "notr" (time_reversal 0: every q fitted, weights 1)
 """
@@ -251,6 +253,123 @@ def main(case, rank, size, d, mode, variant=""):
     np.savez(os.path.join(d, f"rank{rank}.npz"), **out)
 
 
+def main_group(case, size, d, variant=""):
+    """All SIZE ranks in this one process through fisdf_group (FISDF_GROUP_COPY, every rank on
+    GPU 0, one host thread per rank inside the library): writes the same rank{r}.npz files."""
+    from cases import inputs
+    cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(case)
+    nao = cell.nao_nr()
+    dms = np.concatenate([dm, Cl.make_dm(nao, kmesh, cell, seed=99, scale=0.2)[None]])
+    lib = _lib.load()
+
+    def call(ctx, name, *args):
+        rc = getattr(lib, name)(ctx, *args)
+        if rc != 0:
+            raise RuntimeError(f"{name}: {lib.fisdf_last_error(ctx).decode()}")
+
+    ctx = C.c_void_p()
+    assert lib.fisdf_create(0, None, C.byref(ctx)) == 0, lib.fisdf_last_error(None)
+
+    def upload(a):
+        a = np.ascontiguousarray(a)
+        p = C.c_void_p()
+        call(ctx, "fisdf_malloc", C.c_size_t(a.nbytes), C.byref(p))
+        call(ctx, "fisdf_memcpy_htod", p, a.ctypes.data_as(C.c_void_p), C.c_size_t(a.nbytes))
+        return p
+
+    def download(c, ptr, shape, dtype=complex):
+        h = np.empty(shape, dtype)
+        call(c, "fisdf_memcpy_dtoh", h.ctypes.data_as(C.c_void_p), C.c_void_p(ptr),
+             C.c_size_t(h.nbytes))
+        return h
+
+    def alloc(nbytes):
+        p = C.c_void_p()
+        call(ctx, "fisdf_malloc", C.c_size_t(nbytes), C.byref(p))
+        return p
+
+    d_x0, d_f, d_dms = upload(x0), upload(chi), upload(dms.astype(np.complex128))
+    km, kp = _lib.iarr(kmesh)
+    me, mp = _lib.iarr(cell.mesh)
+    aa, ap = _lib.darr(cell.a.ravel())
+    opts = _lib.BuildOpts()
+    lib.fisdf_build_opts_default(C.byref(opts))
+    opts.nip_max = int(nao * c0)                                           # fftisdf.py:383
+    if variant == "notr":
+        opts.time_reversal = 0
+    elif variant:
+        raise ValueError(variant)
+    trace = os.environ.get("FISDF_WORKER_TRACE") is not None
+    say = (lambda m: print(m, file=sys.stderr, flush=True)) if trace else (lambda m: None)  # noqa: E731
+    devs, devp = _lib.iarr([0] * size)
+    g = C.c_void_p()
+    say("group_create")
+    assert lib.fisdf_group_create(size, devp, _lib.GROUP_COPY, C.byref(g)) == 0, \
+        lib.fisdf_last_error(None)
+    ptrs = lambda p: (C.c_void_p * size)(*([p.value] * size))  # noqa: E731
+    nip = C.c_int()
+    say("group_build")
+    rc = lib.fisdf_group_build(g, ptrs(d_x0), x0.shape[1], ptrs(d_f), nao, kp, mp, ap,
+                               C.byref(opts), C.byref(nip))
+    assert rc == 0, lib.fisdf_group_last_error(g)
+    nip = nip.value
+    nbytes = dms.size * 16
+    say("group_get_jk")
+    vjs = [alloc(nbytes) for _ in range(size)]
+    vks = [alloc(nbytes) for _ in range(size)]
+    rc = lib.fisdf_group_get_jk(g, ptrs(d_dms), 2, 1, 1, (C.c_void_p * size)(*[v.value for v in vjs]),
+                                (C.c_void_p * size)(*[v.value for v in vks]))
+    assert rc == 0, lib.fisdf_group_last_error(g)
+    say("results")
+    outs = []
+    for rank in range(size):
+        rc_ = lib.fisdf_group_ctx(g, rank)
+        say(f"rank {rank} ctx {rc_}")
+        rctx = C.c_void_p(rc_)
+        r = _lib.BuildResult()
+        call(rctx, "fisdf_build_get", C.byref(r))
+        assert (r.shard_rank, r.shard_size) == (rank, size)
+        nfit = r.nfit
+        out = dict(fit_qs=np.ctypeslib.as_array(r.fit_qs, (nfit,)).copy() if nfit else
+                   np.zeros(0, np.int32),
+                   perm=np.ctypeslib.as_array(r.perm, (nip,)).copy(),
+                   rows=np.array([r.row0, r.row1]), w0=download(rctx, r.d_W0, (nip, nip)))
+        out["wq"] = (download(rctx, r.d_Wq, (nfit, nip, nip)) if nfit
+                     else np.zeros((0, nip, nip), complex))
+        out["ws_rows"] = download(rctx, r.d_Ws, (r.nk, r.row1 - r.row0, nip), np.float64)
+        out["vj"] = download(ctx, vjs[rank].value, dms.shape)
+        out["vk"] = download(ctx, vks[rank].value, dms.shape)
+        outs.append(out)
+    say("group_destroy")
+    assert lib.fisdf_group_destroy(g) == 0
+    say("reference")
+    # the 1-GPU composite build, same inputs
+    nip1 = C.c_int()
+    call(ctx, "fisdf_build", d_x0, x0.shape[1], d_f, nao, kp, mp, ap, C.byref(opts),
+         C.byref(nip1))
+    say("reference built")
+    r1 = _lib.BuildResult()
+    call(ctx, "fisdf_build_get", C.byref(r1))
+    outs[0]["ref_fit_qs"] = np.ctypeslib.as_array(r1.fit_qs, (r1.nfit,)).copy()
+    outs[0]["ref_wq"] = download(ctx, r1.d_Wq, (r1.nfit, nip, nip))
+    outs[0]["ref_ws"] = download(ctx, r1.d_Ws, (r1.nk, nip, nip), np.float64)
+    call(ctx, "fisdf_get_jk", d_dms, 2, 1, 1, vjs[0], vks[0])
+    outs[0]["ref_vj"] = download(ctx, vjs[0].value, dms.shape)
+    outs[0]["ref_vk"] = download(ctx, vks[0].value, dms.shape)
+    say("reference done")
+    for p in [d_x0, d_f, d_dms] + vjs + vks:
+        call(ctx, "fisdf_free", p)
+    assert lib.fisdf_destroy(ctx) == 0
+    say("freed")
+    assert "torch" not in sys.modules, "the C-ABI path must not need torch"
+    for rank, out in enumerate(outs):
+        np.savez(os.path.join(d, f"rank{rank}.npz"), **out)
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5],
-         sys.argv[6] if len(sys.argv) > 6 else "")
+    if sys.argv[5] == "group":
+        main_group(sys.argv[1], int(sys.argv[3]), sys.argv[4],
+                   sys.argv[6] if len(sys.argv) > 6 else "")
+    else:
+        main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5],
+             sys.argv[6] if len(sys.argv) > 6 else "")

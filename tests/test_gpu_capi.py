@@ -65,7 +65,8 @@ def test_capi_build_get_jk_torch_free(name):
 @pytest.mark.parametrize("mode,size,name,variant", [
     ("host", 2, "toy222", ""), ("host", 3, "toy331_fr", ""), ("rccl", 1, "toy222", ""),
     ("host", 2, "toy331_fr", "svd"), ("host", 3, "toy222", "notr"),
-    ("host", 6, "toy331_fr", "")])   # 5 fitted q on 6 ranks: one rank fits none
+    ("host", 6, "toy331_fr", ""),    # 5 fitted q on 6 ranks: one rank fits none
+    ("group", 3, "toy331_fr", ""), ("group", 2, "toy222", "notr")])
 def test_capi_build_sharded(mode, size, name, variant):
     """fisdf_build_sharded (SURVEY §8(e) through the C-ABI, no torch): SIZE ranks on GPU 0
     (tests/capi_shard_worker.py), the collectives from the caller (host: a file mailbox per
@@ -73,10 +74,13 @@ def test_capi_build_sharded(mode, size, name, variant):
     communicator).  Every rank's W_q equal the 1-GPU build's bit for bit, every rank holds W_0,
     the W_s row blocks are the 1-GPU W_s rows, and the all-reduced J/K of every rank equal the
     1-GPU get_jk to rounding.  Variants: fit="svd" (the minimum-norm operator on every q) and
-    time reversal off (all nk q fitted and shared)."""
+    time reversal off (all nk q fitted and shared).  group: every rank in one process through
+    fisdf_group (SURVEY §8(b)'s multi-device handle: a thread and a stream per rank, the
+    collectives as device copies between the ranks' buffers)."""
     with tempfile.TemporaryDirectory() as tmp:
+        nproc = 1 if mode == "group" else size   # group: all ranks in one process (fisdf_group)
         procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "capi_shard_worker.py"), name,
-                                   str(r), str(size), tmp, mode, variant]) for r in range(size)]
+                                   str(r), str(size), tmp, mode, variant]) for r in range(nproc)]
         rcs = []
         for p in procs:
             try:
@@ -85,7 +89,7 @@ def test_capi_build_sharded(mode, size, name, variant):
                 for q in procs:
                     q.kill()
                 raise
-        assert rcs == [0] * size, rcs
+        assert rcs == [0] * nproc, rcs
         outs = [dict(np.load(os.path.join(tmp, f"rank{r}.npz"))) for r in range(size)]
     ref = outs[0]
     qs = np.concatenate([o["fit_qs"] for o in outs])
