@@ -295,8 +295,11 @@ def main_group(case, size, d, variant=""):
     opts = _lib.BuildOpts()
     lib.fisdf_build_opts_default(C.byref(opts))
     opts.nip_max = int(nao * c0)                                           # fftisdf.py:383
+    kind = _lib.GROUP_COPY
     if variant == "notr":
         opts.time_reversal = 0
+    elif variant == "rccl":      # the group's RCCL collectives (distinct devices: one rank here)
+        kind = _lib.GROUP_RCCL
     elif variant:
         raise ValueError(variant)
     trace = os.environ.get("FISDF_WORKER_TRACE") is not None
@@ -304,7 +307,7 @@ def main_group(case, size, d, variant=""):
     devs, devp = _lib.iarr([0] * size)
     g = C.c_void_p()
     say("group_create")
-    assert lib.fisdf_group_create(size, devp, _lib.GROUP_COPY, C.byref(g)) == 0, \
+    assert lib.fisdf_group_create(size, devp, kind, C.byref(g)) == 0, \
         lib.fisdf_last_error(None)
     ptrs = lambda p: (C.c_void_p * size)(*([p.value] * size))  # noqa: E731
     nip = C.c_int()

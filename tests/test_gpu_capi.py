@@ -66,7 +66,7 @@ def test_capi_build_get_jk_torch_free(name):
     ("host", 2, "toy222", ""), ("host", 3, "toy331_fr", ""), ("rccl", 1, "toy222", ""),
     ("host", 2, "toy331_fr", "svd"), ("host", 3, "toy222", "notr"),
     ("host", 6, "toy331_fr", ""),    # 5 fitted q on 6 ranks: one rank fits none
-    ("group", 3, "toy331_fr", ""), ("group", 2, "toy222", "notr")])
+    ("group", 3, "toy331_fr", ""), ("group", 2, "toy222", "notr"), ("group", 1, "toy222", "rccl")])
 def test_capi_build_sharded(mode, size, name, variant):
     """fisdf_build_sharded (SURVEY §8(e) through the C-ABI, no torch): SIZE ranks on GPU 0
     (tests/capi_shard_worker.py), the collectives from the caller (host: a file mailbox per
