@@ -8,10 +8,13 @@ are evaluated once on the host and are resident in HBM before the timed region.
 
   python bench.py [--gpus N --steps K --warmup W] [--config c3|c2|c1] [--no-cpu-baseline]
 
-For N > 1 launch with torch.distributed.run; the fitted q are sharded over ranks (RCCL
-all-to-all of y pieces, reduce-scatter of W_s rows, broadcast of W_0), rank 0 prints one
-JSON line.  FISDF_BENCH_BACKEND=gloo (rehearsal only: ranks may share one GPU, collectives
-staged through the host) replaces RCCL.
+For N > 1 the fitted q are sharded over N ranks, one process per GPU (RCCL all-to-all of y
+pieces, reduce-scatter of W_s rows, broadcast of W_0), and rank 0 prints one JSON line.  Under
+torch.distributed.run (WORLD_SIZE set) each process is one rank; `python bench.py --gpus N` on
+its own starts torch.distributed.run --nproc-per-node N as a child (launch_ranks) and exits with
+its status — non-zero, with a message, if fewer than N GPUs are visible.
+FISDF_BENCH_BACKEND=gloo (rehearsal only: ranks may share one GPU, collectives staged through
+the host) replaces RCCL.
 """
 import argparse
 import json
@@ -251,17 +254,88 @@ def emulate_ranks(args):
     print(json.dumps(out))
 
 
+def _backend():
+    backend = os.environ.get("FISDF_BENCH_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        raise SystemExit(f"FISDF_BENCH_BACKEND must be nccl or gloo, not {backend!r}")
+    return backend
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_cmd(argv, n, port):
+    """The child command that runs `n` ranks of this bench, one process per GPU
+    (torch.distributed.run on 127.0.0.1), with the caller's own arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` started as ONE process (no WORLD_SIZE in the environment): start the
+    N-rank job as a child process — torch.distributed.run, one rank per GPU over RCCL — and exit
+    with its status.  Rank 0 of the child prints the JSON line (n_gpus = the communicator size).
+    Nothing here touches the GPU (device_count does not initialise HIP on this image), so the
+    parent never holds a device while its child runs; with fewer than N devices it stops with a
+    message instead of running fewer ranks.  FISDF_BENCH_BACKEND=gloo (rehearsal: ranks share
+    the visible GPUs, collectives staged through the host) skips the device-count check."""
+    import subprocess
+    backend = _backend()
+    if backend == "nccl" and os.environ.get("FISDF_BENCH_PROBE") != "1":
+        import torch
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs (one rank per GPU "
+                  f"over RCCL), this host has {have}", file=sys.stderr)
+            return 2
+    cmd = rank_launch_cmd(argv, args.gpus, _free_port())
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
+def probe_ranks(args):
+    """FISDF_BENCH_PROBE=1 (tests, no GPU needed): join the process group the bench would use
+    (gloo), all-reduce one value per rank and print the line rank 0 would head its result with —
+    the launcher's N-rank path without the ISDF build."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    dist.init_process_group("gloo")
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    if dist.get_rank() == 0:
+        print(json.dumps({"probe": True, "n_gpus": dist.get_world_size(), "world_env": world,
+                          "allreduce_sum": float(t.item()), "gpus_arg": args.gpus}))
+    dist.destroy_process_group()
+    return 0
+
+
 def main():
     args = parse()
     if args.emulate_ranks > 0:
         return emulate_ranks(args)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, sys.argv[1:])
+    if os.environ.get("FISDF_BENCH_PROBE") == "1":
+        return probe_ranks(args)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    backend = os.environ.get("FISDF_BENCH_BACKEND", "nccl")
-    if backend not in ("nccl", "gloo"):
-        raise SystemExit(f"FISDF_BENCH_BACKEND must be nccl or gloo, not {backend!r}")
+    backend = _backend()
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: running (and reporting) "
+              f"{world} ranks", file=sys.stderr)
+    if backend == "nccl" and torch.cuda.device_count() < world:
+        print(f"bench.py: {world} ranks need {world} visible GPUs (one rank per GPU over RCCL), "
+              f"this host has {torch.cuda.device_count()}", file=sys.stderr)
+        return 2
     # one GPU per rank; a gloo rehearsal may place several ranks on one GPU
     dev = local if backend == "nccl" else local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev)
@@ -273,6 +347,7 @@ def main():
         else:
             dist.init_process_group("gloo")
         comm = dist.group.WORLD
+        world = dist.get_world_size(comm)          # the communicator's size is what is reported
 
     from fisdf import ISDF
     from fisdf import _lib
@@ -462,4 +537,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -1392,8 +1392,9 @@ int fisdf_build_y_qs(fisdf_ctx* c, const void* fv, long f_kstride, int g0, int n
     const size_t yw = y_fused_workspace(kmesh, nip, nao, nblk);
     // self-conjugate q stored real (half their bytes) when the caller's fit reads them so:
     // the composite build on the whole grid (c->y_real_store)
+    // (a 64-bit mask of q: the fused kernel runs only for nk <= 64, so larger meshes keep it 0)
     unsigned long long rmask = 0;
-    if (c->y_real_store && g0 == 0 && nblk == ngrid)
+    if (c->y_real_store && g0 == 0 && nblk == ngrid && nk <= 64)
       for (int i = 0; i < nq; ++i) {
         const int q = h_qs[i];
         const int i2 = q % kmesh[2], i1 = (q / kmesh[2]) % kmesh[1], i0 = q / (kmesh[1] * kmesh[2]);

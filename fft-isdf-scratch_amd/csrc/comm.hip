@@ -14,6 +14,7 @@
 
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "common.h"
 #include "fisdf.h"
@@ -25,6 +26,7 @@ struct Rccl {
   std::string err;
   decltype(&ncclGetUniqueId) get_unique_id = nullptr;
   decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommInitAll) comm_init_all = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
   decltype(&ncclGroupStart) group_start = nullptr;
@@ -54,6 +56,7 @@ const Rccl& rccl() {
     };
     sym(r.get_unique_id, "ncclGetUniqueId");
     sym(r.comm_init_rank, "ncclCommInitRank");
+    sym(r.comm_init_all, "ncclCommInitAll");
     sym(r.comm_destroy, "ncclCommDestroy");
     sym(r.error_string, "ncclGetErrorString");
     sym(r.group_start, "ncclGroupStart");
@@ -113,7 +116,41 @@ int cb_broadcast(void* user, void* buf, size_t bytes, int root, void* stream) {
                                 static_cast<hipStream_t>(stream)));
 }
 
+void fill_comm(RcclComm* u, int rank, int size, fisdf_comm* out) {
+  std::memset(out, 0, sizeof(*out));
+  out->rank = rank;
+  out->size = size;
+  out->user = u;
+  out->all_to_all = cb_all_to_all;
+  out->reduce_scatter_f64 = cb_reduce_scatter;
+  out->allreduce_f64 = cb_allreduce;
+  out->broadcast = cb_broadcast;
+}
+
 }  // namespace
+
+namespace fisdf {
+
+// every rank of a one-process group at once (fisdf_group, FISDF_GROUP_RCCL): ncclCommInitAll on
+// the devices in rank order, from the calling thread — all-or-nothing, so a device that cannot
+// join fails the whole call instead of leaving the other ranks blocked inside ncclCommInitRank
+int rccl_init_all(int n, const int* devices, fisdf_comm* out) {
+  FISDF_CHECK(n >= 1 && devices && out, "comm_rccl_init_all: bad arguments");
+  const Rccl& R = rccl();
+  FISDF_CHECK(R.ok, "comm_rccl_init_all: " + R.err);
+  std::vector<ncclComm_t> comms(n, nullptr);
+  const ncclResult_t e = R.comm_init_all(comms.data(), n, devices);
+  FISDF_CHECK(e == ncclSuccess, std::string("ncclCommInitAll: ") + R.error_string(e));
+  for (int r = 0; r < n; ++r) {
+    auto* u = new RcclComm();
+    u->comm = comms[r];
+    u->size = n;
+    fill_comm(u, r, n, &out[r]);
+  }
+  return 0;
+}
+
+}  // namespace fisdf
 
 static_assert(sizeof(ncclUniqueId) == FISDF_COMM_ID_BYTES, "RCCL unique id size");
 
@@ -146,14 +183,7 @@ int fisdf_comm_rccl_init(const unsigned char* h_id, int rank, int size, int devi
     delete u;
     FISDF_CHECK(false, std::string("ncclCommInitRank: ") + R.error_string(e));
   }
-  std::memset(out, 0, sizeof(*out));
-  out->rank = rank;
-  out->size = size;
-  out->user = u;
-  out->all_to_all = cb_all_to_all;
-  out->reduce_scatter_f64 = cb_reduce_scatter;
-  out->allreduce_f64 = cb_allreduce;
-  out->broadcast = cb_broadcast;
+  fill_comm(u, rank, size, out);
   return 0;
 }
 

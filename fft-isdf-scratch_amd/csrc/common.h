@@ -3,7 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <mutex>
+#include <set>
 #include <string>
+#include <tuple>
 
 namespace fisdf {
 
@@ -38,6 +41,20 @@ void set_error(const std::string& msg);
     int _r = (call);           \
     if (_r != 0) return _r;    \
   } while (0)
+
+// ---- hipFuncAttributeMaxDynamicSharedMemorySize, set once per (kernel, device, size): safe from
+// the rank threads of a fisdf_group (several devices, concurrent first calls)
+inline int func_max_lds(const void* fn, int bytes) {
+  static std::mutex m;
+  static std::set<std::tuple<const void*, int, int>> done;
+  int dev = 0;
+  FISDF_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(m);
+  if (done.count({fn, dev, bytes})) return 0;
+  FISDF_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  done.insert({fn, dev, bytes});
+  return 0;
+}
 
 // ---- kernel-exact stage timing: when set, the next zgemm()/herk() call's kernels record their
 // execution span {first workgroup start, last wave end} (s_memrealtime, 100 MHz ticks) into

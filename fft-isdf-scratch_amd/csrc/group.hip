@@ -4,8 +4,8 @@
 // through the same entries an MPI caller uses (fisdf_build_sharded, fisdf_get_jk).
 //
 // Collectives (kind):
-//   FISDF_GROUP_RCCL  the library's RCCL fisdf_comm (comm.hip), one communicator per rank made
-//                     by concurrent ncclCommInitRank calls; distinct devices (xGMI)
+//   FISDF_GROUP_RCCL  the library's RCCL fisdf_comm (comm.hip), one communicator per rank, all
+//                     made by one ncclCommInitAll (all-or-nothing); distinct devices (xGMI)
 //   FISDF_GROUP_COPY  device copies between the ranks' own buffers (hipMemcpyPeerAsync, which
 //                     also serves ranks sharing a device) ordered by per-rank events, with a host
 //                     barrier between publishing and reading; sums in rank order on every rank,
@@ -192,6 +192,9 @@ int copy_broadcast(void* user, void* buf, size_t bytes, int root, void* stream) 
 }
 
 }  // namespace
+
+int rccl_init_all(int n, const int* devices, fisdf_comm* out);  // comm.hip
+
 }  // namespace fisdf
 
 using namespace fisdf;
@@ -248,7 +251,8 @@ int fisdf_group_create(int n, const int* devices, int kind, fisdf_group** out) {
   g->n = n;
   g->kind = kind;
   g->dev.assign(devices, devices + n);
-  auto fail = [&](const std::string& m) {
+  // m by value: a message taken from g->err must outlive the group it belongs to
+  auto fail = [&](std::string m) {
     fisdf_group_destroy(g);
     FISDF_CHECK(false, "group_create: " + m);
     return -1;
@@ -293,12 +297,11 @@ int fisdf_group_create(int n, const int* devices, int kind, fisdf_group** out) {
       c.broadcast = copy_broadcast;
     }
   } else {
-    unsigned char id[FISDF_COMM_ID_BYTES];
-    if (fisdf_comm_rccl_unique_id(id) != 0) return fail(fisdf_last_error(nullptr));
     g->hub.bar.n = n;
-    // ncclCommInitRank blocks until every rank has joined: one thread per rank
-    if (run_ranks(g, [&](int r) { return fisdf_comm_rccl_init(id, r, n, g->dev[r], &g->comm[r]); }))
-      return fail(g->err);
+    // one call for every rank (ncclCommInitAll): no rank can be left blocked in its init when
+    // another rank's device fails to join
+    if (rccl_init_all(n, g->dev.data(), g->comm.data()) != 0)
+      return fail(fisdf_last_error(nullptr));
   }
   *out = g;
   return 0;

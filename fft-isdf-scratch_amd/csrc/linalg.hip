@@ -1532,12 +1532,8 @@ int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long 
   cplx* XT = work;
   cplx* FT = work + (size_t)nsl * nao * nip;
   const size_t tl = sizeof(cplx) * 64 * (size_t)(nao + 1);
-  static bool tattr = false;
-  if (!tattr) {  // nao up to 128: 64 x 129 x 16 B of LDS
-    FISDF_HIP(hipFuncSetAttribute((const void*)yf_transpose_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 132 * 1024));
-    tattr = true;
-  }
+  // nao up to 128: 64 x 129 x 16 B of LDS
+  FISDF_TRY(func_max_lds((const void*)yf_transpose_kernel, 132 * 1024));
   hipLaunchKernelGGL(yf_transpose_kernel, dim3((nip + 63) / 64, nsl), dim3(256), tl, s, X,
                      (long)nip * nao, nip, nao, plan, XT);
   FISDF_HIP(hipGetLastError());
@@ -1551,12 +1547,7 @@ int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long 
   static const int mode = getenv("FISDF_YF_MODE") ? atoi(getenv("FISDF_YF_MODE")) : 0;
 #define FISDF_YF(a, b, c)                                                                      \
   if (n0 == a && n1 == b && n2 == c) {                                                         \
-    static bool attr = false;                                                                  \
-    if (!attr) {                                                                               \
-      FISDF_HIP(hipFuncSetAttribute((const void*)y_fused_kernel<a, b, c>,                      \
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));   \
-      attr = true;                                                                             \
-    }                                                                                          \
+    FISDF_TRY(func_max_lds((const void*)y_fused_kernel<a, b, c>, 80 * 1024));                \
     hipLaunchKernelGGL((y_fused_kernel<a, b, c>), dim3((unsigned)grid), dim3(256), lds, s, XT,  \
                        nip, nao, FT, m, nIt, nGt, plan, qmask, rmask & qmask, yT, qs, Is, goff, \
                        mode, gpair);                                                          \

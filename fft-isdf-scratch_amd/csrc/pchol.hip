@@ -1523,12 +1523,7 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
   FISDF_HIP(hipMemsetAsync(rec, 0, 2 * G * sizeof(u32x4), s));
   FISDF_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
   FISDF_HIP(hipMemsetAsync(rank, 0, sizeof(int), s));
-  static bool attr = false;
-  if (!attr) {
-    FISDF_HIP(hipFuncSetAttribute((const void*)pchol_select_coop,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
-    attr = true;
-  }
+  FISDF_TRY(func_max_lds((const void*)pchol_select_coop, (int)kLds));
   // FISDF_SEL_PROF=1: per-step phase timestamps of workgroup 0 (timing probe), printed below;
   // one 8192-step buffer per device, the probe off for longer selections
   constexpr int kProfSteps = 8192;
@@ -1623,12 +1618,7 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
   FISDF_HIP(hipMemsetAsync(pub, 0, sizeof(u32x4) * SB_NPUB, s));  // no stale batch words
   FISDF_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
   FISDF_HIP(hipMemsetAsync(rank, 0, sizeof(int), s));
-  static bool attr = false;
-  if (!attr) {
-    FISDF_HIP(hipFuncSetAttribute((const void*)pchol_select_batch,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
-    attr = true;
-  }
+  FISDF_TRY(func_max_lds((const void*)pchol_select_batch, (int)kLds));
   // FISDF_SEL_PROF=1: per-batch phase timestamps of the leader (timing probe), printed below
   constexpr int kProfBatches = 8192;
   static unsigned long long* prof[64] = {};

@@ -8,7 +8,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _lib
-from .cell import lattice_translations
+from .cell import cell_rcut, lattice_translations
 
 
 def _shell_tables(cell):
@@ -40,7 +40,7 @@ def eval_ao_band_gpu(device, cell, coords, kpts):
                     atoms.ctypes.data_as(dp), len(sh_l), sh_atom.ctypes.data_as(ip),
                     sh_l.ctypes.data_as(ip), sh_np.ctypes.data_as(ip), exps.ctypes.data_as(dp),
                     coefs.ctypes.data_as(dp), len(tn), tn.ctypes.data_as(ip), len(kpts),
-                    kpts.ctypes.data_as(dp), ap, float(cell.rcut()), nao, _lib.ptr(out))
+                    kpts.ctypes.data_as(dp), ap, cell_rcut(cell), nao, _lib.ptr(out))
     return out
 
 
@@ -75,5 +75,5 @@ def eval_ao_kpts_gpu(device, cell, coords, kmesh):
                     atoms.ctypes.data_as(dp), len(sh_l), sh_atom.ctypes.data_as(ip),
                     sh_l.ctypes.data_as(ip), sh_np.ctypes.data_as(ip), exps.ctypes.data_as(dp),
                     coefs.ctypes.data_as(dp), len(tn), tn.ctypes.data_as(ip), kmp, ap,
-                    float(cell.rcut()), nao, _lib.ptr(out))
+                    cell_rcut(cell), nao, _lib.ptr(out))
     return out

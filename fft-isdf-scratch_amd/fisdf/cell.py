@@ -182,6 +182,16 @@ class Cell:
         rx = [np.fft.fftfreq(n, 1.0 / n) for n in mesh]
         return cartesian_prod(rx) @ self.reciprocal_vectors()
 
+    def pbc_eval_gto(self, eval_name, coords, kpts=None):
+        """``Cell.pbc_eval_gto(eval_name, coords, kpts)`` [pyscf] for AO values ('GTOval'):
+        (nk, ng, nao) complex for a (nk, 3) ``kpts``, (ng, nao) for one k-point or None — the
+        entry the reference calls for its AO inputs (fftisdf.py:367-370)."""
+        if eval_name not in ("GTOval", "GTOval_sph"):
+            raise NotImplementedError(f"pbc_eval_gto: {eval_name!r} (AO values only)")
+        k = np.zeros((1, 3)) if kpts is None else np.asarray(kpts, float)
+        out = eval_ao_band(self, coords, k.reshape(-1, 3))
+        return out[0] if kpts is None or k.ndim == 1 else out
+
     def rcut(self):
         amin = min(float(e.min()) for (_, _, e, _, _) in self.shells)
         lmax = max(l for (_, l, _, _, _) in self.shells)
@@ -189,6 +199,38 @@ class Cell:
         for _ in range(3):  # include the r^l prefactor
             r = math.sqrt((-math.log(self.precision) + lmax * math.log(max(r, 1.0))) / amin)
         return r
+
+
+def cell_rcut(cell):
+    """``cell.rcut``: a method on this module's Cell, an attribute on a PySCF Cell."""
+    r = cell.rcut
+    return float(r() if callable(r) else r)
+
+
+def bloch_ao(cell, coords, kpts, kmesh=None):
+    """Bloch AO values chi_k(r) (nk, ng, nao) complex128 on the host, for any cell object.
+
+    * a cell of this module (explicit ``shells``): the restatement — ``eval_ao_kpts`` on the
+      k-mesh grid when ``kmesh`` is given (kpts = make_kpts(cell, kmesh)), else ``eval_ao_band``;
+    * any other cell with PySCF's ``pbc_eval_gto`` (a ``pyscf.pbc.gto.Cell`` or a duck-typed
+      one): ``cell.pbc_eval_gto("GTOval", coords, kpts=kpts)``, exactly the reference's AO input
+      (fftisdf.py:367-370; ``aoR_loop`` / ``KNumInt.block_loop``, :327-355, evaluates the same
+      values block by block)."""
+    coords = np.asarray(coords, float)
+    kpts = np.asarray(kpts, float).reshape(-1, 3)
+    if hasattr(cell, "shells"):
+        if kmesh is not None:
+            return eval_ao_kpts(cell, coords, kmesh)
+        return eval_ao_band(cell, coords, kpts)
+    if not hasattr(cell, "pbc_eval_gto"):
+        raise TypeError(f"{type(cell).__name__}: a cell needs pbc_eval_gto (PySCF Cell protocol) "
+                        "or explicit shells (fisdf.cell.Cell) to supply AO values")
+    ao = cell.pbc_eval_gto("GTOval", coords, kpts=kpts)
+    ao = np.asarray(ao)
+    nao = cell.nao_nr()
+    if ao.shape != (len(kpts), len(coords), nao):   # a single k-point may come back unbatched
+        ao = ao.reshape(len(kpts), len(coords), nao)
+    return ao.astype(np.complex128, copy=False)
 
 
 def make_kpts(cell, kmesh):
@@ -223,7 +265,7 @@ def lattice_translations(cell, coords):
     (the box of eval_ao_folded), cartesian order."""
     coords = np.asarray(coords, float)
     b = cell.reciprocal_vectors()
-    rc = cell.rcut()
+    rc = cell_rcut(cell)
     frac = coords @ b.T / (2 * np.pi)   # grid extent in fractional coords (may be wrapped)
     fmin, fmax = frac.min(axis=0), frac.max(axis=0)
     reach = rc * np.linalg.norm(b, axis=1) / (2 * np.pi)
@@ -244,7 +286,7 @@ def eval_ao_folded(cell, coords, kmesh):
     nimg = int(np.prod(kmesh))
     nao = cell.nao_nr()
     a = cell.lattice_vectors()
-    rc = cell.rcut()
+    rc = cell_rcut(cell)
     out = np.zeros((nimg, ng, nao))
     atom_xyz = cell.atom_coords()
     rc2 = rc * rc
@@ -282,7 +324,7 @@ def eval_ao_band(cell, coords, kpts):
     ng = coords.shape[0]
     nao = cell.nao_nr()
     a = cell.lattice_vectors()
-    rc2 = cell.rcut() ** 2
+    rc2 = cell_rcut(cell) ** 2
     atom_xyz = cell.atom_coords()
     out = np.zeros((len(kpts), ng, nao), complex)
     shells_by_atom = {}

@@ -206,9 +206,9 @@ def get_coul_svd(df_obj, k0=10.0, kmesh=None, cisdf=0.6, verbose=5, blksize=1600
     if isdf.ao_on_gpu and hasattr(cell, "shells"):
         from .ao import eval_ao_kpts_gpu
         xg = eval_ao_kpts_gpu(d, cell, coords0, (1, 1, 1))               # :49-50, Gamma AOs
-    else:
-        from .cell import eval_ao_kpts
-        xg = d.to_dev(eval_ao_kpts(cell, coords0, (1, 1, 1)))
+    else:                                # any cell with pbc_eval_gto (PySCF protocol)
+        from .cell import bloch_ao
+        xg = d.to_dev(bloch_ao(cell, coords0, np.zeros((1, 3)), (1, 1, 1)))
     nao = cell.nao_nr()
     piv = np.zeros(nip, np.int32)
     npiv, full = c_int(), c_int()

@@ -24,7 +24,7 @@ import time
 import numpy as np
 
 from . import _lib, kshard
-from .cell import eval_ao_kpts, madelung, make_kpts
+from .cell import bloch_ao, madelung, make_kpts
 
 log = logging.getLogger("fisdf")
 
@@ -109,7 +109,10 @@ class _Device:
         if os.environ.get("FISDF_PINNED_D2H", "1") == "0":
             return x.cpu().numpy()
         h = self.torch.empty(tuple(x.shape), dtype=x.dtype, pin_memory=True)
-        h.copy_(x, non_blocking=True)
+        # on the context's stream (the one the library produced x on and the one waited for
+        # below), whatever stream the caller has made current
+        with self.torch.cuda.stream(self.stream):
+            h.copy_(x, non_blocking=True)
         self.stream.synchronize()
         return h.numpy()
 
@@ -189,14 +192,27 @@ class InterpolativeSeparableDensityFitting:
         return self.cell.gen_uniform_grids(self.mesh)
 
     def _eval_ao(self, coords):
-        """Bloch AOs at ``coords`` on the device: the GPU evaluator (ao_on_gpu, default) or
-        the host restatement uploaded (cells without ``shells``, e.g. a PySCF cell, use the
-        host path through ``eval_ao_kpts``)."""
+        """Bloch AOs (nk, ng, nao) at ``coords`` on the device, for the k-mesh of ``build``.
+
+        A cell of ``fisdf.cell`` (explicit ``shells``) is evaluated by the GPU evaluator
+        (``ao_on_gpu``, default; fisdf_eval_ao).  Any other cell is asked for its AO values the
+        way the reference asks PySCF — ``cell.pbc_eval_gto("GTOval", coords, kpts=self.kpts)``
+        (fftisdf.py:367-370; the FFT-grid values of ``aoR_loop``, :327-355, are the same
+        function on ``grids.coords``) — block by block on the host (``blksize`` points at a
+        time, so host memory stays at one block) and uploaded into one device array."""
         kmesh = self._kmesh()
         if self.ao_on_gpu and hasattr(self.cell, "shells"):
             from .ao import eval_ao_kpts_gpu
             return eval_ao_kpts_gpu(self.device, self.cell, coords, kmesh)
-        return self.device.to_dev(eval_ao_kpts(self.cell, coords, kmesh))
+        coords = np.asarray(coords, float)
+        ng, nk = coords.shape[0], len(self.kpts)
+        out = self.device.empty((nk, ng, self.cell.nao_nr()))
+        blk = max(1, int(self.blksize))
+        for g0 in range(0, ng, blk):
+            g1 = min(g0 + blk, ng)
+            out[:, g0:g1] = self.device.to_dev(bloch_ao(self.cell, coords[g0:g1], self.kpts,
+                                                        kmesh))
+        return out
 
     def preload_ao(self):
         """Evaluate the AO inputs (PySCF's job in the reference) on the device before build."""
@@ -226,7 +242,7 @@ class InterpolativeSeparableDensityFitting:
         kmesh = self._kmesh()
         for g0 in range(0, coords.shape[0], blksize):
             g1 = min(g0 + blksize, coords.shape[0])
-            yield (eval_ao_kpts(self.cell, coords[g0:g1], kmesh),), g0, g1
+            yield (bloch_ao(self.cell, coords[g0:g1], self.kpts, kmesh),), g0, g1
 
     def select_interpolation_points(self, x0=None, phase=None):
         """fftisdf.py:357-388 on the GPU; returns X = x0[:, perm[:nip], :] as a host array."""
@@ -844,9 +860,12 @@ def _band_aos(df_obj, kb):
     cache = st.setdefault("band_aos", {})
     key = kb.round(12).tobytes()
     if key not in cache:
-        from .ao import eval_ao_band_gpu
         pts = df_obj.cell.gen_uniform_grids(df_obj.m0)[df_obj.perm]
-        cache[key] = eval_ao_band_gpu(df_obj.device, df_obj.cell, pts, kb)
+        if df_obj.ao_on_gpu and hasattr(df_obj.cell, "shells"):
+            from .ao import eval_ao_band_gpu
+            cache[key] = eval_ao_band_gpu(df_obj.device, df_obj.cell, pts, kb)
+        else:                                   # a PySCF-protocol cell: pbc_eval_gto at kb
+            cache[key] = df_obj.device.to_dev(bloch_ao(df_obj.cell, pts, kb))
     return cache[key]
 
 

@@ -254,8 +254,10 @@ def main(case, rank, size, d, mode, variant=""):
 
 
 def main_group(case, size, d, variant=""):
-    """All SIZE ranks in this one process through fisdf_group (FISDF_GROUP_COPY, every rank on
-    GPU 0, one host thread per rank inside the library): writes the same rank{r}.npz files."""
+    """All SIZE ranks in this one process through fisdf_group (FISDF_GROUP_COPY unless the
+    variant says rccl; one host thread per rank inside the library): writes the same rank{r}.npz
+    files.  Every rank on GPU 0, or — variants multidev / multidev_rccl — rank r on GPU r, its
+    inputs and outputs uploaded to and read from its own device."""
     from cases import inputs
     cell, kmesh, m0, c0, x0, coords, chi, dm = inputs(case)
     nao = cell.nao_nr()
@@ -267,14 +269,20 @@ def main_group(case, size, d, variant=""):
         if rc != 0:
             raise RuntimeError(f"{name}: {lib.fisdf_last_error(ctx).decode()}")
 
-    ctx = C.c_void_p()
-    assert lib.fisdf_create(0, None, C.byref(ctx)) == 0, lib.fisdf_last_error(None)
+    multidev = variant.startswith("multidev")
+    devices = list(range(size)) if multidev else [0] * size
+    ctxs = {}
+    for dev in sorted(set(devices)):          # one plain context per device: memory + copies
+        c_ = C.c_void_p()
+        assert lib.fisdf_create(dev, None, C.byref(c_)) == 0, lib.fisdf_last_error(None)
+        ctxs[dev] = c_
+    ctx = ctxs[0]
 
-    def upload(a):
+    def upload(a, dev=0):
         a = np.ascontiguousarray(a)
         p = C.c_void_p()
-        call(ctx, "fisdf_malloc", C.c_size_t(a.nbytes), C.byref(p))
-        call(ctx, "fisdf_memcpy_htod", p, a.ctypes.data_as(C.c_void_p), C.c_size_t(a.nbytes))
+        call(ctxs[dev], "fisdf_malloc", C.c_size_t(a.nbytes), C.byref(p))
+        call(ctxs[dev], "fisdf_memcpy_htod", p, a.ctypes.data_as(C.c_void_p), C.c_size_t(a.nbytes))
         return p
 
     def download(c, ptr, shape, dtype=complex):
@@ -283,12 +291,14 @@ def main_group(case, size, d, variant=""):
              C.c_size_t(h.nbytes))
         return h
 
-    def alloc(nbytes):
+    def alloc(nbytes, dev=0):
         p = C.c_void_p()
-        call(ctx, "fisdf_malloc", C.c_size_t(nbytes), C.byref(p))
+        call(ctxs[dev], "fisdf_malloc", C.c_size_t(nbytes), C.byref(p))
         return p
 
-    d_x0, d_f, d_dms = upload(x0), upload(chi), upload(dms.astype(np.complex128))
+    up = {dev: (upload(x0, dev), upload(chi, dev), upload(dms.astype(np.complex128), dev))
+          for dev in ctxs}
+    d_x0, d_f, d_dms = up[0]
     km, kp = _lib.iarr(kmesh)
     me, mp = _lib.iarr(cell.mesh)
     aa, ap = _lib.darr(cell.a.ravel())
@@ -298,29 +308,29 @@ def main_group(case, size, d, variant=""):
     kind = _lib.GROUP_COPY
     if variant == "notr":
         opts.time_reversal = 0
-    elif variant == "rccl":      # the group's RCCL collectives (distinct devices: one rank here)
+    elif variant in ("rccl", "multidev_rccl"):   # RCCL: distinct devices (one rank on one GPU)
         kind = _lib.GROUP_RCCL
-    elif variant:
+    elif variant not in ("", "multidev"):
         raise ValueError(variant)
     trace = os.environ.get("FISDF_WORKER_TRACE") is not None
     say = (lambda m: print(m, file=sys.stderr, flush=True)) if trace else (lambda m: None)  # noqa: E731
-    devs, devp = _lib.iarr([0] * size)
+    devs, devp = _lib.iarr(devices)
     g = C.c_void_p()
     say("group_create")
     assert lib.fisdf_group_create(size, devp, kind, C.byref(g)) == 0, \
         lib.fisdf_last_error(None)
-    ptrs = lambda p: (C.c_void_p * size)(*([p.value] * size))  # noqa: E731
+    ptrs = lambda i: (C.c_void_p * size)(*[up[dev][i].value for dev in devices])  # noqa: E731
     nip = C.c_int()
     say("group_build")
-    rc = lib.fisdf_group_build(g, ptrs(d_x0), x0.shape[1], ptrs(d_f), nao, kp, mp, ap,
+    rc = lib.fisdf_group_build(g, ptrs(0), x0.shape[1], ptrs(1), nao, kp, mp, ap,
                                C.byref(opts), C.byref(nip))
     assert rc == 0, lib.fisdf_group_last_error(g)
     nip = nip.value
     nbytes = dms.size * 16
     say("group_get_jk")
-    vjs = [alloc(nbytes) for _ in range(size)]
-    vks = [alloc(nbytes) for _ in range(size)]
-    rc = lib.fisdf_group_get_jk(g, ptrs(d_dms), 2, 1, 1, (C.c_void_p * size)(*[v.value for v in vjs]),
+    vjs = [alloc(nbytes, dev) for dev in devices]
+    vks = [alloc(nbytes, dev) for dev in devices]
+    rc = lib.fisdf_group_get_jk(g, ptrs(2), 2, 1, 1, (C.c_void_p * size)(*[v.value for v in vjs]),
                                 (C.c_void_p * size)(*[v.value for v in vks]))
     assert rc == 0, lib.fisdf_group_last_error(g)
     say("results")
@@ -340,8 +350,8 @@ def main_group(case, size, d, variant=""):
         out["wq"] = (download(rctx, r.d_Wq, (nfit, nip, nip)) if nfit
                      else np.zeros((0, nip, nip), complex))
         out["ws_rows"] = download(rctx, r.d_Ws, (r.nk, r.row1 - r.row0, nip), np.float64)
-        out["vj"] = download(ctx, vjs[rank].value, dms.shape)
-        out["vk"] = download(ctx, vks[rank].value, dms.shape)
+        out["vj"] = download(ctxs[devices[rank]], vjs[rank].value, dms.shape)
+        out["vk"] = download(ctxs[devices[rank]], vks[rank].value, dms.shape)
         outs.append(out)
     say("group_destroy")
     assert lib.fisdf_group_destroy(g) == 0
@@ -360,9 +370,14 @@ def main_group(case, size, d, variant=""):
     outs[0]["ref_vj"] = download(ctx, vjs[0].value, dms.shape)
     outs[0]["ref_vk"] = download(ctx, vks[0].value, dms.shape)
     say("reference done")
-    for p in [d_x0, d_f, d_dms] + vjs + vks:
-        call(ctx, "fisdf_free", p)
-    assert lib.fisdf_destroy(ctx) == 0
+    for rank, dev in enumerate(devices):
+        for p in (vjs[rank], vks[rank]):
+            call(ctxs[dev], "fisdf_free", p)
+    for dev, bufs in up.items():
+        for p in bufs:
+            call(ctxs[dev], "fisdf_free", p)
+    for c_ in ctxs.values():
+        assert lib.fisdf_destroy(c_) == 0
     say("freed")
     assert "torch" not in sys.modules, "the C-ABI path must not need torch"
     for rank, out in enumerate(outs):

@@ -17,6 +17,11 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+def _device_count():
+    import torch
+    return torch.cuda.device_count()
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("name", ["toy222", "toy333_fr"])
 def test_capi_build_get_jk_torch_free(name):
@@ -66,7 +71,8 @@ def test_capi_build_get_jk_torch_free(name):
     ("host", 2, "toy222", ""), ("host", 3, "toy331_fr", ""), ("rccl", 1, "toy222", ""),
     ("host", 2, "toy331_fr", "svd"), ("host", 3, "toy222", "notr"),
     ("host", 6, "toy331_fr", ""),    # 5 fitted q on 6 ranks: one rank fits none
-    ("group", 3, "toy331_fr", ""), ("group", 2, "toy222", "notr"), ("group", 1, "toy222", "rccl")])
+    ("group", 3, "toy331_fr", ""), ("group", 2, "toy222", "notr"), ("group", 1, "toy222", "rccl"),
+    ("group", 2, "toy331_fr", "multidev"), ("group", 2, "toy331_fr", "multidev_rccl")])
 def test_capi_build_sharded(mode, size, name, variant):
     """fisdf_build_sharded (SURVEY §8(e) through the C-ABI, no torch): SIZE ranks on GPU 0
     (tests/capi_shard_worker.py), the collectives from the caller (host: a file mailbox per
@@ -76,7 +82,10 @@ def test_capi_build_sharded(mode, size, name, variant):
     1-GPU get_jk to rounding.  Variants: fit="svd" (the minimum-norm operator on every q) and
     time reversal off (all nk q fitted and shared).  group: every rank in one process through
     fisdf_group (SURVEY §8(b)'s multi-device handle: a thread and a stream per rank, the
-    collectives as device copies between the ranks' buffers)."""
+    collectives as device copies between the ranks' buffers); multidev: rank r on GPU r (device
+    copies across xGMI, or RCCL with 2 ranks), skipped where fewer GPUs are visible."""
+    if variant.startswith("multidev") and _device_count() < size:
+        pytest.skip(f"needs {size} GPUs (one rank per device)")
     with tempfile.TemporaryDirectory() as tmp:
         nproc = 1 if mode == "group" else size   # group: all ranks in one process (fisdf_group)
         procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "capi_shard_worker.py"), name,
