@@ -141,6 +141,8 @@ struct fisdf_ctx {
   // priority fisdf_set_factor_priority asked for (side_hi: the priority it was created with)
   hipStream_t side = nullptr;
   int factor_hi = 0, side_hi = -1;
+  std::vector<hipStream_t> pad;  // FISDF_PAD_QUEUES (ensure_side)
+  void* pad_buf = nullptr;
   hipEvent_t ev_x4 = nullptr, ev_fac = nullptr, ev_chol = nullptr;
   bool f_fac_unjoined = false;  // ev_fac not yet waited on by the main stream (fit lanes do)
   bool f_pending = false;
@@ -187,6 +189,7 @@ struct fisdf_ctx {
     int shard_rank = 0, shard_size = 1, row0 = 0, row1 = 0;
     void* W0 = nullptr;
     bool sharded = false;
+    bool y_streamed = false;  // y formed behind the selection (fisdf_build_y_streamed)
     fisdf_comm comm{};
   } bld;
   // stream of the sharded build's all-to-all (fisdf_build_sharded), forked from `stream`
@@ -199,6 +202,30 @@ struct fisdf_ctx {
   void* alloc_user = nullptr;
   std::map<int, std::pair<void*, size_t>> owned;  // role -> library-owned buffer
   std::vector<void*> lent;                        // buffers from alloc_fn not yet returned
+  // The y build streamed behind the selection (build_impl, FISDF_Y_STREAM): while the
+  // cooperative selection runs on `stream`, aux[0] forms y in blocks of pivots as the kernel
+  // publishes them (pchol_select_coop's progress word).  ys_dev: {progress, spin error} (device
+  // ints); ws_ypiv: the pivots, context-owned so that no later arena user overwrites them under
+  // the y stream; ws_ystream: XT / FT of the fused kernel.  `ys` is the build's request, armed
+  // around the first selection only; enqueued: the y stream received the work.
+  int* ys_dev = nullptr;
+  int* ys_err_pinned = nullptr;
+  hipEvent_t ev_yerr = nullptr;
+  hipEvent_t ev_ysfork = nullptr;  // `stream` just before the selection kernel: the y stream's start
+  DevBuf ws_ypiv, ws_ystream;
+  struct YStream {
+    bool armed = false, enqueued = false;
+    bool stale = false;  // the kernel it followed failed (a stalled step): its pivots were redone
+    int aux = 1;         // the aux stream it runs on
+    const cplx* x0 = nullptr;
+    const cplx* f = nullptr;
+    int ng0 = 0, nao = 0, nip = 0, rows = 64;
+    long m = 0, fks = 0;  // grid points of the y build (columns of yT), k stride of f
+    int kmesh[3] = {0, 0, 0};
+    std::vector<int> qs;
+    cplx* yT = nullptr;
+    unsigned long long rmask = 0;
+  } ys;
 };
 
 namespace fisdf {
@@ -763,8 +790,16 @@ int fisdf_destroy(fisdf_ctx* c) {
   free_factors(c);
   if (c->f_scratch) (void)hipFree(c->f_scratch);
   if (c->f_ring) (void)hipFree(c->f_ring);
-  for (auto* w : {&c->ws_main, &c->ws_side_a, &c->ws_side_b})
+  for (int l = 0; l < 3; ++l)  // the streamed y build's workspaces may still be in use there
+    if (c->aux[l]) (void)hipStreamSynchronize(c->aux[l]);
+  if (c->ys_dev) (void)hipFree(c->ys_dev);
+  if (c->ys_err_pinned) (void)hipHostFree(c->ys_err_pinned);
+  if (c->ev_yerr) (void)hipEventDestroy(c->ev_yerr);
+  if (c->ev_ysfork) (void)hipEventDestroy(c->ev_ysfork);
+  for (auto* w : {&c->ws_main, &c->ws_side_a, &c->ws_side_b, &c->ws_ypiv, &c->ws_ystream})
     if (w->p) (void)hipFree(w->p);
+  for (hipStream_t p : c->pad) (void)hipStreamDestroy(p);
+  if (c->pad_buf) (void)hipFree(c->pad_buf);
   if (c->side) {
     (void)hipStreamSynchronize(c->side);
     (void)hipStreamDestroy(c->side);
@@ -1068,6 +1103,113 @@ int fisdf_tri_inverse(fisdf_ctx* c, const void* L, int n, int batch, void* Linv)
 // Cholesky (in that order of preference), then ONE pinned read-back of {error flag, rank, pivots}
 // and one stream synchronisation (round 2 synchronised twice through pageable copies); a
 // cooperative run that reports a stalled step is redone on the non-cooperative paths.
+// the streamed y build's work on aux[0], enqueued right after the selection kernel (so it never
+// precedes it on any queue): the fused y kernel block by block, each block's XT rows waiting on
+// the kernel's progress word (y_fused_stream).  Ordered after everything on `stream` before the
+// selection (the previous build's readers of the y buffer and workspaces included).
+static int ensure_side(fisdf_ctx* c);
+
+static int ystream_enqueue(fisdf_ctx* c, const int* piv) {
+  fisdf_ctx::YStream& Y = c->ys;
+  // the side stream first, then the aux streams: the order the unstreamed build creates them in
+  // (the runtime places a process's streams on hardware queues in creation order, and the fit's
+  // two lanes serialise when aux[0] lands elsewhere: C3 89 vs 81 ms/step, profiles/r06/lanes/)
+  FISDF_TRY(ensure_side(c));
+  FISDF_TRY(ensure_aux(c));
+  const int nq = (int)Y.qs.size();
+  const size_t yw = y_fused_workspace(Y.kmesh, Y.nip, Y.nao, (int)Y.m);
+  FISDF_CHECK(yw > 0 && nq > 0, "streamed y: the fused kernel does not apply");
+  void* wb = nullptr;
+  FISDF_TRY(devbuf_get(c->ws_ystream, yw, &wb));
+  // FISDF_Y_STREAM_AUX (read per build; A/B): the aux stream that carries the streamed y
+  const int ia = [] {
+    const char* e = getenv("FISDF_Y_STREAM_AUX");
+    const int v = e ? atoi(e) : 1;
+    return (v >= 0 && v <= 2) ? v : 1;
+  }();
+  c->ys.aux = ia;
+  hipStream_t ys = c->aux[ia];
+  aux_fork(c, ia);
+  FISDF_HIP(hipStreamWaitEvent(ys, c->ev_ysfork, 0));
+  bool handled = false;
+  {
+    StageTimer tm(c, FISDF_ST_Y, ys);
+    FISDF_TRY(y_fused_stream(ys, Y.x0, Y.ng0, Y.nao, piv, c->ys_dev, c->ys_dev + 1, Y.nip, Y.rows,
+                             Y.f, Y.fks, (int)Y.m, Y.kmesh, Y.qs.data(), nq, Y.yT,
+                             (long)Y.nip * Y.m, Y.m, 0, (cplx*)wb, yw, Y.rmask, &handled));
+  }
+  FISDF_CHECK(handled, "streamed y: nothing enqueued");
+  Y.enqueued = true;
+  return 0;
+}
+
+// after the selection: whether yT holds the y build of the selected points (the selection gave
+// the cap's points, its first pass did not fail, the q-list is the armed one); the y stream's
+// spin-error flag is queued for read-back (ev_yerr).  The caller joins aux[0] (ystream_join).
+static bool ystream_valid(fisdf_ctx* c, int nip, const int* qs, int nq) {
+  const fisdf_ctx::YStream& Y = c->ys;
+  return Y.enqueued && !Y.stale && nip == Y.nip && (int)Y.qs.size() == nq &&
+         std::equal(Y.qs.begin(), Y.qs.end(), qs);
+}
+
+static int ystream_join(fisdf_ctx* c) {
+  const int ia = c->ys.aux;
+  if (!c->ys.enqueued || c->aux_joined[ia] == c->aux_use[ia]) return 0;
+  FISDF_TRY(aux_join(c, ia));
+  FISDF_HIP(hipMemcpyAsync(c->ys_err_pinned, c->ys_dev + 1, sizeof(int), hipMemcpyDeviceToHost,
+                           c->stream));
+  FISDF_HIP(hipEventRecord(c->ev_yerr, c->stream));
+  return 0;
+}
+
+// the streamed y's bounded waits all met their pivots (call after ystream_join)
+static int ystream_check(fisdf_ctx* c) {
+  FISDF_HIP(hipEventSynchronize(c->ev_yerr));
+  FISDF_CHECK(*c->ys_err_pinned == 0, "streamed y: the selection's progress never arrived");
+  return 0;
+}
+
+// arm the streamed y for the next selection: y_q (q in qs, ascending) of rows [0, nip_max) on m
+// grid points (f: k stride fks) into yT[slot][I][g], self-conjugate q in rmask stored real.
+// *armed = false when the fused kernel does not cover the k-mesh (nothing will stream).
+static int ystream_arm(fisdf_ctx* c, const void* x0, int ng0, const void* f, long fks, long m,
+                       int nao, int nip_max, const int kmesh[3], const int* qs, int nq, void* yT,
+                       unsigned long long rmask, bool* armed) {
+  *armed = false;
+  FISDF_TRY(ystream_join(c));  // a streamed y never finished (an error in between) is joined
+  c->ys = fisdf_ctx::YStream();
+  if (nip_max <= 0 || m <= 0 || nq <= 0 || !y_fused_applies(kmesh, nao)) return 0;
+  FISDF_CHECK(x0 && f && yT && qs, "y_stream_arm: null argument");
+  if (!c->ys_dev) {
+    FISDF_HIP(hipMalloc((void**)&c->ys_dev, 4 * sizeof(int)));
+    FISDF_HIP(hipHostMalloc((void**)&c->ys_err_pinned, sizeof(int), hipHostMallocDefault));
+    FISDF_HIP(hipEventCreateWithFlags(&c->ev_yerr, hipEventDisableTiming));
+    FISDF_HIP(hipEventCreateWithFlags(&c->ev_ysfork, hipEventDisableTiming));
+  }
+  fisdf_ctx::YStream& Y = c->ys;
+  Y.x0 = (const cplx*)x0;
+  Y.f = (const cplx*)f;
+  Y.fks = fks;
+  Y.m = m;
+  Y.ng0 = ng0;
+  Y.nao = nao;
+  Y.nip = std::min(nip_max, ng0);
+  for (int i = 0; i < 3; ++i) Y.kmesh[i] = kmesh[i];
+  Y.qs.assign(qs, qs + nq);
+  Y.yT = (cplx*)yT;
+  Y.rmask = rmask;
+  // FISDF_Y_STREAM_ROWS: pivots per block (a multiple of 16; default 64)
+  static const int rows_env = [] {
+    const char* e = getenv("FISDF_Y_STREAM_ROWS");
+    const int v = e ? atoi(e) : 64;
+    return (v >= 16 && v % 16 == 0 && v <= 1024) ? v : 64;
+  }();
+  Y.rows = rows_env;
+  Y.armed = true;
+  *armed = true;
+  return 0;
+}
+
 static int select_pivots_dev(fisdf_ctx* c, const cplx* X2, double scale, int ng0, int nip_max,
                              double tol, cplx* X4, int* piv, int* rank, cplx* L, double* d,
                              int* flags, double* w, int* h_perm, int* h_rank) {
@@ -1079,11 +1221,33 @@ static int select_pivots_dev(fisdf_ctx* c, const cplx* X2, double scale, int ng0
     FISDF_HIP(hipHostMalloc((void**)&c->sel_pinned, sizeof(int) * nint, hipHostMallocDefault));
     c->sel_cap = nint;
   }
+  // an armed streamed y (build_impl, fisdf_y_stream_arm) is for this selection only
+  const bool armed = c->ys.armed;
+  c->ys.armed = false;
   for (int pass = 0; pass < 2; ++pass) {
     bool handled = false;
     const int* coop_err = nullptr;
+    // a streamed y build reads the pivots while the kernel runs: the selection then writes them
+    // to the context's own buffer and publishes its progress
+    const bool stream_y = armed && pass == 0 && c->ys.nip == nip_max;
+    int* progress = nullptr;
+    if (stream_y) {
+      void* pp = nullptr;
+      FISDF_TRY(devbuf_get(c->ws_ypiv, sizeof(int) * (size_t)nip_max, &pp));
+      piv = (int*)pp;
+      progress = c->ys_dev;
+      FISDF_HIP(hipMemsetAsync(c->ys_dev, 0, 2 * sizeof(int), c->stream));
+      // the y stream starts from here, beside the kernel (not after it)
+      FISDF_HIP(hipEventRecord(c->ev_ysfork, c->stream));
+    }
+    bool publishes = false;
     FISDF_TRY(pchol_select_real(c->stream, X2, scale, ng0, nip_max, tol, piv, rank, (double*)X4,
-                                flags, &handled, pass == 0, &coop_err));
+                                flags, &handled, pass == 0, &coop_err, progress, &publishes));
+    if (stream_y) {
+      // whatever ran, consumers waiting on the progress word are released when it has ended
+      FISDF_HIP(hipMemsetD32Async(c->ys_dev, kSelDone, 1, c->stream));
+      if (handled && publishes) FISDF_TRY(ystream_enqueue(c, piv));
+    }
     if (!handled) {
       FISDF_TRY(square_scale(c->stream, X2, scale, X4, (long)ng0 * ng0));
       void* trail = nullptr;
@@ -1098,6 +1262,7 @@ static int select_pivots_dev(fisdf_ctx* c, const cplx* X2, double scale, int ng0
     FISDF_HIP(hipMemcpyAsync(hp + 1, rank, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     FISDF_HIP(hipMemcpyAsync(hp + 2, piv, sizeof(int) * nip_max, hipMemcpyDeviceToHost, c->stream));
     FISDF_HIP(hipStreamSynchronize(c->stream));
+    if (stream_y && hp[0] != 0) c->ys.stale = true;
     if (hp[0] == 0) {
       *h_rank = hp[1];
       std::memcpy(h_perm, hp + 2, sizeof(int) * nip_max);
@@ -1581,6 +1746,20 @@ static int ensure_side(fisdf_ctx* c) {
   // (fisdf_set_factor_priority).  One side stream at a time: an extra stream changes
   // how HIP maps the context's streams onto the process's hardware queues (4 here), and two
   // fit lanes sharing a queue serialise (C3 +5 ms/step measured with a second side stream)
+  // FISDF_PAD_QUEUES=n (experiment): n extra streams, each given one small
+  // copy so the runtime maps it onto a hardware queue, created before the side stream — in the
+  // place the cooperative launch's own queue takes when the selection is launched cooperatively
+  static const int pad_env = getenv("FISDF_PAD_QUEUES") ? atoi(getenv("FISDF_PAD_QUEUES")) : 0;
+  if (pad_env > 0 && c->pad.empty()) {
+    if (!c->pad_buf) FISDF_HIP(hipMalloc(&c->pad_buf, 256));
+    for (int i = 0; i < pad_env && i < 8; ++i) {
+      hipStream_t p = nullptr;
+      FISDF_HIP(hipStreamCreateWithFlags(&p, hipStreamNonBlocking));
+      FISDF_HIP(hipMemsetAsync(c->pad_buf, 0, 256, p));
+      FISDF_HIP(hipStreamSynchronize(p));
+      c->pad.push_back(p);
+    }
+  }
   if (c->side && c->side_hi != c->factor_hi) {
     FISDF_HIP(hipStreamSynchronize(c->side));
     FISDF_HIP(hipStreamDestroy(c->side));
@@ -3087,6 +3266,45 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
     FISDF_TRY(build_alloc(c, BR_X, sizeof(cplx) * (size_t)nk * nip_ub * nao, &X));
     FISDF_TRY(build_alloc(c, BR_X4, sizeof(cplx) * (size_t)nk * nip_ub * nip_ub, &x4));
   }
+  // The y build streamed behind the selection (1-GPU composite build, time reversal, a k-mesh
+  // the fused kernel covers; FISDF_Y_STREAM=0: off): y is formed at the point cap nip_ub on
+  // aux[0] while the selection runs, and is kept when the selection returns exactly nip_ub
+  // points with time reversal confirmed — else it is discarded and built the usual way.
+  // read per build: the GPU tests compare the two paths in one process
+  const bool y_stream_env = [] {
+    const char* e = getenv("FISDF_Y_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  static const bool y_real_env = [] {  // the self-conjugate q's y real; FISDF_Y_REAL=0: off
+    const char* e = getenv("FISDF_Y_REAL");
+    return !(e && e[0] == '0');
+  }();
+  struct YsScope {  // the request is this build's only: cleared on every exit
+    fisdf_ctx* c;
+    ~YsScope() {
+      // an error between the enqueue and the join leaves the y stream joined all the same, so
+      // the buffers it writes are not handed back under it
+      (void)ystream_join(c);
+      c->ys = fisdf_ctx::YStream();
+    }
+  } ys_scope{c};
+  void* yT_pre = nullptr;  // the y buffer taken before the selection (streamed y)
+  std::vector<int> ys_qs, ys_partner;
+  std::vector<double> ys_wt;
+  if (y_stream_env && !comm && !o.perm && tr && nip_ub > 0 && y_fused_applies(kmesh, nao)) {
+    tr_classes(kmesh, true, ys_qs, ys_partner, ys_wt);
+    FISDF_TRY(build_alloc(c, BR_Y, sizeof(cplx) * (size_t)ys_qs.size() * nip_ub * ngrid, &yT_pre));
+    unsigned long long rmask = 0;
+    if (y_real_env && o.real_self_conjugate && fft3d_reads_real(mesh[0], mesh[1], mesh[2]))
+      for (int q : ys_qs) {
+        const int i2 = q % kmesh[2], i1 = (q / kmesh[2]) % kmesh[1], i0 = q / (kmesh[1] * kmesh[2]);
+        if ((2 * i0) % kmesh[0] == 0 && (2 * i1) % kmesh[1] == 0 && (2 * i2) % kmesh[2] == 0)
+          rmask |= 1ull << q;
+      }
+    bool armed = false;
+    FISDF_TRY(ystream_arm(c, x0, ng0, f, ngrid * nao, ngrid, nao, nip_ub, kmesh, ys_qs.data(),
+                          (int)ys_qs.size(), yT_pre, rmask, &armed));
+  }
   // interpolation points (:33 -> :357-388), or the caller's
   std::vector<int> perm;
   for (int attempt = 0;; ++attempt) {
@@ -3099,6 +3317,7 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
       int npiv = 0, full = 0;
       FISDF_TRY(fisdf_select_points_km(c, x0, kmesh, ng0, nao, cap, o.select_tol, perm.data(),
                                        &npiv, &full));
+      c->ys.armed = false;  // a second selection (time reversal refuted) streams nothing
       perm.resize(std::min(cap, npiv));                                           // :383
     }
     if (!check_tr || attempt > 0) break;
@@ -3138,23 +3357,38 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
   std::vector<int> ranks(nmine, 0);
   int used = 0, ncod = 0;
   long row0 = 0, row1 = nip;
+  // the streamed y is this build's y when the selection gave the cap's points under time
+  // reversal (the q-list it was formed for) and the y stream met no stalled wait
+  const bool y_streamed = tr && ystream_valid(c, nip, qs.data(), nq);
+  // a discarded streamed y: its stream joins before its buffer goes back (the usual build may be
+  // handed the same memory)
+  if (c->ys.enqueued && !y_streamed) FISDF_TRY(ystream_join(c));
+  if (yT_pre && !y_streamed) {
+    FISDF_TRY(build_return(c, yT_pre));
+    yT_pre = nullptr;
+  }
   if (!comm) {
     // the factorisation (replaces zgelsy's QRCP, :108) on the side stream, overlapped with y
     FISDF_TRY(fisdf_factor_x4_mark(c));
-    void* yT;
-    FISDF_TRY(build_alloc(c, BR_Y, sizeof(cplx) * (size_t)nq * nip * ngrid, &yT));
+    void* yT = yT_pre;
+    if (!yT) FISDF_TRY(build_alloc(c, BR_Y, sizeof(cplx) * (size_t)nq * nip * ngrid, &yT));
     // the self-conjugate q's y real (half their y writes and FFT reads); FISDF_Y_REAL=0: off
-    static const bool y_real_env = [] {
-      const char* e = getenv("FISDF_Y_REAL");
-      return !(e && e[0] == '0');
-    }();
     struct YRealScope {  // the mode is this build's only: reset on every exit
       fisdf_ctx* c;
       ~YRealScope() { c->y_real_store = false; c->y_real_slot.clear(); }
     } y_real_scope{c};
     c->y_real_store = y_real_env && o.real_self_conjugate && fft3d_reads_real(mesh[0], mesh[1], mesh[2]);
-    FISDF_TRY(fisdf_build_y_qs(c, f, ngrid * nao, 0, (int)ngrid, (int)ngrid, X, nip, nao, kmesh,
-                               a, qs.data(), nq, yT));                             // :67-87
+    if (y_streamed) {
+      // the fit comes after the y stream; joined only now, after x4 has been marked for the
+      // factor chain, so the side stream does not wait for y
+      FISDF_TRY(ystream_join(c));
+      // what fisdf_build_y_qs records for the fit: the slots stored real
+      c->y_real_slot.assign(nq, 0);
+      for (int i = 0; i < nq; ++i) c->y_real_slot[i] = (c->ys.rmask >> qs[i]) & 1ull ? 1 : 0;
+    } else {
+      FISDF_TRY(fisdf_build_y_qs(c, f, ngrid * nao, 0, (int)ngrid, (int)ngrid, X, nip, nao, kmesh,
+                                 a, qs.data(), nq, yT));                           // :67-87
+    }
     FISDF_TRY(fisdf_factor_x4_async(c, x4, qs.data(), nq, nip, o.fit_tol,
                                     o.real_self_conjugate ? kmesh : nullptr));
     FISDF_TRY(build_alloc(c, BR_WQ, sizeof(cplx) * (size_t)nq * nn, &Wq));
@@ -3163,6 +3397,8 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
     FISDF_TRY(fisdf_factor_x4_wait(c, ranks.data()));
     FISDF_TRY(fisdf_factor_info(c, &used));
     FISDF_TRY(fisdf_min_norm_info(c, &ncod));
+    // a block that waited past its bound built y from unfinished pivots
+    if (y_streamed) FISDF_TRY(ystream_check(c));
     // y is dead once the fit is enqueued: fit_coulomb_qs joined its lanes and FFT stream into
     // c->stream (aux_join, checked by build_return), so a stream-ordered free cannot overtake a
     // reader
@@ -3289,6 +3525,7 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
   B.Ws = Ws;
   B.W0 = W0;
   B.sharded = comm != nullptr;
+  B.y_streamed = y_streamed;
   if (comm) B.comm = *comm;
   B.shard_rank = RK;
   B.shard_size = NR;
@@ -3314,6 +3551,40 @@ int fisdf_build_sharded(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, in
   FISDF_TRY(device_guard(c));
   FISDF_CHECK(comm != nullptr, "build_sharded: comm is null (fisdf_build is the 1-GPU build)");
   return build_impl(c, comm, x0, ng0, f, nao, kmesh, mesh, a, opts, h_nip);
+}
+
+int fisdf_y_stream_arm(fisdf_ctx* c, const void* x0, int ng0, const void* f, long f_kstride,
+                       int m, int nao, int nip_max, const int kmesh[3], const int* h_qs, int nq,
+                       void* yT, int* h_armed) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(kmesh && h_armed && ng0 > 0 && nao > 0, "y_stream_arm: bad arguments");
+  FISDF_TRY(check_qlist(h_qs, nq, kmesh[0] * kmesh[1] * kmesh[2], "y_stream_arm"));
+  FISDF_CHECK(c->ys.enqueued == false, "y_stream_arm: the previous streamed y is not finished");
+  bool armed = false;
+  if (c->time_reversal)  // the fused kernel folds fx over k <= -k
+    FISDF_TRY(ystream_arm(c, x0, ng0, f, f_kstride, m, nao, nip_max, kmesh, h_qs, nq, yT, 0,
+                          &armed));
+  *h_armed = armed ? 1 : 0;
+  return 0;
+}
+
+int fisdf_y_stream_finish(fisdf_ctx* c, int nip, int* h_streamed) {
+  FISDF_TRY(device_guard(c));
+  FISDF_CHECK(h_streamed, "y_stream_finish: null output");
+  const bool ok = c->ys.enqueued && ystream_valid(c, nip, c->ys.qs.data(), (int)c->ys.qs.size());
+  const bool had = c->ys.enqueued;
+  FISDF_TRY(ystream_join(c));
+  if (had) FISDF_TRY(ystream_check(c));
+  *h_streamed = ok ? 1 : 0;
+  c->ys = fisdf_ctx::YStream();
+  return 0;
+}
+
+int fisdf_build_y_streamed(fisdf_ctx* c, int* h_streamed) {
+  FISDF_TRY(ctx_guard(c));
+  FISDF_CHECK(h_streamed, "build_y_streamed: null output");
+  *h_streamed = c->bld.valid && c->bld.y_streamed ? 1 : 0;
+  return 0;
 }
 
 int fisdf_build_get(fisdf_ctx* c, fisdf_build_result* out) {

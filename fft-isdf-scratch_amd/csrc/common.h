@@ -144,9 +144,17 @@ int chol_unpivoted(hipStream_t s, cplx* W, int n, int batch, double tol_rel, int
 // flags (1) device.  When the cooperative kernel ran (allow_coop), *coop_err is the device address
 // of its error flag: nonzero after the stream completes = a stalled step, redo with
 // allow_coop = false.
+// progress (device int, nullable): the cooperative kernel publishes the count of final pivots
+// every kSelPublish pivots and kSelDone at its end, with piv[] written agent-coherent, so work
+// on other streams can start on the first pivots while the selection runs (the streamed y
+// build, api.hip); *publishes tells whether the kernel that ran does so (the other paths
+// publish nothing: their consumers see only the kSelDone the caller writes after the kernel)
+constexpr int kSelPublish = 16;
+constexpr int kSelDone = 1 << 30;
 int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rmax, double tol,
                       int* piv, int* rank, double* work, int* flags, bool* handled,
-                      bool allow_coop, const int** coop_err);
+                      bool allow_coop, const int** coop_err, int* progress = nullptr,
+                      bool* publishes = nullptr);
 
 // Where plane i0 of input row r lives when the rows arrive in grid slices (the all-to-all
 // pieces of a k-sharded build): in + base + r * ld, one entry per plane (device table)

@@ -99,6 +99,18 @@ int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long 
             const int kmesh[3], const int* h_qs, int nq, cplx* yT, long qs, long Is, long goff,
             unsigned long long* mon, cplx* work, size_t work_bytes, unsigned long long rmask,
             bool* handled);
+// whether the fused kernel covers this k-mesh (time reversal assumed)
+bool y_fused_applies(const int kmesh[3], int nao);
+// The same y build streamed behind a running selection (api.hip build_impl): rows [0, nip) of
+// y in blocks of `rows` (a multiple of 16); block [lo, hi) forms its XT rows straight from x0
+// through piv[lo..hi) once the selection's progress word (device) reaches hi, then runs the
+// fused kernel on its I-tiles.  X is never read; work holds XT (nip rows) and FT as for
+// y_fused.  *err (device) is set if a block waited past the bound.  *handled as for y_fused.
+int y_fused_stream(hipStream_t s, const cplx* x0, int ng0, int nao, const int* piv,
+                   const int* progress, int* err, int nip, int rows, const cplx* F, long fks,
+                   int m, const int kmesh[3], const int* h_qs, int nq, cplx* yT, long qs, long Is,
+                   long goff, cplx* work, size_t work_bytes, unsigned long long rmask,
+                   bool* handled);
 int kmesh_rep_runs(const int kmesh[3], std::vector<int>* runs);
 // Bloch AO values (ao.hip): F (nimg, ng, nao) f64 workspace, scratch for the small tables;
 // nkb > 0: at the nkb band k-points h_kband (any k) instead of the k-mesh, F (nT, ng, nao)

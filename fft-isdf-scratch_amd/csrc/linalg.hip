@@ -645,11 +645,62 @@ __global__ __launch_bounds__(256) void yf_transpose_kernel(const cplx* __restric
   }
 }
 
+// XT[j][mu][I] = x0[k_j][piv[I]][mu] for the rows [lo, hi) of a streamed y build
+// (y_fused_stream): the pivots come from a selection still running on another stream, so one
+// thread per workgroup first waits until the selection has published at least `hi` of them
+// (pchol_select_coop's progress word, agent-coherent; kSelDone once it has ended, also written
+// by the caller after the kernel whatever path ran).  The wait is bounded: past ~10 s it sets
+// *err (the build then fails loudly) and goes on with whatever pivots are there; a pivot is
+// clamped into [0, ng0) before it addresses x0.
+constexpr long kXtSpinCap = 3000000;  // s_sleep(127) rounds: ~10 s
+__global__ __launch_bounds__(256) void yf_xt_stream_kernel(const cplx* __restrict__ x0,
+                                                           long kstride, int ng0, int nao,
+                                                           const int* __restrict__ piv,
+                                                           const int* __restrict__ progress,
+                                                           int lo, int hi, int nip, YfPlan plan,
+                                                           cplx* __restrict__ XT,
+                                                           int* __restrict__ err) {
+  extern __shared__ cplx tile[];  // [64][nao + 1]
+  __shared__ int s_p[64];
+  if (threadIdx.x == 0) {
+    long spins = 0;
+    while (__hip_atomic_load(progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hi) {
+      __builtin_amdgcn_s_sleep(127);
+      if (++spins > kXtSpinCap) {
+        atomicExch(err, 1);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  const int j = blockIdx.y;
+  const int k = j < plan.nA ? plan.kA[j] : plan.kB[j - plan.nA];
+  const int r0 = lo + blockIdx.x * 64, nr = min(64, hi - r0), ld = nao + 1;
+  if (threadIdx.x < 64) {
+    int p = 0;
+    if ((int)threadIdx.x < nr)
+      p = __hip_atomic_load(&piv[r0 + threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_p[threadIdx.x] = min(max(p, 0), ng0 - 1);
+  }
+  __syncthreads();
+  const cplx* sp = x0 + (long)k * kstride;
+  for (int e = threadIdx.x; e < nr * nao; e += 256) {
+    const int r = e / nao, mu = e - r * nao;
+    tile[r * ld + mu] = sp[(long)s_p[r] * nao + mu];
+  }
+  __syncthreads();
+  cplx* dp = XT + (long)j * nao * nip + r0;
+  for (int e = threadIdx.x; e < nao * 64; e += 256) {
+    const int mu = e >> 6, r = e & 63;
+    if (r < nr) dp[(long)mu * nip + r] = tile[r * ld + mu];
+  }
+}
+
 template <int N0, int N1, int N2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void y_fused_kernel(
     const cplx* __restrict__ XT, int nip, int nao, const cplx* __restrict__ FT, int m,
     int nIt, int nGt, YfPlan plan, unsigned long long qmask, unsigned long long rmask,
-    cplx* __restrict__ yT, long qs, long Is, long goff, int mode, int gpair) {
+    cplx* __restrict__ yT, long qs, long Is, long goff, int mode, int gpair, int it0) {
   constexpr int P = N1 * N2, NK = N0 * P;
   constexpr int R = yf_inplane_rank<N1, N2>(P);         // in-plane representatives
   constexpr int NC = (N0 - 1) / 2;                        // complex planes 1..NC (N0 <= 4: 0 or 1)
@@ -663,7 +714,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int grp = j / (nIt * gpair), rem = j - grp * nIt * gpair;
   const int it = rem / gpair, gt = (grp * gpair + rem % gpair) * 8 + xcd;
   if (gt >= nGt) return;
-  const int I0 = it * 16, g0 = gt * 16;
+  const int I0 = (it0 + it) * 16, g0 = gt * 16;  // it0: the launch's first I-tile (streamed y)
   const int Ia = I0 + (lane & 15), ga = g0 + (lane & 15);
   const bool okI = Ia < nip, okg = ga < m;
   cplx tw0[N0], tw1[N1], tw2[N2];
@@ -1496,35 +1547,78 @@ size_t y_fused_workspace(const int kmesh[3], int nip, int nao, int m) {
   return sizeof(cplx) * (size_t)nslot * nao * ((size_t)nip + m);
 }
 
+// the fused kernel's slot plan and q mask for this k-mesh / q-list; false: the fused kernel
+// does not apply (the caller's two-kernel path runs)
+static int yf_setup(const int kmesh[3], int nao, const int* h_qs, int nq, YfPlan* plan,
+                    unsigned long long* qmask, size_t* lds, bool* ok) {
+  *ok = false;
+  const int n0 = kmesh[0], n1 = kmesh[1], n2 = kmesh[2];
+  const int nk = n0 * n1 * n2, P = n1 * n2;
+  if (nk > 64 || n0 > 4 || P > 16 || nao > 128) return 0;
+  for (int i = 0; i < nq; ++i)
+    FISDF_CHECK(h_qs[i] >= 0 && h_qs[i] < nk && (i == 0 || h_qs[i] > h_qs[i - 1]),
+                "y_fused: q-list must be ascending and inside the k-mesh");
+  *qmask = 0;
+  for (int i = 0; i < nq; ++i) *qmask |= 1ull << h_qs[i];
+  // slot order of the kernel: chunk A = plane 1 (if 1 < N0 - 1), all P; chunk B = planes
+  // 0 (and N0/2 if even) at their in-plane representatives bc <= -bc, ascending
+  *plan = YfPlan{};
+  if (n0 >= 3)
+    for (int bc = 0; bc < P; ++bc) plan->kA[plan->nA++] = P + bc;
+  const int nr = (n0 % 2 == 0 && n0 > 1) ? 2 : 1;
+  for (int pi = 0; pi < nr; ++pi) {
+    const int a = pi == 0 ? 0 : n0 / 2;
+    for (int bc = 0; bc < P; ++bc) {
+      const int b = bc / n2, c = bc % n2;
+      if (bc <= ((n1 - b) % n1) * n2 + (n2 - c) % n2) plan->kB[plan->nB++] = a * P + bc;
+    }
+  }
+  *lds = sizeof(cplx) * 256 * (size_t)std::max(plan->nA, plan->nB);
+  *ok = *lds <= 80 * 1024;
+  return 0;
+}
+
+// y_fused_kernel over the I-tiles [it0, it0 + nIt) of a (nip, m) column grid
+static int yf_launch(hipStream_t s, const int kmesh[3], const cplx* XT, int nip, int nao,
+                     const cplx* FT, int m, int it0, int nIt, const YfPlan& plan,
+                     unsigned long long qmask, unsigned long long rmask, cplx* yT, long qs,
+                     long Is, long goff, size_t lds, bool* handled) {
+  const int n0 = kmesh[0], n1 = kmesh[1], n2 = kmesh[2];
+  const int nGt = (m + 15) / 16;
+  constexpr int gpair = 4;  // g-tiles per group of the XCD walk (2 / 8 measured no better)
+  const long grid = (long)nIt * ((nGt + 8 * gpair - 1) / (8 * gpair)) * gpair * 8;
+  FISDF_CHECK(grid < (1L << 31), "y_fused: grid too large");
+  FISDF_CHECK(it0 >= 0 && nIt >= 1 && (it0 + nIt - 1) * 16 < nip, "y_fused: I-tiles out of range");
+  static const int mode = getenv("FISDF_YF_MODE") ? atoi(getenv("FISDF_YF_MODE")) : 0;
+#define FISDF_YF(a, b, c)                                                                      \
+  if (n0 == a && n1 == b && n2 == c) {                                                         \
+    FISDF_TRY(func_max_lds((const void*)y_fused_kernel<a, b, c>, 80 * 1024));                \
+    hipLaunchKernelGGL((y_fused_kernel<a, b, c>), dim3((unsigned)grid), dim3(256), lds, s, XT,  \
+                       nip, nao, FT, m, nIt, nGt, plan, qmask, rmask & qmask, yT, qs, Is, goff, \
+                       mode, gpair, it0);                                                     \
+    FISDF_HIP(hipGetLastError());                                                              \
+    *handled = true;                                                                           \
+    return 0;                                                                                  \
+  }
+  FISDF_YF(1, 1, 1) FISDF_YF(1, 1, 2) FISDF_YF(2, 2, 2) FISDF_YF(3, 3, 1) FISDF_YF(3, 3, 3)
+  FISDF_YF(4, 4, 4) FISDF_YF(2, 2, 1) FISDF_YF(1, 2, 2) FISDF_YF(4, 4, 1) FISDF_YF(2, 2, 4)
+#undef FISDF_YF
+  return 0;
+}
+
 int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long fks, int m,
             const int kmesh[3], const int* h_qs, int nq, cplx* yT, long qs, long Is, long goff,
             unsigned long long* mon, cplx* work, size_t work_bytes, unsigned long long rmask,
             bool* handled) {
   (void)mon;  // fx_s is real by construction here (t_{-a} = conj(t_a)); nothing to monitor
   *handled = false;
-  const int n0 = kmesh[0], n1 = kmesh[1], n2 = kmesh[2];
-  const int nk = n0 * n1 * n2, P = n1 * n2;
-  if (nk > 64 || n0 > 4 || P > 16 || m <= 0 || nip <= 0) return 0;
-  for (int i = 0; i < nq; ++i)
-    FISDF_CHECK(h_qs[i] >= 0 && h_qs[i] < nk && (i == 0 || h_qs[i] > h_qs[i - 1]),
-                "y_fused: q-list must be ascending and inside the k-mesh");
+  if (m <= 0 || nip <= 0) return 0;
+  YfPlan plan;
   unsigned long long qmask = 0;
-  for (int i = 0; i < nq; ++i) qmask |= 1ull << h_qs[i];
-  // slot order of the kernel: chunk A = plane 1 (if 1 < N0 - 1), all P; chunk B = planes
-  // 0 (and N0/2 if even) at their in-plane representatives bc <= -bc, ascending
-  YfPlan plan{};
-  if (n0 >= 3)
-    for (int bc = 0; bc < P; ++bc) plan.kA[plan.nA++] = P + bc;
-  const int nr = (n0 % 2 == 0 && n0 > 1) ? 2 : 1;
-  for (int pi = 0; pi < nr; ++pi) {
-    const int a = pi == 0 ? 0 : n0 / 2;
-    for (int bc = 0; bc < P; ++bc) {
-      const int b = bc / n2, c = bc % n2;
-      if (bc <= ((n1 - b) % n1) * n2 + (n2 - c) % n2) plan.kB[plan.nB++] = a * P + bc;
-    }
-  }
-  const size_t lds = sizeof(cplx) * 256 * (size_t)std::max(plan.nA, plan.nB);
-  if (lds > 80 * 1024 || nao > 128) return 0;
+  size_t lds = 0;
+  bool ok = false;
+  FISDF_TRY(yf_setup(kmesh, nao, h_qs, nq, &plan, &qmask, &lds, &ok));
+  if (!ok) return 0;
   // mu-major copies of the plan's k: XT [slot][mu][I], FT [slot][mu][g]
   const int nsl = plan.nA + plan.nB;
   FISDF_CHECK(work && work_bytes >= sizeof(cplx) * (size_t)nsl * nao * ((size_t)nip + m),
@@ -1540,24 +1634,62 @@ int y_fused(hipStream_t s, const cplx* X, int nip, int nao, const cplx* F, long 
   hipLaunchKernelGGL(yf_transpose_kernel, dim3((m + 63) / 64, nsl), dim3(256), tl, s, F, fks, m,
                      nao, plan, FT);
   FISDF_HIP(hipGetLastError());
-  const int nIt = (nip + 15) / 16, nGt = (m + 15) / 16;
-  constexpr int gpair = 4;  // g-tiles per group of the XCD walk (2 / 8 measured no better)
-  const long grid = (long)nIt * ((nGt + 8 * gpair - 1) / (8 * gpair)) * gpair * 8;
-  FISDF_CHECK(grid < (1L << 31), "y_fused: grid too large");
-  static const int mode = getenv("FISDF_YF_MODE") ? atoi(getenv("FISDF_YF_MODE")) : 0;
-#define FISDF_YF(a, b, c)                                                                      \
-  if (n0 == a && n1 == b && n2 == c) {                                                         \
-    FISDF_TRY(func_max_lds((const void*)y_fused_kernel<a, b, c>, 80 * 1024));                \
-    hipLaunchKernelGGL((y_fused_kernel<a, b, c>), dim3((unsigned)grid), dim3(256), lds, s, XT,  \
-                       nip, nao, FT, m, nIt, nGt, plan, qmask, rmask & qmask, yT, qs, Is, goff, \
-                       mode, gpair);                                                          \
-    FISDF_HIP(hipGetLastError());                                                              \
-    *handled = true;                                                                           \
-    return 0;                                                                                  \
+  return yf_launch(s, kmesh, XT, nip, nao, FT, m, 0, (nip + 15) / 16, plan, qmask, rmask, yT, qs,
+                   Is, goff, lds, handled);
+}
+
+bool y_fused_applies(const int kmesh[3], int nao) {
+  static const int inst[][3] = {{1, 1, 1}, {1, 1, 2}, {2, 2, 2}, {3, 3, 1}, {3, 3, 3},
+                                {4, 4, 4}, {2, 2, 1}, {1, 2, 2}, {4, 4, 1}, {2, 2, 4}};
+  bool have = false;  // the instantiations yf_launch dispatches to
+  for (const auto& k : inst) have |= k[0] == kmesh[0] && k[1] == kmesh[1] && k[2] == kmesh[2];
+  if (!have) return false;
+  YfPlan plan;
+  unsigned long long qmask = 0;
+  size_t lds = 0;
+  bool ok = false;
+  const int q0 = 0;
+  if (yf_setup(kmesh, nao, &q0, 1, &plan, &qmask, &lds, &ok) != 0) return false;
+  return ok;
+}
+
+int y_fused_stream(hipStream_t s, const cplx* x0, int ng0, int nao, const int* piv,
+                   const int* progress, int* err, int nip, int rows, const cplx* F, long fks,
+                   int m, const int kmesh[3], const int* h_qs, int nq, cplx* yT, long qs, long Is,
+                   long goff, cplx* work, size_t work_bytes, unsigned long long rmask,
+                   bool* handled) {
+  *handled = false;
+  if (m <= 0 || nip <= 0) return 0;
+  FISDF_CHECK(rows >= 16 && rows % 16 == 0 && rows <= 64 * 16, "y_fused_stream: bad row block");
+  YfPlan plan;
+  unsigned long long qmask = 0;
+  size_t lds = 0;
+  bool ok = false;
+  FISDF_TRY(yf_setup(kmesh, nao, h_qs, nq, &plan, &qmask, &lds, &ok));
+  if (!ok) return 0;
+  const int nsl = plan.nA + plan.nB;
+  FISDF_CHECK(work && work_bytes >= sizeof(cplx) * (size_t)nsl * nao * ((size_t)nip + m),
+              "y_fused_stream: workspace too small");
+  cplx* XT = work;
+  cplx* FT = work + (size_t)nsl * nao * nip;
+  const size_t tl = sizeof(cplx) * 64 * (size_t)(nao + 1);
+  FISDF_TRY(func_max_lds((const void*)yf_transpose_kernel, 132 * 1024));
+  FISDF_TRY(func_max_lds((const void*)yf_xt_stream_kernel, 132 * 1024));
+  // f's copy needs no pivot: it runs while the selection finds the first block
+  hipLaunchKernelGGL(yf_transpose_kernel, dim3((m + 63) / 64, nsl), dim3(256), tl, s, F, fks, m,
+                     nao, plan, FT);
+  FISDF_HIP(hipGetLastError());
+  for (int lo = 0; lo < nip; lo += rows) {
+    const int hi = std::min(nip, lo + rows);
+    hipLaunchKernelGGL(yf_xt_stream_kernel, dim3((hi - lo + 63) / 64, nsl), dim3(256), tl, s, x0,
+                       (long)ng0 * nao, ng0, nao, piv, progress, lo, hi, nip, plan, XT, err);
+    FISDF_HIP(hipGetLastError());
+    bool h = false;
+    FISDF_TRY(yf_launch(s, kmesh, XT, nip, nao, FT, m, lo / 16, (hi - lo + 15) / 16, plan, qmask,
+                        rmask, yT, qs, Is, goff, lds, &h));
+    FISDF_CHECK(h, "y_fused_stream: no kernel for this k-mesh");
   }
-  FISDF_YF(1, 1, 1) FISDF_YF(1, 1, 2) FISDF_YF(2, 2, 2) FISDF_YF(3, 3, 1) FISDF_YF(3, 3, 3)
-  FISDF_YF(4, 4, 4) FISDF_YF(2, 2, 1) FISDF_YF(1, 2, 2) FISDF_YF(4, 4, 1) FISDF_YF(2, 2, 4)
-#undef FISDF_YF
+  *handled = true;
   return 0;
 }
 

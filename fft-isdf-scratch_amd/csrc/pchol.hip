@@ -514,7 +514,8 @@ __device__ __forceinline__ bool sc_better(double v2, int i2, double v, int i) {
 __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
     const cplx* __restrict__ X2, double scale, int n, int rmax, double tol, int RW, int K, int tpr,
     int* __restrict__ piv, int* __restrict__ rank, u32x4* __restrict__ rec,
-    double* __restrict__ Lg, int* __restrict__ err, unsigned long long* __restrict__ prof) {
+    double* __restrict__ Lg, int* __restrict__ err, unsigned long long* __restrict__ prof,
+    int* __restrict__ progress) {
   extern __shared__ double sm[];
   double* Lr = sm;                    // RW x K, row-major (columns >= K only in the global L)
   double* Lp = Lr + (long)RW * K;     // pivot row L[p, :j]
@@ -607,7 +608,20 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
         s_p = i;
         s_dp = v;
         if (w == 0) {
-          if (!stop) piv[j] = i;
+          if (progress) {
+            // streamed consumers (the y build behind the selection, api.hip) read piv[] while
+            // the kernel runs: the pivot goes out agent-coherent, and every kSelPublish pivots
+            // (and at the end) the count follows once the pivot stores have completed
+            if (!stop) __hip_atomic_store(&piv[j], i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool last = stop || j + 1 >= rmax;
+            if (last || ((j + 1) % kSelPublish) == 0) {
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+              __hip_atomic_store(progress, last ? kSelDone : j + 1, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+            }
+          } else if (!stop) {
+            piv[j] = i;
+          }
           if (stop || j + 1 >= rmax) rank[0] = stop ? j : j + 1;
         }
       }
@@ -1456,8 +1470,15 @@ hipError_t launch_coresident(const void* fn, int grid, int threads, void** args,
   }();
   if (coop) {
     // one cooperative launch at a time in the process: concurrent ones from several host threads
-    // (fisdf_group's ranks) left the runtime crashing in its exit handlers
+    // (fisdf_group's ranks) left the runtime crashing in its exit handlers.  FISDF_COOP_MUTEX=0
+    // (diagnosis only, tools/crash_probe.sh) drops the lock to reproduce that crash.
+    static const bool serial = [] {
+      const char* e = getenv("FISDF_COOP_MUTEX");
+      return !(e && e[0] == '0');
+    }();
     static std::mutex mu;
+    if (!serial)
+      return hipLaunchCooperativeKernel(fn, dim3(grid), dim3(threads), args, (unsigned)lds, s);
     std::lock_guard<std::mutex> lk(mu);
     return hipLaunchCooperativeKernel(fn, dim3(grid), dim3(threads), args, (unsigned)lds, s);
   }
@@ -1474,7 +1495,7 @@ hipError_t launch_coresident(const void* fn, int grid, int threads, void** args,
 // stalled step), which the caller reads back with the pivots and the rank in one copy.
 int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n, int rmax,
                              double tol, int* piv, int* rank, double* work, bool* handled,
-                             const int** err_dev) {
+                             const int** err_dev, int* progress) {
   *handled = false;
   *err_dev = nullptr;
   if (!select_coop_enabled() || n < 64) return 0;
@@ -1537,7 +1558,7 @@ int pchol_select_coop_launch(hipStream_t s, const cplx* X2, double scale, int n,
   if (profp) FISDF_HIP(hipMemsetAsync(profp, 0, sizeof(unsigned long long) * 4 * rmax, s));
   void* args[] = {(void*)&X2, (void*)&scale, (void*)&n,   (void*)&rmax, (void*)&tol, (void*)&RW,
                   (void*)&K,   (void*)&tpr,   (void*)&piv, (void*)&rank, (void*)&rec, (void*)&Lg,
-                  (void*)&err, (void*)&profp};
+                  (void*)&err, (void*)&profp, (void*)&progress};
   const hipError_t e =
       launch_coresident((const void*)pchol_select_coop, G, SC_THREADS, args, lds, s, ncu);
   if (e != hipSuccess) {  // refused (e.g. not co-resident): the caller's blocked path runs
@@ -1672,9 +1693,10 @@ int pchol_select_batch_launch(hipStream_t s, const cplx* X2, double scale, int n
 
 int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rmax, double tol,
                       int* piv, int* rank, double* work, int* flags, bool* handled,
-                      bool allow_coop, const int** coop_err) {
+                      bool allow_coop, const int** coop_err, int* progress, bool* publishes) {
   *handled = false;
   *coop_err = nullptr;
+  if (publishes) *publishes = false;
   if (rmax <= 0) return 0;
   const int mode = select_mode(rmax);
   if (allow_coop && mode == 0) {
@@ -1684,8 +1706,11 @@ int pchol_select_real(hipStream_t s, const cplx* X2, double scale, int n, int rm
   }
   if (allow_coop && mode <= 1) {
     FISDF_TRY(pchol_select_coop_launch(s, X2, scale, n, rmax, tol, piv, rank, work, handled,
-                                       coop_err));
-    if (*handled) return 0;
+                                       coop_err, progress));
+    if (*handled) {
+      if (publishes) *publishes = progress != nullptr;
+      return 0;
+    }
   }
   if (n > 8 * PR_THREADS) return 0;
   double* W = work;

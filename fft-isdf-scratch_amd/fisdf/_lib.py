@@ -101,6 +101,9 @@ _SIGS = {
     # composite entries
     "fisdf_build_opts_default": ([_vp], None),
     "fisdf_build": ([_vp, _vp, _i, _vp, _i, _ip, _ip, _dp, _vp, _ip], _i),
+    "fisdf_build_y_streamed": ([_vp, _ip], _i),
+    "fisdf_y_stream_arm": ([_vp, _vp, _i, _vp, _l, _i, _i, _i, _ip, _ip, _i, _vp, _ip], _i),
+    "fisdf_y_stream_finish": ([_vp, _i, _ip], _i),
     "fisdf_build_get": ([_vp, _vp], _i),
     "fisdf_build_release": ([_vp], _i),
     "fisdf_get_x": ([_vp, _vp], _i),

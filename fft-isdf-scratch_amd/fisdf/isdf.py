@@ -134,6 +134,7 @@ class InterpolativeSeparableDensityFitting:
     fit_tol = 4.2e-15       # relative pivot cut of the x4_q factorisation: where
                             # its ranks reproduce gelsy's at rcond = eps (fftisdf.py:108)
     select_tol = -1.0       # dpstrf default tolerance (ng0*eps*max diag)
+    y_streamed = False      # the last 1-GPU build formed y behind the selection
     # cap on the number of interpolation points; None -> int(nao * c0) (fftisdf.py:383);
     # the get_coul drivers set it directly (fftdf-with-k-lstsq.py:71, fftdf-with-k.py:64)
     nip_max = None
@@ -605,6 +606,9 @@ def _build_one_gpu(df_obj):
     df_obj.time_reversal_used = bool(r.time_reversal)
     df_obj.tr_deviation = float(r.tr_deviation)
     df_obj.nip = nip
+    ys = C_int()
+    d.ctx.call("fisdf_build_y_streamed", byref(ys))
+    df_obj.y_streamed = bool(ys.value)     # y formed behind the selection (fisdf_build_y_streamed)
     return df_obj
 
 
@@ -672,7 +676,30 @@ def build(df_obj):
     tr = bool(df_obj.time_reversal) and _time_reversal_holds(df_obj, df_obj._ao_parent,
                                                               df_obj._ao_grid, kmesh)
     df_obj.time_reversal_used = tr
+    # y streamed behind the selection (fisdf_y_stream_arm): this rank's grid slice
+    # of y for every fitted q is formed on a second stream as the replicated selection publishes
+    # its pivots, at the point cap; kept when the selection reaches the cap
+    ys_send = None
+    sharded = d.sharded(df_obj)
     if df_obj._dev_state is None or "X" not in df_obj._dev_state:
+        if sharded and tr and os.environ.get("FISDF_Y_STREAM", "1") != "0":
+            ng0 = df_obj._ao_parent.shape[1]
+            cap = int(nao * df_obj.c0) if df_obj.nip_max is None else int(df_obj.nip_max)
+            nip_cap = max(1, min(cap, ng0))
+            qs0 = np.ascontiguousarray(_fit_qset(df_obj, kmesh, tr)[0], dtype=np.int32)
+            g0, ng = kshard.grid_slices(df_obj.mesh, d.size)[d.rank]
+            if ng:
+                send_pre = d.empty((len(qs0), nip_cap, ng))
+                f = df_obj._ao_grid
+                fptr = _lib._vp(f.data_ptr() + g0 * nao * f.element_size())
+                d.ctx.call("fisdf_set_time_reversal", 1)
+                armed = C_int()
+                d.ctx.call("fisdf_y_stream_arm", _lib.ptr(df_obj._ao_parent), ng0, fptr,
+                           ngrid * nao, ng, nao, nip_cap, km_p, qs0.ctypes.data_as(_lib._ip),
+                           len(qs0), _lib.ptr(send_pre), byref(armed))
+                if armed.value:
+                    ys_send = send_pre
+                del send_pre
         df_obj._select(time_reversal=tr)                                 # fftisdf.py:33
     X = df_obj._dev_state["X"]
     nip = X.shape[1]
@@ -705,11 +732,19 @@ def build(df_obj):
     d.ctx.call("fisdf_set_half_grid", -1 if df_obj.half_grid is None else int(bool(df_obj.half_grid)))
     # the side stream starts from here (x4 built); the factor chain itself is enqueued after
     # the y build, since it reads ranks back to the host part-way (a blocking copy)
-    sharded = d.sharded(df_obj)
     # a k-shard's 1/N-grid y build is short, so its factor chain runs at the greatest priority
     d.ctx.call("fisdf_set_factor_priority", 1 if sharded else 0)
     if nq:
         d.ctx.call("fisdf_factor_x4_mark")
+    y_streamed = False
+    if ys_send is not None:
+        # after the mark: the factor chain does not wait for the y stream, the exchange does
+        got = C_int()
+        d.ctx.call("fisdf_y_stream_finish", nip, byref(got))
+        y_streamed = bool(got.value)
+        if not y_streamed:
+            ys_send = None
+    df_obj.y_streamed = y_streamed
 
     def factor_async():
         if nq:
@@ -728,8 +763,12 @@ def build(df_obj):
         slices = kshard.grid_slices(df_obj.mesh, d.size)
         g0, ng = slices[d.rank]
         all_qs = np.ascontiguousarray(fit_qs, dtype=np.int32)
-        send = d.empty((len(all_qs), nip, ng))
-        if ng:
+        if y_streamed:
+            send = ys_send                      # formed behind the selection
+        else:
+            send = d.empty((len(all_qs), nip, ng))
+        ys_send = None
+        if ng and not y_streamed:
             fptr = _lib._vp(f.data_ptr() + g0 * nao * f.element_size())
             d.ctx.call("fisdf_build_y_qs", fptr, ngrid * nao, 0, ng, ng, _lib.ptr(X), nip, nao,
                        km_p, a_p, all_qs.ctypes.data_as(_lib._ip), len(all_qs), _lib.ptr(send))

@@ -98,6 +98,28 @@ void fisdf_build_opts_default(fisdf_build_opts* opts);
 int fisdf_build(fisdf_ctx* ctx, const void* d_x0, int ng0, const void* d_f, int nao,
                 const int kmesh[3], const int mesh[3], const double a[9],
                 const fisdf_build_opts* opts, int* h_nip);
+/* 1 in *h_streamed if the last fisdf_build formed y (:67-87) behind the selection: its fused y
+ * kernel started on the first pivots the cooperative selection kernel published, on a second
+ * stream, instead of after the selection (the selection's own points, time reversal, a k-mesh the
+ * fused kernel covers; environment FISDF_Y_STREAM=0, read per build, turns it off).  The y,
+ * hence every result, is the same either way. */
+int fisdf_build_y_streamed(fisdf_ctx* ctx, int* h_streamed);
+/* The same streamed y for a caller that drives the stages itself (the k-sharded mirror, one
+ * process per GPU).  arm, before fisdf_select_points(_km) / fisdf_select_pivots: the arguments of
+ * fisdf_build_y_qs (d_f at the first grid point of the m-point block, k stride f_kstride; y_q of
+ * the ascending q-list h_qs into d_yT[slot][I][g], slot stride nip_max * m) with the point cap
+ * nip_max in place of nip and d_x0 (nk, ng0, nao) in place of X; time reversal must be on
+ * (fisdf_set_time_reversal) and the k-mesh one the fused y kernel covers, else *h_armed = 0 and
+ * nothing streams.  The next selection then forms y on a second stream as its pivots appear.
+ * finish, after the selection, with the nip it returned: *h_streamed = 1 if d_yT holds
+ * fisdf_build_y_qs's result for those points (the caller skips it), 0 if not (the caller builds
+ * y as usual, e.g. the selection stopped below the cap); either way the context stream is
+ * ordered after the y stream.  Not synchronous for the device; finish waits for the y stream's
+ * host-visible completion flag. */
+int fisdf_y_stream_arm(fisdf_ctx* ctx, const void* d_x0, int ng0, const void* d_f, long f_kstride,
+                       int m, int nao, int nip_max, const int kmesh[3], const int* h_qs, int nq,
+                       void* d_yT, int* h_armed);
+int fisdf_y_stream_finish(fisdf_ctx* ctx, int nip, int* h_streamed);
 
 /* What the last build left resident.  Pointers stay valid until the next fisdf_build,
  * fisdf_build_release or fisdf_destroy on the context.  fisdf_build restores the context's stage

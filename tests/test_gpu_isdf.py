@@ -576,3 +576,41 @@ def test_time_reversal_guard():
     df2.build()
     assert df2.time_reversal_used and df2.tr_deviation < 1e-12, df2.tr_deviation
     assert len(df2.fit_qs) < nk
+
+
+@pytest.mark.parametrize("name", ["toy222", "toy331_fr", "toy333_fr", "diamond_szv_gamma",
+                                  "toy222_rank", "toy666"])
+def test_streamed_y_matches(name):
+    """The y build streamed behind the selection (fisdf_build: y formed in blocks of pivots on a
+    second stream while the cooperative selection kernel publishes them) gives the build of the
+    unstreamed path bit for bit: same points, W_q, W_s and J/K.  It engages when the selection
+    returns the point cap under time reversal on a k-mesh the fused y kernel covers; otherwise
+    (a rank-deficient parent Gram, toy222_rank; a 6x6x6 mesh) the streamed y is discarded or
+    never started, and the result is again that of the unstreamed build."""
+    import os
+    res = {}
+    for on in ("0", "1"):
+        os.environ["FISDF_Y_STREAM"] = on
+        try:
+            df, o, dm = make_df(name, inject=False)
+            df.build()
+            vj, vk = df.get_jk(dm)
+            st = df._dev_state
+            res[on] = (df.perm.copy(), st["Wq"].cpu().numpy(), st["Ws"].cpu().numpy(), vj, vk,
+                       df.y_streamed, df.nip)
+        finally:
+            os.environ.pop("FISDF_Y_STREAM", None)
+    a, b = res["0"], res["1"]
+    cell, kmesh, m0, c0, *_ = inputs(name)
+    cap = min(int(cell.nao_nr() * c0), int(np.prod(m0)))
+    print(f"\n{name}: nip {b[6]} (cap {cap}), streamed {b[5]} (unstreamed run {a[5]})")
+    assert not a[5]
+    assert np.array_equal(a[0], b[0])
+    for i, what in ((1, "W_q"), (2, "W_s"), (3, "J"), (4, "K")):
+        assert np.array_equal(a[i], b[i]), what
+    fused = name != "toy666"          # k-meshes with a fused y kernel (linalg.hip yf_launch)
+    # the cooperative selection (the kernel that publishes its pivots) runs below 800 pivots,
+    # on a parent grid of at least 64 points, when its scratch fits (fewer pivots than points)
+    ng0 = int(np.prod(m0))
+    coop = cap < 800 and ng0 >= 64 and cap < ng0
+    assert b[5] == (fused and coop and b[6] == cap)

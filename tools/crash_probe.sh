@@ -20,7 +20,7 @@ for m in 0 1; do
   rm -rf $D
 done
 for c in 1 0; do
-  FISDF_COOP_LAUNCH=$c AMD_LOG_LEVEL=3 timeout -k 10 300 python3 -u bench.py --steps 2 --warmup 1 \
+  FISDF_Y_STREAM=0 FISDF_COOP_LAUNCH=$c AMD_LOG_LEVEL=3 timeout -k 10 300 python3 -u bench.py --steps 2 --warmup 1 \
     --no-cpu-baseline --no-isolated > $OUT/bench_coop$c.json 2> $OUT/bench_coop$c.amdlog
   rc=$?
   echo "bench coop=$c rc=$rc"; cut -c1-300 $OUT/bench_coop$c.json

@@ -1,0 +1,42 @@
+#!/bin/bash
+# Fit-lane serialisation A/B: C3 bench (3 steps) under launch / stream variants,
+# each line: variant, ms/step, TRSM and HERK average launch (ms; ~0.95 / 0.92 = lanes serialised,
+# ~1.74 / 1.23 = overlapped).  Then the group crash with the cooperative-launch mutex off under
+# the runtime log (how many cooperative queues the rank threads create).
+# Usage: bash tools/r06_lanes.sh TAG [ab2]
+set -o pipefail
+TAG=${1:-r06_lanes}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+run() {  # name, env...
+  local name=$1; shift
+  env "$@" timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-isolated > $OUT/$name.json 2> $OUT/$name.err || { echo "$name FAILED"; tail -20 $OUT/$name.err; return 1; }
+  python3 -c "import json; d=json.load(open('$OUT/$name.json')); print('$name', d['ms_per_step'], round(d['roofline']['avg_launch_ms'],3), round(d['roofline_secondary']['avg_launch_ms'],3), d['stages_ms_per_step']['y'])"
+}
+if [ "$2" = "ab2" ]; then
+run base FISDF_Y_STREAM=0 && \
+run ys_aux0 FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=0 && \
+run ys_aux1 FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=1 && \
+run ys_aux2 FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=2 && \
+run plain_pad1 FISDF_Y_STREAM=0 FISDF_COOP_LAUNCH=0 FISDF_PAD_QUEUES=1 && \
+run base_b FISDF_Y_STREAM=0 && \
+run ys_aux1_b FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=1 && \
+run plain_pad1_b FISDF_Y_STREAM=0 FISDF_COOP_LAUNCH=0 FISDF_PAD_QUEUES=1 && \
+run ys_plain_pad1 FISDF_Y_STREAM=1 FISDF_COOP_LAUNCH=0 FISDF_PAD_QUEUES=1 || exit 1
+exit 0
+fi
+run base FISDF_Y_STREAM=0 && \
+run ys_aux1 FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=1 && \
+run ys_aux2 FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=2 && \
+run ys_aux0 FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=0 && \
+run plain FISDF_Y_STREAM=0 FISDF_COOP_LAUNCH=0 && \
+run plain_pad1 FISDF_Y_STREAM=0 FISDF_COOP_LAUNCH=0 FISDF_PAD_QUEUES=1 && \
+run plain_pad2 FISDF_Y_STREAM=0 FISDF_COOP_LAUNCH=0 FISDF_PAD_QUEUES=2 || exit 1
+D=$(mktemp -d)
+FISDF_COOP_MUTEX=0 AMD_LOG_LEVEL=3 timeout -k 10 240 python3 -u tests/capi_shard_worker.py toy331_fr 0 3 $D group > $OUT/group_m0.out 2> $OUT/group_m0.amdlog
+echo "group mutex=0 rc=$? cooperative queues created: $(grep -c 'cooperative: 1' $OUT/group_m0.amdlog)"
+grep -E "SWq|cooperative queue" $OUT/group_m0.amdlog | cut -c1-300 > $OUT/group_m0_queues.txt
+gzip -f $OUT/group_m0.amdlog
+rm -rf $D
+exit 0
