@@ -3270,10 +3270,11 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
   // the fused kernel covers; FISDF_Y_STREAM=0: off): y is formed at the point cap nip_ub on
   // aux[0] while the selection runs, and is kept when the selection returns exactly nip_ub
   // points with time reversal confirmed — else it is discarded and built the usual way.
-  // read per build: the GPU tests compare the two paths in one process
+  // read per build: the GPU tests compare the two paths in one process.  Off unless
+  // FISDF_Y_STREAM=1 until the C3 A/B shows it pays on one GPU
   const bool y_stream_env = [] {
     const char* e = getenv("FISDF_Y_STREAM");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   static const bool y_real_env = [] {  // the self-conjugate q's y real; FISDF_Y_REAL=0: off
     const char* e = getenv("FISDF_Y_REAL");
