@@ -216,7 +216,7 @@ struct fisdf_ctx {
   struct YStream {
     bool armed = false, enqueued = false;
     bool stale = false;  // the kernel it followed failed (a stalled step): its pivots were redone
-    int aux = 1;         // the aux stream it runs on
+    int aux = 2;         // the aux stream it runs on
     const cplx* x0 = nullptr;
     const cplx* f = nullptr;
     int ng0 = 0, nao = 0, nip = 0, rows = 64;
@@ -1121,11 +1121,13 @@ static int ystream_enqueue(fisdf_ctx* c, const int* piv) {
   FISDF_CHECK(yw > 0 && nq > 0, "streamed y: the fused kernel does not apply");
   void* wb = nullptr;
   FISDF_TRY(devbuf_get(c->ws_ystream, yw, &wb));
-  // FISDF_Y_STREAM_AUX (read per build; A/B): the aux stream that carries the streamed y
+  // the aux stream that carries the streamed y: aux[2], the fit's FFT stream, whose FFTs then
+  // follow y in stream order (C3 79.8 / 79.4 ms/step against 81.6 / 81.2 on aux[1] and 79.9 on
+  // aux[0], profiles/r06/lanes2-3); FISDF_Y_STREAM_AUX (read per build) for A/B
   const int ia = [] {
     const char* e = getenv("FISDF_Y_STREAM_AUX");
-    const int v = e ? atoi(e) : 1;
-    return (v >= 0 && v <= 2) ? v : 1;
+    const int v = e ? atoi(e) : 2;
+    return (v >= 0 && v <= 2) ? v : 2;
   }();
   c->ys.aux = ia;
   hipStream_t ys = c->aux[ia];
@@ -1746,10 +1748,12 @@ static int ensure_side(fisdf_ctx* c) {
   // (fisdf_set_factor_priority).  One side stream at a time: an extra stream changes
   // how HIP maps the context's streams onto the process's hardware queues (4 here), and two
   // fit lanes sharing a queue serialise (C3 +5 ms/step measured with a second side stream)
-  // FISDF_PAD_QUEUES=n (experiment): n extra streams, each given one small
-  // copy so the runtime maps it onto a hardware queue, created before the side stream — in the
-  // place the cooperative launch's own queue takes when the selection is launched cooperatively
-  static const int pad_env = getenv("FISDF_PAD_QUEUES") ? atoi(getenv("FISDF_PAD_QUEUES")) : 0;
+  // One padding stream (given one small memset so the runtime maps it onto a hardware queue)
+  // before the side stream, in the place the cooperative launch's own queue takes when the
+  // selection is launched cooperatively: without it, with the plain launch, the fit's two lanes
+  // serialise (C3 90.3 vs 81.3 ms/step; profiles/r06/lanes/).  FISDF_PAD_QUEUES=n overrides.
+  static const int pad_env = getenv("FISDF_PAD_QUEUES") ? atoi(getenv("FISDF_PAD_QUEUES"))
+                                                        : (coop_launch_enabled() ? 0 : 1);
   if (pad_env > 0 && c->pad.empty()) {
     if (!c->pad_buf) FISDF_HIP(hipMalloc(&c->pad_buf, 256));
     for (int i = 0; i < pad_env && i < 8; ++i) {
@@ -3270,11 +3274,10 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
   // the fused kernel covers; FISDF_Y_STREAM=0: off): y is formed at the point cap nip_ub on
   // aux[0] while the selection runs, and is kept when the selection returns exactly nip_ub
   // points with time reversal confirmed — else it is discarded and built the usual way.
-  // read per build: the GPU tests compare the two paths in one process.  Off unless
-  // FISDF_Y_STREAM=1 until the C3 A/B shows it pays on one GPU
+  // read per build: the GPU tests compare the two paths in one process (FISDF_Y_STREAM=0: off)
   const bool y_stream_env = [] {
     const char* e = getenv("FISDF_Y_STREAM");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   static const bool y_real_env = [] {  // the self-conjugate q's y real; FISDF_Y_REAL=0: off
     const char* e = getenv("FISDF_Y_REAL");

@@ -1452,23 +1452,31 @@ bool select_coop_enabled() {
 }
 
 // Launch of a grid whose workgroups wait on each other (the selection kernels): every workgroup
-// must be resident at once.  Default: hipLaunchCooperativeKernel.  FISDF_COOP_LAUNCH=0 launches
-// plainly after the occupancy check (the same residency, MI355X_MICROARCH.md).  Why both
-// (profiles/r05/rocprof_exit/README.txt):
+// must be resident at once.  Default (round 6): a plain launch after the occupancy check (the
+// same residency, MI355X_MICROARCH.md); FISDF_COOP_LAUNCH=1: hipLaunchCooperativeKernel.  Why
+// (profiles/r05/rocprof_exit/README.txt, profiles/r06/lanes/README.txt):
 //  * a process that made one cooperative launch SIGSEGVs in its exit handlers under rocprofv3
-//    (ROCm 7.2; a one-kernel control program with one cooperative launch reproduces it, the same
-//    program without it exits cleanly) — the plain launch leaves profiled processes exiting 0;
-//  * but the plain launch moves the context's streams onto the 4 hardware queues differently: the
-//    two fit lanes then share one and serialise (C3 89.9 vs 81.0 ms/step on one box), so the
-//    cooperative launch stays the default and profiles are judged by their output files.
-// Returns hipErrorCooperativeLaunchTooLarge when the grid would not be co-resident.
-hipError_t launch_coresident(const void* fn, int grid, int threads, void** args, size_t lds,
-                             hipStream_t s, int ncu) {
+//    (ROCm 7.2; a one-kernel control program reproduces it); the plain launch exits cleanly;
+//  * concurrent first cooperative launches from several host threads (fisdf_group's ranks) each
+//    create the device's cooperative queue (three "cooperative: 1" queue creations in the
+//    runtime log for three rank threads), which the runtime's exit handlers then tear down
+//    badly (SIGSEGV in libhsa-runtime64 under libamdhip64's atexit, main thread);
+//  * what made the plain launch slower (the two fit lanes serialised: C3 90 vs 81 ms/step) is
+//    the order the runtime creates hardware queues in, not the launch: the cooperative queue is
+//    created between the context stream's queue and the side / aux streams' ones, and one
+//    padding stream in that place (ensure_side, api.hip) gives the plain launch the same step
+//    time (80.6-80.7 ms either way, interleaved on one box).
+bool coop_launch_enabled() {
   static const bool coop = [] {
     const char* e = getenv("FISDF_COOP_LAUNCH");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
-  if (coop) {
+  return coop;
+}
+
+hipError_t launch_coresident(const void* fn, int grid, int threads, void** args, size_t lds,
+                             hipStream_t s, int ncu) {
+  if (coop_launch_enabled()) {
     // one cooperative launch at a time in the process: concurrent ones from several host threads
     // (fisdf_group's ranks) left the runtime crashing in its exit handlers.  FISDF_COOP_MUTEX=0
     // (diagnosis only, tools/crash_probe.sh) drops the lock to reproduce that crash.

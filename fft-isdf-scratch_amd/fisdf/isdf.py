@@ -678,11 +678,13 @@ def build(df_obj):
     df_obj.time_reversal_used = tr
     # y streamed behind the selection (fisdf_y_stream_arm): this rank's grid slice
     # of y for every fitted q is formed on a second stream as the replicated selection publishes
-    # its pivots, at the point cap; kept when the selection reaches the cap
+    # its pivots, at the point cap; kept when the selection reaches the cap.  Opt-in here
+    # (FISDF_Y_STREAM_SHARDED=1): on an emulated 8-way C3 rank its 1/8-grid y hides under the
+    # selection but slows it by as much (16.5-17.4 vs 17.0 ms, profiles/r06/lanes3/)
     ys_send = None
     sharded = d.sharded(df_obj)
     if df_obj._dev_state is None or "X" not in df_obj._dev_state:
-        if sharded and tr and os.environ.get("FISDF_Y_STREAM", "1") != "0":
+        if sharded and tr and os.environ.get("FISDF_Y_STREAM_SHARDED", "0") == "1":
             ng0 = df_obj._ao_parent.shape[1]
             cap = int(nao * df_obj.c0) if df_obj.nip_max is None else int(df_obj.nip_max)
             nip_cap = max(1, min(cap, ng0))

@@ -63,7 +63,7 @@ def main():
                      vjw0=R.get_j_kpts(xip, ob["w0"], dm), vkw0=R.get_k_kpts(xip, ob["wq"], dm, phase))
     np.savez(out, vj=vj, vk=vk, perm=df.perm, ranks=df.ranks, vj0=vj0, vk0=vk0,
              perm0=o["perm"], wq=df._wq, my_qs=df.my_qs, fit_lanes=lanes.value,
-             fit_pipe=depth.value, **extra)
+             fit_pipe=depth.value, y_streamed=bool(getattr(df, "y_streamed", False)), **extra)
     torch.cuda.synchronize()
     dist.destroy_process_group()
 

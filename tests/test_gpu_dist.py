@@ -56,15 +56,20 @@ def _oracle_on(name, perm):
             R.get_k_kpts(xip, ob["wq"], dm, phase))
 
 
-@pytest.mark.parametrize("name,world", [("toy222", 2), ("toy331", 3), ("toy333_fr", 4)])
-def test_sharded_build_matches_single_gpu(name, world):
+@pytest.mark.parametrize("name,world,ys", [("toy222", 2, "0"), ("toy331", 3, "0"),
+                                           ("toy333_fr", 4, "0"), ("toy222", 2, "1"),
+                                           ("toy331_fr", 3, "1")])
+def test_sharded_build_matches_single_gpu(name, world, ys):
+    """ys = "1": each rank's grid slice of y streamed behind its replicated selection
+    (FISDF_Y_STREAM_SHARDED, fisdf_y_stream_arm / _finish), with the same result."""
     port = _port()
     with tempfile.TemporaryDirectory() as tmp:
         procs = []
         for r in range(world):
             env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
                        MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                       FISDF_DIST_EXTRAS="1" if name == "toy333_fr" else "0")
+                       FISDF_DIST_EXTRAS="1" if name == "toy333_fr" else "0",
+                       FISDF_Y_STREAM_SHARDED=ys)
             procs.append(subprocess.Popen(
                 [sys.executable, os.path.join(HERE, "dist_worker.py"), name, "gloo",
                  os.path.join(tmp, f"r{r}.npz")], env=env))
@@ -76,6 +81,8 @@ def test_sharded_build_matches_single_gpu(name, world):
     vj0, vk0 = _oracle_on(name, df1.perm)
     scale = max(1.0, abs(vk1).max(), abs(vj1).max())
     for r, o in enumerate(outs):
+        # the streamed y engaged where asked (each rank's selection reaches the cap here)
+        assert bool(o["y_streamed"]) == (ys == "1"), (r, bool(o["y_streamed"]))
         # the N-rank build reproduces the 1-GPU one
         assert np.array_equal(o["perm"], df1.perm), "sharded selection != 1-GPU selection"
         dj1, dk1 = abs(o["vj"] - vj1).max(), abs(o["vk"] - vk1).max()

@@ -14,6 +14,34 @@ run() {  # name, env...
   env "$@" timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-isolated > $OUT/$name.json 2> $OUT/$name.err || { echo "$name FAILED"; tail -20 $OUT/$name.err; return 1; }
   python3 -c "import json; d=json.load(open('$OUT/$name.json')); print('$name', d['ms_per_step'], round(d['roofline']['avg_launch_ms'],3), round(d['roofline_secondary']['avg_launch_ms'],3), d['stages_ms_per_step']['y'])"
 }
+if [ "$2" = "ab4" ]; then
+run coop_ys FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=2 && \
+run plain_ys FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=2 FISDF_COOP_LAUNCH=0 FISDF_PAD_QUEUES=1 && \
+run coop FISDF_Y_STREAM=0 && \
+run plain FISDF_Y_STREAM=0 FISDF_COOP_LAUNCH=0 FISDF_PAD_QUEUES=1 && \
+run coop_ys_b FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=2 && \
+run plain_ys_b FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=2 FISDF_COOP_LAUNCH=0 FISDF_PAD_QUEUES=1 && \
+run coop_b FISDF_Y_STREAM=0 && \
+run plain_b FISDF_Y_STREAM=0 FISDF_COOP_LAUNCH=0 FISDF_PAD_QUEUES=1 || exit 1
+FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=2 FISDF_COOP_LAUNCH=0 FISDF_PAD_QUEUES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline --no-isolated --steps 3 --warmup 1 > $OUT/prof_bench.json 2> $OUT/prof.err
+echo "profiled plain_ys rc=$?"
+exit 0
+fi
+if [ "$2" = "ab3" ]; then
+run base FISDF_Y_STREAM=0 && \
+run ys2 FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=2 && \
+run ys2_g242 FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=2 FISDF_SEL_WGS=242 && \
+run ys0_g242 FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=0 FISDF_SEL_WGS=242 && \
+run base_g242 FISDF_Y_STREAM=0 FISDF_SEL_WGS=242 && \
+run base_b FISDF_Y_STREAM=0 && \
+run ys2_g242_b FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=2 FISDF_SEL_WGS=242 && \
+run ys2_b FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=2 || exit 1
+for v in "0 128" "1 128" "1 242"; do set -- $v
+  FISDF_Y_STREAM=$1 FISDF_SEL_WGS=$2 timeout -k 10 400 python -u bench.py --emulate-ranks 8 --steps 5 --warmup 2 > $OUT/emu8_ys$1_g$2.json 2> $OUT/emu8_ys$1_g$2.err || { echo "EMU $v FAILED"; tail -20 $OUT/emu8_ys$1_g$2.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$OUT/emu8_ys$1_g$2.json')); print('emu8 ys=$1 g=$2 max', d['max_rank_ms'], [r['ms_per_step'] for r in d['ranks']])"
+done
+exit 0
+fi
 if [ "$2" = "ab2" ]; then
 run base FISDF_Y_STREAM=0 && \
 run ys_aux0 FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=0 && \
