@@ -656,8 +656,20 @@ int ensure_aux(fisdf_ctx* c) {
     if (hipRuntimeGetVersion(&v) != hipSuccess) return 1;
     return (v / 10000000 > 7 || (v / 10000000 == 7 && (v / 100000) % 100 >= 2)) ? 1 : 0;
   }();
+  // FISDF_FFT_CUS=n (experiment): the FFT stream confined to n CUs spread evenly over the device
+  // (hipExtStreamCreateWithCUMask), so the HBM-bound FFTs stop taking workgroup slots on every CU
+  static const int fft_cus = getenv("FISDF_FFT_CUS") ? atoi(getenv("FISDF_FFT_CUS")) : 0;
   for (int l = 0; l < 3; ++l) {
-    if (l == 2 && fft_prio != 1)
+    if (l == 2 && fft_cus > 0) {
+      const int ncu = num_cus(c->device);
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+      const int n = std::min(fft_cus, ncu);
+      for (int i = 0; i < n; ++i) {
+        const int cu = (int)((long)i * ncu / n);
+        mask[cu / 32] |= 1u << (cu % 32);
+      }
+      FISDF_HIP(hipExtStreamCreateWithCUMask(&c->aux[l], (uint32_t)mask.size(), mask.data()));
+    } else if (l == 2 && fft_prio != 1)
       FISDF_HIP(hipStreamCreateWithPriority(&c->aux[l], hipStreamNonBlocking,
                                             fft_prio == 2 ? greatest : least));
     else

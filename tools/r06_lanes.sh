@@ -11,9 +11,20 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 run() {  # name, env...
   local name=$1; shift
-  env "$@" timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-isolated > $OUT/$name.json 2> $OUT/$name.err || { echo "$name FAILED"; tail -20 $OUT/$name.err; return 1; }
+  env FISDF_NOOP=1 "$@" timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-isolated > $OUT/$name.json 2> $OUT/$name.err || { echo "$name FAILED"; tail -20 $OUT/$name.err; return 1; }
   python3 -c "import json; d=json.load(open('$OUT/$name.json')); print('$name', d['ms_per_step'], round(d['roofline']['avg_launch_ms'],3), round(d['roofline_secondary']['avg_launch_ms'],3), d['stages_ms_per_step']['y'])"
 }
+if [ "$2" = "ab5" ]; then
+run base && \
+run aux0 FISDF_Y_STREAM_AUX=0 && \
+run aux0_fft64 FISDF_Y_STREAM_AUX=0 FISDF_FFT_CUS=64 && \
+run aux0_fft128 FISDF_Y_STREAM_AUX=0 FISDF_FFT_CUS=128 && \
+run aux0_fft192 FISDF_Y_STREAM_AUX=0 FISDF_FFT_CUS=192 && \
+run base_b && \
+run aux0_fft128_b FISDF_Y_STREAM_AUX=0 FISDF_FFT_CUS=128 && \
+run aux0_b FISDF_Y_STREAM_AUX=0 || exit 1
+exit 0
+fi
 if [ "$2" = "ab4" ]; then
 run coop_ys FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=2 && \
 run plain_ys FISDF_Y_STREAM=1 FISDF_Y_STREAM_AUX=2 FISDF_COOP_LAUNCH=0 FISDF_PAD_QUEUES=1 && \
