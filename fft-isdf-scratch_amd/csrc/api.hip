@@ -3226,9 +3226,21 @@ int comm_check(int rc, const char* what) {
 // fisdf_build (comm NULL) and fisdf_build_sharded: ISDF.build() (fftisdf.py:308-325 ->
 // build(df_obj), :22-128), the same stage sequence as the Python mirror's build (fisdf/isdf.py
 // build(): its unsharded branch, and its k-sharded branch with the caller's collectives)
+// FISDF_HOST_TRACE=1 (diagnosis): host timestamps (CLOCK_MONOTONIC, the clock of Python's
+// time.perf_counter) of the composite build's hand-offs, to stderr — where the host holds the
+// device idle between a step's last kernel and the next step's first
+static void host_mark(const char* what) {
+  static const bool on = getenv("FISDF_HOST_TRACE") != nullptr;
+  if (!on) return;
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  fprintf(stderr, "fisdf-host %.6f %s\n", ts.tv_sec + 1e-9 * ts.tv_nsec, what);
+}
+
 int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, const void* f,
                int nao, const int kmesh[3], const int mesh[3], const double a[9],
                const fisdf_build_opts* opts_in, int* h_nip) {
+  host_mark("build enter");
   fisdf_build_opts o;
   fisdf_build_opts_default(&o);
   if (opts_in) o = *opts_in;
@@ -3272,7 +3284,9 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
   }
   // the previous build's buffers go back to the caller's allocator now, while the check runs
   // (in the mirror each is a Python callback: done first, they left the GPU idle between steps)
+  host_mark("tr check enqueued");
   build_return_all(c);
+  host_mark("previous buffers returned");
   // X and x4 at their upper bound (the point cap) taken now, while the check runs: the caller's
   // allocator (a Python callback in the mirror, ~40 us each) then no longer sits in the idle gap
   // between the selection's read-back and the gather
@@ -3321,6 +3335,7 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
     FISDF_TRY(ystream_arm(c, x0, ng0, f, ngrid * nao, ngrid, nao, nip_ub, kmesh, ys_qs.data(),
                           (int)ys_qs.size(), yT_pre, rmask, &armed));
   }
+  host_mark("allocations + y stream armed");
   // interpolation points (:33 -> :357-388), or the caller's
   std::vector<int> perm;
   for (int attempt = 0;; ++attempt) {
@@ -3344,6 +3359,7 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
                       "max |a| = %.3e): every q fitted\n", tr_dev);
     tr = false;
   }
+  host_mark("selection read back");
   const int nip = (int)perm.size();
   FISDF_CHECK(nip > 0, "build: no interpolation points");
   const long nn = (long)nip * nip;
@@ -3410,7 +3426,9 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
     FISDF_TRY(build_alloc(c, BR_WQ, sizeof(cplx) * (size_t)nq * nn, &Wq));
     // the fit waits for the factor's verdict itself
     FISDF_TRY(fisdf_fit_coulomb_qs(c, qs.data(), nq, yT, nip, mesh, kmesh, a, Wq)); // :97-121
+    host_mark("fit enqueued");
     FISDF_TRY(fisdf_factor_x4_wait(c, ranks.data()));
+    host_mark("factor ranks read back");
     FISDF_TRY(fisdf_factor_info(c, &used));
     FISDF_TRY(fisdf_min_norm_info(c, &ncod));
     // a block that waited past its bound built y from unfinished pivots
@@ -3548,6 +3566,7 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
   B.row0 = (int)row0;
   B.row1 = (int)row1;
   if (h_nip) *h_nip = nip;
+  host_mark("build return");
   return 0;
 }
 

@@ -527,6 +527,9 @@ __global__ __launch_bounds__(SC_THREADS) void pchol_select_coop(
   __shared__ double s_dp, s_thr;
   const int G = gridDim.x, w = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r0 = w * RW, nr = max(0, min(RW, n - r0));
+  // with a streamed consumer (progress) other kernels share the CUs: the dependent pivot chain
+  // issues first
+  if (progress) __builtin_amdgcn_s_setprio(3);
   if (tid < RW) {
     double v = -1e300;
     if (tid < nr) {

@@ -12,8 +12,18 @@ export TMPDIR=/tmp
 run() {  # name, env...
   local name=$1; shift
   env FISDF_NOOP=1 "$@" timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-isolated > $OUT/$name.json 2> $OUT/$name.err || { echo "$name FAILED"; tail -20 $OUT/$name.err; return 1; }
-  python3 -c "import json; d=json.load(open('$OUT/$name.json')); print('$name', d['ms_per_step'], round(d['roofline']['avg_launch_ms'],3), round(d['roofline_secondary']['avg_launch_ms'],3), d['stages_ms_per_step']['y'])"
+  python3 -c "import json; d=json.load(open('$OUT/$name.json')); s=d['stages_ms_per_step']; print('$name', d['ms_per_step'], round(d['roofline']['avg_launch_ms'],3), round(d['roofline_secondary']['avg_launch_ms'],3), 'sel', s['select'], 'y', s['y'])"
 }
+if [ "$2" = "ab6" ]; then
+run ys && \
+run ys_g242 FISDF_SEL_WGS=242 && \
+run ys_g176 FISDF_SEL_WGS=176 && \
+run ys_r32 FISDF_Y_STREAM_ROWS=32 && \
+run ys_b && \
+run ys_g242_b FISDF_SEL_WGS=242 && \
+run ys_r32_b FISDF_Y_STREAM_ROWS=32 || exit 1
+exit 0
+fi
 if [ "$2" = "ab5" ]; then
 run base && \
 run aux0 FISDF_Y_STREAM_AUX=0 && \
