@@ -1455,8 +1455,10 @@ bool select_coop_enabled() {
 }
 
 // Launch of a grid whose workgroups wait on each other (the selection kernels): every workgroup
-// must be resident at once.  Default (round 6): a plain launch after the occupancy check (the
-// same residency, MI355X_MICROARCH.md); FISDF_COOP_LAUNCH=1: hipLaunchCooperativeKernel.  Why
+// must be resident at once.  Default (round 6) below the HIP 7.2 runtime (torch's bundled 7.0,
+// the mirror and bench.py): a plain launch after the occupancy check (the same residency,
+// MI355X_MICROARCH.md); from 7.2 on (the torch-free C-ABI) hipLaunchCooperativeKernel, which is
+// faster there; FISDF_COOP_LAUNCH=0/1 forces either.  Why the plain launch where it is as fast
 // (profiles/r05/rocprof_exit/README.txt, profiles/r06/lanes/README.txt):
 //  * a process that made one cooperative launch SIGSEGVs in its exit handlers under rocprofv3
 //    (ROCm 7.2; a one-kernel control program reproduces it); the plain launch exits cleanly;
@@ -1472,7 +1474,14 @@ bool select_coop_enabled() {
 bool coop_launch_enabled() {
   static const bool coop = [] {
     const char* e = getenv("FISDF_COOP_LAUNCH");
-    return e && e[0] == '1';
+    if (e) return e[0] == '1';
+    // the plain launch (+ padding stream) matches the cooperative one on the ROCm 7.0 runtime
+    // torch bundles (C3 80.6-80.7 ms either way) but not on the system 7.2 runtime the torch-free
+    // C-ABI runs on (83.3 vs 79.5 ms/step, padding 0-2 streams: 82.9-83.5; profiles/r06/capi/):
+    // cooperative from 7.2 on
+    int v = 0;
+    if (hipRuntimeGetVersion(&v) != hipSuccess) return false;
+    return v / 10000000 > 7 || (v / 10000000 == 7 && (v / 100000) % 100 >= 2);
   }();
   return coop;
 }
