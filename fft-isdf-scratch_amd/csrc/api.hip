@@ -1212,8 +1212,8 @@ static int ystream_arm(fisdf_ctx* c, const void* x0, int ng0, const void* f, lon
   Y.qs.assign(qs, qs + nq);
   Y.yT = (cplx*)yT;
   Y.rmask = rmask;
-  // FISDF_Y_STREAM_ROWS: pivots per block (a multiple of 16; default 64)
-  static const int rows_env = [] {
+  // FISDF_Y_STREAM_ROWS: pivots per block (a multiple of 16; default 64; read per build)
+  const int rows_env = [] {
     const char* e = getenv("FISDF_Y_STREAM_ROWS");
     const int v = e ? atoi(e) : 64;
     return (v >= 16 && v % 16 == 0 && v <= 1024) ? v : 64;

@@ -4,6 +4,9 @@ so box-to-box and process-to-process variance drop out of the comparison.  Only 
 library reads per call / per build can be compared this way (FISDF_Y_STREAM,
 FISDF_Y_STREAM_AUX, FISDF_SEL_WGS, FISDF_SEL_LDS_COLS, FISDF_Y_STREAM_ROWS, ...).
   python tools/ab_inproc.py --cfg "base:FISDF_Y_STREAM=0" --cfg "ys:" [--rounds 4 --steps 4]
+A setting "ctx.NAME=a/b" calls the context entry NAME(ctx, a, b) (ints) before the
+configuration's steps, and NAME's round-6 defaults are put back before the next one
+(fisdf_set_fit_pipe -> (-1, 0), fisdf_set_fit_lanes -> 0).
 Prints one JSON line: per configuration the per-round ms/step and their mean / min."""
 import argparse
 import json
@@ -46,11 +49,17 @@ def main():
         df.get_jk(dm)
 
     res = {n: [] for n, _ in cfgs}
+    defaults = {"fisdf_set_fit_pipe": (-1, 0), "fisdf_set_fit_lanes": (0,)}
     for r in range(a.rounds):
         for name, env in cfgs:
             for k in keys:
                 os.environ.pop(k, None)
-            os.environ.update(env)
+            for fn, dv in defaults.items():
+                d.ctx.call(fn, *dv)
+            for k, v in env.items():
+                if k.startswith("ctx."):
+                    d.ctx.call(k[4:], *[int(x) for x in v.split("/")])
+            os.environ.update({k: v for k, v in env.items() if not k.startswith("ctx.")})
             step()
             torch.cuda.synchronize()
             t = time.perf_counter()
