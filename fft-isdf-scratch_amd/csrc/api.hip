@@ -219,7 +219,7 @@ struct fisdf_ctx {
     int aux = 2;         // the aux stream it runs on
     const cplx* x0 = nullptr;
     const cplx* f = nullptr;
-    int ng0 = 0, nao = 0, nip = 0, rows = 64;
+    int ng0 = 0, nao = 0, nip = 0, rows = 128;
     long m = 0, fks = 0;  // grid points of the y build (columns of yT), k stride of f
     int kmesh[3] = {0, 0, 0};
     std::vector<int> qs;
@@ -1212,11 +1212,13 @@ static int ystream_arm(fisdf_ctx* c, const void* x0, int ng0, const void* f, lon
   Y.qs.assign(qs, qs + nq);
   Y.yT = (cplx*)yT;
   Y.rmask = rmask;
-  // FISDF_Y_STREAM_ROWS: pivots per block (a multiple of 16; default 64; read per build)
+  // pivots per block, FISDF_Y_STREAM_ROWS (a multiple of 16; read per build): 128 — C3 in one
+  // process, 4 interleaved rounds: 64 rows 78.77, 128 78.29, 192 78.23, 256 78.45, unstreamed
+  // 79.96 ms/step (profiles/r06/ab9_inproc.json); fewer, larger launches beat an earlier start
   const int rows_env = [] {
     const char* e = getenv("FISDF_Y_STREAM_ROWS");
-    const int v = e ? atoi(e) : 64;
-    return (v >= 16 && v % 16 == 0 && v <= 1024) ? v : 64;
+    const int v = e ? atoi(e) : 128;
+    return (v >= 16 && v % 16 == 0 && v <= 1024) ? v : 128;
   }();
   Y.rows = rows_env;
   Y.armed = true;
