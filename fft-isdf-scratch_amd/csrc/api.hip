@@ -2951,14 +2951,23 @@ static int get_k_block(fisdf_ctx* c, const void* Xv, const double* Ws_rows, long
     } else {
       FISDF_TRY(zgemm(c->stream, OP_N, OP_T, nb, nip, nao, ONE, T, nao, ba, X, nao, xs, ZERO, B1,
                       nip, bn, nk));
-      // rho_s = Phi rho_k (:215), real (:216), and V_s = W_s * rho_s^T (:219) for the block
-      // rows, both in the GEMM's epilogue (EPI_WSRHO: Re(W_s) Re(.), max |Im rho_s| recorded)
-      FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, bn, nk, ONE, phase, nk, 0, B1, bn, 0, ZERO, B2,
-                      bn, 0, 1, 1, (cplx*)(void*)Ws_rows, EPI_WSRHO, c->maximag + 2, GEMM_FULL,
-                      ws_Rstride));
-      // V_k = Phi^T V_s (:222)
-      FISDF_TRY(zgemm(c->stream, OP_T, OP_N, nk, bn, nk, ONE, phase, nk, 0, B2, bn, 0, ZERO, B1,
-                      bn, 0, 1));
+      // round 6: the transform pair and the product in one register pass per column (C3: 0.50
+      // -> ~0.2 ms); FISDF_K_DFT=0 (read per call: the GPU tests compare) keeps the GEMMs
+      bool done = false;
+      const char* kd = getenv("FISDF_K_DFT");
+      if (!(kd && kd[0] == '0'))
+        FISDF_TRY(k_wsrho_reg(c->stream, B1, bn, kmesh, Ws_rows, ws_Rstride, c->maximag + 2,
+                              &done));
+      if (!done) {
+        // rho_s = Phi rho_k (:215), real (:216), and V_s = W_s * rho_s^T (:219) for the block
+        // rows, both in the GEMM's epilogue (EPI_WSRHO: Re(W_s) Re(.), max |Im rho_s| recorded)
+        FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, bn, nk, ONE, phase, nk, 0, B1, bn, 0, ZERO, B2,
+                        bn, 0, 1, 1, (cplx*)(void*)Ws_rows, EPI_WSRHO, c->maximag + 2, GEMM_FULL,
+                        ws_Rstride));
+        // V_k = Phi^T V_s (:222)
+        FISDF_TRY(zgemm(c->stream, OP_T, OP_N, nk, bn, nk, ONE, phase, nk, 0, B2, bn, 0, ZERO, B1,
+                        bn, 0, 1));
+      }
     }
     // K_k (block part) = X_k[I]^H (V_k[I, :] X_k)  (:225)
     FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nb, nao, nip, ONE, B1, nip, bn, X, nao, xs, ZERO, T,

@@ -126,5 +126,10 @@ int kmesh_y(hipStream_t s, const cplx* FX, long ncol, const int kmesh[3], const 
             unsigned long long* mon, bool conj_out = false);
 // whether kmesh_y runs its register kernel for this k-mesh and column count (no device q-list)
 bool kmesh_y_reg_applies(const int kmesh[3], long ncol);
+// get_k's rho_s = Phi rho_k, V_s = W_s * Re(rho_s), V_k = Phi^T V_s in place on B (nk rows of
+// ncol columns; W_s row s at Ws + s * ws_Rstride) for the register k-meshes; *handled = false
+// (nothing enqueued) otherwise.  max |Im rho_s| into *mon
+int k_wsrho_reg(hipStream_t s, cplx* B, long ncol, const int kmesh[3], const double* Ws,
+                long ws_Rstride, unsigned long long* mon, bool* handled);
 
 }  // namespace fisdf

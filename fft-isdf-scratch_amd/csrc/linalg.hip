@@ -499,6 +499,50 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   if ((threadIdx.x & 63) == 0 && mon) atomicMax(mon, (unsigned long long)__double_as_longlong(mi));
 }
 
+// get_k's k-mesh transform pair in registers (fftisdf.py:211-222), one thread per (I, J) column
+// of the block rows, in place: rho_s = Phi rho_k (:215, real: max |Im| recorded, :216),
+// V_s = W_s * Re(rho_s) (:219; W_s real, row s at Ws + s * ws_Rstride), V_k = Phi^T V_s (:222) —
+// the separable DFTs of kmesh_y_reg_kernel (Phi[R][q] = e^{i T_R . k_q} / sqrt(nk) is symmetric,
+// so Phi^T is the same transform) instead of two dense nk x nk GEMMs with the product in the
+// first one's epilogue: one read of rho_k and W_s, one write of V_k.
+template <int N0, int N1, int N2>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_wsrho_reg_kernel(
+    cplx* __restrict__ B, long ncol, const double* __restrict__ Ws, long ws_Rstride,
+    unsigned long long* __restrict__ mon) {
+  constexpr int NK = N0 * N1 * N2;
+  cplx tw0[N0], tw1[N1], tw2[N2];
+#pragma unroll
+  for (int t = 0; t < N0; ++t) { double s, c; sincospi(2.0 * t / N0, &s, &c); tw0[t] = cmk(c, s); }
+#pragma unroll
+  for (int t = 0; t < N1; ++t) { double s, c; sincospi(2.0 * t / N1, &s, &c); tw1[t] = cmk(c, s); }
+#pragma unroll
+  for (int t = 0; t < N2; ++t) { double s, c; sincospi(2.0 * t / N2, &s, &c); tw2[t] = cmk(c, s); }
+  const double sc = 1.0 / sqrt((double)NK);
+  double mi = 0.0;
+  for (long col = blockIdx.x * (long)blockDim.x + threadIdx.x; col < ncol;
+       col += (long)gridDim.x * blockDim.x) {
+    cplx v[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) v[k] = B[(long)k * ncol + col];
+    reg_axis_dft<N0, N1 * N2, NK>(v, tw0);
+    reg_axis_dft<N1, N2, NK>(v, tw1);
+    reg_axis_dft<N2, 1, NK>(v, tw2);
+#pragma unroll
+    for (int s = 0; s < NK; ++s) {
+      mi = fmax(mi, fabs(v[s].y * sc));
+      v[s] = cmk(Ws[(long)s * ws_Rstride + col] * (v[s].x * sc), 0.0);
+    }
+    reg_axis_dft<N0, N1 * N2, NK>(v, tw0);
+    reg_axis_dft<N1, N2, NK>(v, tw1);
+    reg_axis_dft<N2, 1, NK>(v, tw2);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) B[(long)k * ncol + col] = cmk(v[k].x * sc, v[k].y * sc);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mi = fmax(mi, __shfl_xor(mi, o, 64));
+  if ((threadIdx.x & 63) == 0 && mon) atomicMax(mon, (unsigned long long)__double_as_longlong(mi));
+}
+
 // Fused y build for the register k-meshes under time reversal (fftisdf.py:76-85).  One
 // workgroup per 16 (I) x 16 (g) column tile; fx_k = X_k f_k^H is formed on FP64 MFMA for the
 // representative k (K = nao, 3-multiplication complex form: t1 = Xr fr, t2 = Xi fi,
@@ -1483,6 +1527,24 @@ int kmesh_rep_runs(const int kmesh[3], std::vector<int>* runs) {
 #define FISDF_KM_REG_MESHES(X)                                                                 \
   X(1, 1, 1) X(1, 1, 2) X(2, 2, 2) X(3, 3, 1) X(3, 3, 3) X(4, 4, 4) X(2, 2, 1) X(1, 2, 2)       \
   X(4, 4, 1) X(2, 2, 4)
+
+int k_wsrho_reg(hipStream_t s, cplx* B, long ncol, const int kmesh[3], const double* Ws,
+                long ws_Rstride, unsigned long long* mon, bool* handled) {
+  *handled = false;
+  if (ncol <= 0) return 0;
+  const unsigned grid = (unsigned)std::max<long>(1, std::min<long>((ncol + 63) / 64, 32768));
+#define FISDF_KW(a, b, c)                                                                      \
+  if (kmesh[0] == a && kmesh[1] == b && kmesh[2] == c) {                                       \
+    hipLaunchKernelGGL((k_wsrho_reg_kernel<a, b, c>), dim3(grid), dim3(64), 0, s, B, ncol, Ws,  \
+                       ws_Rstride, mon);                                                       \
+    FISDF_HIP(hipGetLastError());                                                              \
+    *handled = true;                                                                           \
+    return 0;                                                                                  \
+  }
+  FISDF_KM_REG_MESHES(FISDF_KW)
+#undef FISDF_KW
+  return 0;
+}
 
 bool kmesh_y_reg_applies(const int kmesh[3], long ncol) {
   bool on = false;

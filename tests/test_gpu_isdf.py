@@ -614,3 +614,27 @@ def test_streamed_y_matches(name):
     ng0 = int(np.prod(m0))
     coop = cap < 800 and ng0 >= 64 and cap < ng0
     assert b[5] == (fused and coop and b[6] == cap)
+
+
+@pytest.mark.parametrize("name", ["toy222", "toy331_fr", "toy333_fr", "nio_small"])
+def test_get_k_register_transform(name):
+    """get_k's k-mesh transform pair (rho_s = Phi rho_k, V_s = W_s Re(rho_s), V_k = Phi^T V_s,
+    fftisdf.py:211-222) in one register pass per column equals the two dense Phi GEMMs with the
+    product in the first one's epilogue (FISDF_K_DFT=0) to rounding, and the oracle's K."""
+    import os
+    df, o, dm = make_df(name)
+    df.build()
+    res = {}
+    for on in ("0", "1"):
+        os.environ["FISDF_K_DFT"] = on
+        try:
+            res[on] = df.get_jk(dm)
+        finally:
+            os.environ.pop("FISDF_K_DFT", None)
+    scale = max(1.0, abs(res["0"][1]).max())
+    d = abs(res["1"][1] - res["0"][1]).max() / scale
+    ek = abs(res["1"][1] - o["vk"]).max()
+    print(f"\n{name}: |K(register) - K(GEMMs)| / max|K| = {d:.1e}; |dK| vs oracle {ek:.2e}")
+    assert d < 1e-13
+    assert ek < JK_TOL
+    assert np.array_equal(res["1"][0], res["0"][0])     # J untouched
