@@ -212,6 +212,7 @@ struct fisdf_ctx {
   int* ys_err_pinned = nullptr;
   hipEvent_t ev_yerr = nullptr;
   hipEvent_t ev_ysfork = nullptr;  // `stream` just before the selection kernel: the y stream's start
+  hipEvent_t ev_ys2[2] = {nullptr, nullptr};  // the streamed y's second stream (FISDF_Y_STREAM_2S)
   DevBuf ws_ypiv, ws_ystream;
   struct YStream {
     bool armed = false, enqueued = false;
@@ -808,6 +809,8 @@ int fisdf_destroy(fisdf_ctx* c) {
   if (c->ys_err_pinned) (void)hipHostFree(c->ys_err_pinned);
   if (c->ev_yerr) (void)hipEventDestroy(c->ev_yerr);
   if (c->ev_ysfork) (void)hipEventDestroy(c->ev_ysfork);
+  for (hipEvent_t e : c->ev_ys2)
+    if (e) (void)hipEventDestroy(e);
   for (auto* w : {&c->ws_main, &c->ws_side_a, &c->ws_side_b, &c->ws_ypiv, &c->ws_ystream})
     if (w->p) (void)hipFree(w->p);
   for (hipStream_t p : c->pad) (void)hipStreamDestroy(p);
@@ -1145,12 +1148,29 @@ static int ystream_enqueue(fisdf_ctx* c, const int* piv) {
   hipStream_t ys = c->aux[ia];
   aux_fork(c, ia);
   FISDF_HIP(hipStreamWaitEvent(ys, c->ev_ysfork, 0));
+  // blocks alternate over aux[ia] and a second aux stream (one block's tail overlaps the next
+  // one's start), ordered back into aux[ia] at the end, so joining aux[ia] joins both: C3 in one
+  // process 79.05 / 79.30 against 79.52 / 79.59 ms/step on one stream (profiles/r06/ab11-12);
+  // FISDF_Y_STREAM_2S=0 (read per build) keeps one stream
+  const char* e2 = getenv("FISDF_Y_STREAM_2S");
+  const int i2 = (e2 && e2[0] == '0') ? -1 : (ia == 0 ? 1 : 0);
+  if (i2 >= 0 && !c->ev_ys2[0]) {
+    FISDF_HIP(hipEventCreateWithFlags(&c->ev_ys2[0], hipEventDisableTiming));
+    FISDF_HIP(hipEventCreateWithFlags(&c->ev_ys2[1], hipEventDisableTiming));
+  }
   bool handled = false;
   {
     StageTimer tm(c, FISDF_ST_Y, ys);
     FISDF_TRY(y_fused_stream(ys, Y.x0, Y.ng0, Y.nao, piv, c->ys_dev, c->ys_dev + 1, Y.nip, Y.rows,
                              Y.f, Y.fks, (int)Y.m, Y.kmesh, Y.qs.data(), nq, Y.yT,
-                             (long)Y.nip * Y.m, Y.m, 0, (cplx*)wb, yw, Y.rmask, &handled));
+                             (long)Y.nip * Y.m, Y.m, 0, (cplx*)wb, yw, Y.rmask, &handled,
+                             i2 >= 0 ? c->aux[i2] : nullptr, c->ev_ys2[0], c->ev_ys2[1]));
+  }
+  // aux[i2]'s work is ordered before aux[ia]'s last command: joined with it (buffer-return
+  // bookkeeping, check_aux_joined)
+  if (i2 >= 0) {
+    aux_fork(c, i2);
+    c->aux_joined[i2] = c->aux_use[i2];
   }
   FISDF_CHECK(handled, "streamed y: nothing enqueued");
   Y.enqueued = true;

@@ -1719,10 +1719,11 @@ int y_fused_stream(hipStream_t s, const cplx* x0, int ng0, int nao, const int* p
                    const int* progress, int* err, int nip, int rows, const cplx* F, long fks,
                    int m, const int kmesh[3], const int* h_qs, int nq, cplx* yT, long qs, long Is,
                    long goff, cplx* work, size_t work_bytes, unsigned long long rmask,
-                   bool* handled) {
+                   bool* handled, hipStream_t s2, hipEvent_t ev_a, hipEvent_t ev_b) {
   *handled = false;
   if (m <= 0 || nip <= 0) return 0;
   FISDF_CHECK(rows >= 16 && rows % 16 == 0 && rows <= 64 * 16, "y_fused_stream: bad row block");
+  FISDF_CHECK(!s2 || (ev_a && ev_b), "y_fused_stream: a second stream needs two events");
   YfPlan plan;
   unsigned long long qmask = 0;
   size_t lds = 0;
@@ -1741,15 +1742,26 @@ int y_fused_stream(hipStream_t s, const cplx* x0, int ng0, int nao, const int* p
   hipLaunchKernelGGL(yf_transpose_kernel, dim3((m + 63) / 64, nsl), dim3(256), tl, s, F, fks, m,
                      nao, plan, FT);
   FISDF_HIP(hipGetLastError());
-  for (int lo = 0; lo < nip; lo += rows) {
+  // s2 (optional): odd blocks on a second stream, so one block's tail overlaps the next one's
+  // start; s waits for s2 at the end (everything after the call on s sees the whole y)
+  if (s2) {
+    FISDF_HIP(hipEventRecord(ev_a, s));
+    FISDF_HIP(hipStreamWaitEvent(s2, ev_a, 0));
+  }
+  for (int lo = 0, b = 0; lo < nip; lo += rows, ++b) {
     const int hi = std::min(nip, lo + rows);
-    hipLaunchKernelGGL(yf_xt_stream_kernel, dim3((hi - lo + 63) / 64, nsl), dim3(256), tl, s, x0,
+    hipStream_t sb = (s2 && (b & 1)) ? s2 : s;
+    hipLaunchKernelGGL(yf_xt_stream_kernel, dim3((hi - lo + 63) / 64, nsl), dim3(256), tl, sb, x0,
                        (long)ng0 * nao, ng0, nao, piv, progress, lo, hi, nip, plan, XT, err);
     FISDF_HIP(hipGetLastError());
     bool h = false;
-    FISDF_TRY(yf_launch(s, kmesh, XT, nip, nao, FT, m, lo / 16, (hi - lo + 15) / 16, plan, qmask,
+    FISDF_TRY(yf_launch(sb, kmesh, XT, nip, nao, FT, m, lo / 16, (hi - lo + 15) / 16, plan, qmask,
                         rmask, yT, qs, Is, goff, lds, &h));
     FISDF_CHECK(h, "y_fused_stream: no kernel for this k-mesh");
+  }
+  if (s2) {
+    FISDF_HIP(hipEventRecord(ev_b, s2));
+    FISDF_HIP(hipStreamWaitEvent(s, ev_b, 0));
   }
   *handled = true;
   return 0;
