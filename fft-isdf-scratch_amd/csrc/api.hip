@@ -105,7 +105,7 @@ struct fisdf_ctx {
   struct DevBuf {
     void* p = nullptr;
     size_t n = 0;
-  } ws_main, ws_side_a, ws_side_b;
+  } ws_main, ws_side_a, ws_side_b, ws_x4;  // ws_x4: x2_k of an x4 built on the side stream
   int* f_nip_dev = nullptr;     // device copy of nip (scatter of a full W_PP)
   int lanes = 0;           // fisdf_set_fit_lanes; 0: environment FISDF_FIT_LANES / default
   bool time_reversal = false;  // fisdf_set_time_reversal: fx_{-k} = conj(fx_k) in build_y
@@ -217,6 +217,7 @@ struct fisdf_ctx {
   struct YStream {
     bool armed = false, enqueued = false;
     bool stale = false;  // the kernel it followed failed (a stalled step): its pivots were redone
+    bool gated = false;  // later blocks wait for the gate (ys_dev[2]): someone must open it
     int aux = 2;         // the aux stream it runs on
     const cplx* x0 = nullptr;
     const cplx* f = nullptr;
@@ -811,7 +812,7 @@ int fisdf_destroy(fisdf_ctx* c) {
   if (c->ev_ysfork) (void)hipEventDestroy(c->ev_ysfork);
   for (hipEvent_t e : c->ev_ys2)
     if (e) (void)hipEventDestroy(e);
-  for (auto* w : {&c->ws_main, &c->ws_side_a, &c->ws_side_b, &c->ws_ypiv, &c->ws_ystream})
+  for (auto* w : {&c->ws_main, &c->ws_side_a, &c->ws_side_b, &c->ws_x4, &c->ws_ypiv, &c->ws_ystream})
     if (w->p) (void)hipFree(w->p);
   for (hipStream_t p : c->pad) (void)hipStreamDestroy(p);
   if (c->pad_buf) (void)hipFree(c->pad_buf);
@@ -1158,13 +1159,24 @@ static int ystream_enqueue(fisdf_ctx* c, const int* piv) {
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_ys2[0], hipEventDisableTiming));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_ys2[1], hipEventDisableTiming));
   }
+  // FISDF_Y_GATE_FROM=b (experiment, read per build; default -1, off): the blocks from b on also
+  // wait for the gate (ys_dev[2]), which the build opens once x4 is done, so they leave the CU
+  // slots to x4 and the factor chain when the selection ends.  x4 then takes 1.3 ms instead of
+  // 3.0, but the chain after it stretches from 4.1 to 5.2 ms beside the released blocks and the
+  // step is 0.5-1 ms slower (profiles/r06/r06_gate)
+  const int gate_from = [] {
+    const char* e = getenv("FISDF_Y_GATE_FROM");
+    return e ? atoi(e) : -1;
+  }();
+  Y.gated = gate_from >= 0;
   bool handled = false;
   {
     StageTimer tm(c, FISDF_ST_Y, ys);
     FISDF_TRY(y_fused_stream(ys, Y.x0, Y.ng0, Y.nao, piv, c->ys_dev, c->ys_dev + 1, Y.nip, Y.rows,
                              Y.f, Y.fks, (int)Y.m, Y.kmesh, Y.qs.data(), nq, Y.yT,
                              (long)Y.nip * Y.m, Y.m, 0, (cplx*)wb, yw, Y.rmask, &handled,
-                             i2 >= 0 ? c->aux[i2] : nullptr, c->ev_ys2[0], c->ev_ys2[1]));
+                             i2 >= 0 ? c->aux[i2] : nullptr, c->ev_ys2[0], c->ev_ys2[1],
+                             c->ys_dev + 2, gate_from));
   }
   // aux[i2]'s work is ordered before aux[ia]'s last command: joined with it (buffer-return
   // bookkeeping, check_aux_joined)
@@ -1186,9 +1198,18 @@ static bool ystream_valid(fisdf_ctx* c, int nip, const int* qs, int nq) {
          std::equal(Y.qs.begin(), Y.qs.end(), qs);
 }
 
+// open the streamed y's gate on stream st (stream-ordered: after whatever st has enqueued)
+static int ystream_open_gate(fisdf_ctx* c, hipStream_t st) {
+  if (!c->ys.enqueued || !c->ys.gated) return 0;
+  FISDF_HIP(hipMemsetD32Async(c->ys_dev + 2, 1, 1, st));
+  c->ys.gated = false;
+  return 0;
+}
+
 static int ystream_join(fisdf_ctx* c) {
   const int ia = c->ys.aux;
   if (!c->ys.enqueued || c->aux_joined[ia] == c->aux_use[ia]) return 0;
+  FISDF_TRY(ystream_open_gate(c, c->stream));  // nobody opened it: the join would wait forever
   FISDF_TRY(aux_join(c, ia));
   FISDF_HIP(hipMemcpyAsync(c->ys_err_pinned, c->ys_dev + 1, sizeof(int), hipMemcpyDeviceToHost,
                            c->stream));
@@ -1272,7 +1293,7 @@ static int select_pivots_dev(fisdf_ctx* c, const cplx* X2, double scale, int ng0
       FISDF_TRY(devbuf_get(c->ws_ypiv, sizeof(int) * (size_t)nip_max, &pp));
       piv = (int*)pp;
       progress = c->ys_dev;
-      FISDF_HIP(hipMemsetAsync(c->ys_dev, 0, 2 * sizeof(int), c->stream));
+      FISDF_HIP(hipMemsetAsync(c->ys_dev, 0, 3 * sizeof(int), c->stream));
       // the y stream starts from here, beside the kernel (not after it)
       FISDF_HIP(hipEventRecord(c->ev_ysfork, c->stream));
     }
@@ -1498,10 +1519,20 @@ static bool x4_dft_enabled() {
   return on;
 }
 
+static int build_x4_on(fisdf_ctx* c, hipStream_t st, fisdf_ctx::DevBuf* wsb, const void* Xv,
+                       int nip, int nao, const int kmesh[3], const double a[9], void* x4v);
+
 int fisdf_build_x4(fisdf_ctx* c, const void* Xv, int nip, int nao, const int kmesh[3],
                    const double a[9], void* x4v) {
   FISDF_TRY(device_guard(c));
-  StageTimer tm(c, FISDF_ST_X4);
+  return build_x4_on(c, c->stream, nullptr, Xv, nip, nao, kmesh, a, x4v);
+}
+
+// x4 on stream st; wsb (optional): the x2_k workspace of the register path from this grow-only
+// buffer instead of the arena (whose users are ordered on c->stream only)
+static int build_x4_on(fisdf_ctx* c, hipStream_t st, fisdf_ctx::DevBuf* wsb, const void* Xv,
+                       int nip, int nao, const int kmesh[3], const double a[9], void* x4v) {
+  StageTimer tm(c, FISDF_ST_X4, st);
   const int nk = kmesh[0] * kmesh[1] * kmesh[2];
   const cplx* phase;
   FISDF_TRY(get_phase(c, kmesh, a, &phase));
@@ -1510,7 +1541,7 @@ int fisdf_build_x4(fisdf_ctx* c, const void* Xv, int nip, int nao, const int kme
   if (nk == 1) {
     // Gamma only: Phi = 1, so x2_s = x2_k and x4 = x2_s^2 (:45) straight from the x2 GEMM's
     // epilogue with the reality monitor of :43 (the two Phi GEMMs would run with M = 1)
-    FISDF_TRY(zgemm(c->stream, OP_R, OP_T, nip, nip, nao, ONE, X, nao, 0, X, nao, 0, ZERO,
+    FISDF_TRY(zgemm(st, OP_R, OP_T, nip, nip, nao, ONE, X, nao, 0, X, nao, 0, ZERO,
                     (cplx*)x4v, nip, 0, 1, 1, nullptr, EPI_CSQUARE, c->maximag + 0));
     return 0;
   }
@@ -1522,14 +1553,17 @@ int fisdf_build_x4(fisdf_ctx* c, const void* Xv, int nip, int nao, const int kme
     const bool half = c->time_reversal;
     const int nks = half ? kmesh_half_count(kmesh) : nk;
     void* base;
-    FISDF_TRY(arena_get(c, sizeof(cplx) * (size_t)nks * nn, &base));
+    if (wsb)
+      FISDF_TRY(devbuf_get(*wsb, sizeof(cplx) * (size_t)nks * nn, &base));
+    else
+      FISDF_TRY(arena_get(c, sizeof(cplx) * (size_t)nks * nn, &base));
     cplx* X2k = (cplx*)base;
     std::vector<int> runs = {0, nk};
     if (half) FISDF_TRY(kmesh_rep_runs(kmesh, &runs));
     // x2_k = X_k^* X_k^T  (:38), one batched GEMM per run of stored k
     for (size_t r = 0, slot = 0; r < runs.size(); r += 2) {
       const int k0 = runs[r], nb = runs[r + 1] - runs[r];
-      FISDF_TRY(zgemm(c->stream, OP_R, OP_T, nip, nip, nao, ONE, X + (long)k0 * nip * nao, nao,
+      FISDF_TRY(zgemm(st, OP_R, OP_T, nip, nip, nao, ONE, X + (long)k0 * nip * nao, nao,
                       (long)nip * nao, X + (long)k0 * nip * nao, nao, (long)nip * nao, ZERO,
                       X2k + (long)slot * nn, nip, nn, nb));
       slot += nb;
@@ -1538,10 +1572,11 @@ int fisdf_build_x4(fisdf_ctx* c, const void* Xv, int nip, int nao, const int kme
     // x4_k = Phi^H x4_s (:46) for every k
     std::vector<int> all(nk);
     for (int q = 0; q < nk; ++q) all[q] = q;
-    FISDF_TRY(kmesh_y(c->stream, X2k, nn, kmesh, all.data(), nullptr, nk, nip, (cplx*)x4v, nn, nip,
+    FISDF_TRY(kmesh_y(st, X2k, nn, kmesh, all.data(), nullptr, nk, nip, (cplx*)x4v, nn, nip,
                       0, half, c->maximag + 0, true));
     return 0;
   }
+  FISDF_CHECK(st == c->stream, "build_x4: the dense path runs on the context stream only");
   Carver cv;
   size_t o1 = cv.take(sizeof(cplx) * nk * nn);
   size_t o2 = cv.take(sizeof(cplx) * nk * nn);
@@ -1550,14 +1585,14 @@ int fisdf_build_x4(fisdf_ctx* c, const void* Xv, int nip, int nao, const int kme
   cplx* X2k = (cplx*)((char*)base + o1);
   cplx* X2s = (cplx*)((char*)base + o2);
   // x2_k = X_k^* X_k^T  (:38)
-  FISDF_TRY(zgemm(c->stream, OP_R, OP_T, nip, nip, nao, ONE, X, nao, (long)nip * nao, X, nao,
+  FISDF_TRY(zgemm(st, OP_R, OP_T, nip, nip, nao, ONE, X, nao, (long)nip * nao, X, nao,
                   (long)nip * nao, ZERO, X2k, nip, nn, nk));
   // x2_s = Phi x2_k  (:41), must be real (:43), squared in the GEMM's epilogue:
   // x4_s = x2_s * x2_s (:45), recording max|Im x2_s|
-  FISDF_TRY(zgemm(c->stream, OP_N, OP_N, nk, nn, nk, ONE, phase, nk, 0, X2k, nn, 0, ZERO, X2s, nn,
+  FISDF_TRY(zgemm(st, OP_N, OP_N, nk, nn, nk, ONE, phase, nk, 0, X2k, nn, 0, ZERO, X2s, nn,
                   0, 1, 1, nullptr, EPI_CSQUARE, c->maximag + 0));
   // x4_k = Phi^H x4_s (:46)
-  FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nk, nn, nk, ONE, phase, nk, 0, X2s, nn, 0, ZERO,
+  FISDF_TRY(zgemm(st, OP_C, OP_N, nk, nn, nk, ONE, phase, nk, 0, X2s, nn, 0, ZERO,
                   (cplx*)x4v, nn, 0, 1));
   return 0;
 }
@@ -3293,7 +3328,9 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
                     comm->allreduce_f64 && comm->broadcast,
                 "build_sharded: incomplete fisdf_comm");
   // a k-shard's 1/N-grid y build is short, so its factor chain runs at the greatest priority
-  FISDF_TRY(fisdf_set_factor_priority(c, NR > 1 ? 1 : 0));
+  // FISDF_FACTOR_PRIO=0/1 (A/B) overrides: 1-GPU least, k-shard greatest
+  const char* fpe = getenv("FISDF_FACTOR_PRIO");
+  FISDF_TRY(fisdf_set_factor_priority(c, fpe ? (fpe[0] == '1' ? 1 : 0) : (NR > 1 ? 1 : 0)));
   // time reversal (X_{-k} = conj(X_k), real AOs): the selection Gram, x2_k (x4) and fx_k (y)
   // are formed for the representatives k <= -k only.  The inputs are checked on the side
   // stream beside the selection; a violation (complex basis, shifted k-mesh) is found when the
@@ -3398,7 +3435,17 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
   if (!X) FISDF_TRY(build_alloc(c, BR_X, sizeof(cplx) * (size_t)nk * nip * nao, &X));
   FISDF_TRY(fisdf_gather_points(c, x0, nk, ng0, nao, perm.data(), nip, X));        // :388
   if (!x4) FISDF_TRY(build_alloc(c, BR_X4, sizeof(cplx) * (size_t)nk * nn, &x4));
-  FISDF_TRY(fisdf_build_x4(c, X, nip, nao, kmesh, a, x4));                         // :38-48
+  // FISDF_X4_SIDE=1 (experiment, read per build): with y streamed, x4 on the side stream at the
+  // head of the factor chain it feeds.  Beside the streamed y its 0.2 ms DFT kernel stretches to
+  // 2.6 ms on either stream and the chain after it to 4 ms; measured +0.3 ms/step on the side
+  // stream, and no better at the greatest priority (profiles/r06/r06_x4side)
+  const char* x4e = getenv("FISDF_X4_SIDE");
+  const bool x4_side = !comm && (x4e && x4e[0] == '1') && c->ys.enqueued && !c->ys.stale && tr &&
+                       nip == c->ys.nip;
+  if (!x4_side) {
+    FISDF_TRY(fisdf_build_x4(c, X, nip, nao, kmesh, a, x4));                       // :38-48
+    FISDF_TRY(ystream_open_gate(c, c->stream));
+  }
   std::vector<int> qs, partner;
   std::vector<double> wt;
   tr_classes(kmesh, tr, qs, partner, wt);
@@ -3430,9 +3477,15 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
     FISDF_TRY(build_return(c, yT_pre));
     yT_pre = nullptr;
   }
+  FISDF_CHECK(!x4_side || y_streamed, "build: x4 on the side stream without the streamed y");
   if (!comm) {
     // the factorisation (replaces zgelsy's QRCP, :108) on the side stream, overlapped with y
     FISDF_TRY(fisdf_factor_x4_mark(c));
+    if (x4_side) {  // X gathered (ev_x4) -> x4 -> the factor chain, all on the side stream
+      FISDF_HIP(hipStreamWaitEvent(c->side, c->ev_x4, 0));
+      FISDF_TRY(build_x4_on(c, c->side, &c->ws_x4, X, nip, nao, kmesh, a, x4));  // :38-48
+      FISDF_TRY(ystream_open_gate(c, c->side));
+    }
     void* yT = yT_pre;
     if (!yT) FISDF_TRY(build_alloc(c, BR_Y, sizeof(cplx) * (size_t)nq * nip * ngrid, &yT));
     // the self-conjugate q's y real (half their y writes and FFT reads); FISDF_Y_REAL=0: off
