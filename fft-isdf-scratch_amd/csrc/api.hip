@@ -144,6 +144,8 @@ struct fisdf_ctx {
   std::vector<hipStream_t> pad;  // FISDF_PAD_QUEUES (ensure_side)
   void* pad_buf = nullptr;
   hipEvent_t ev_x4 = nullptr, ev_fac = nullptr, ev_chol = nullptr;
+  hipEvent_t ev_fac_early = nullptr;  // the first f_early slots' operators (factor_finish)
+  int f_early = 0;
   bool f_fac_unjoined = false;  // ev_fac not yet waited on by the main stream (fit lanes do)
   bool f_pending = false;
   bool x4_marked = false;  // fisdf_factor_x4_mark recorded ev_x4 for the next factor_x4_async
@@ -821,6 +823,7 @@ int fisdf_destroy(fisdf_ctx* c) {
     (void)hipStreamDestroy(c->side);
     (void)hipEventDestroy(c->ev_x4);
     (void)hipEventDestroy(c->ev_fac);
+    (void)hipEventDestroy(c->ev_fac_early);
     (void)hipEventDestroy(c->ev_chol);
   }
   if (c->ev_fork) {
@@ -1732,16 +1735,39 @@ int factor_finish(fisdf_ctx* c, hipStream_t s, const int* rank_dev_src, bool nee
   // starts its FFTs while the operators below are still being built (it waits on ev_fac
   // per lane before its first TRSM)
   FISDF_HIP(hipEventRecord(c->ev_chol, s));
-  FISDF_TRY(gather_lp(s, c->f_L, nip, nip, c->f_piv, c->f_rank_dev, nip, c->f_Lp, nk));
-  if (need_linv)
-    FISDF_TRY(trinv_blocks(s, c->f_Lp, nip, nip, nn, nb, (long)nblk * nb * nb, c->f_Linv, nk));
-  FISDF_TRY(build_trsm_q(s, c->f_Lp, nip, nn, c->f_Q, nk, GEMM_FULL));
-  // L^{-1} by the same block-row substitution applied to the identity (the fit then applies it
-  // as one lower-triangular GEMM over the grid; J/K within 2-3x of the TRSM's rounding,
-  // tests/experiments/explicit_tri_inverse.py)
-  FISDF_TRY(set_identity(s, c->f_Li, nip, nk));
-  FISDF_TRY(trsm_merged_batched(s, c->f_Q, nn, nip, c->f_Li, nip, nn, nip, nk, true, c->f_ksw,
-                                 c->f_ksw_elems));
+  // the operators of slots [z0, z0 + nz): every kernel below works per slot (strides from the
+  // batch index; split-K from the block row's shape only), so a slot's operators do not depend on
+  // which slots share the launch
+  const long sLi = (long)nblk * nb * nb;
+  auto operators = [&](int z0, int nz) -> int {
+    if (nz <= 0) return 0;
+    FISDF_TRY(gather_lp(s, c->f_L + z0 * nn, nip, nip, c->f_piv + (long)z0 * nip,
+                        c->f_rank_dev + z0, nip, c->f_Lp + z0 * nn, nz));
+    if (need_linv)
+      FISDF_TRY(trinv_blocks(s, c->f_Lp + z0 * nn, nip, nip, nn, nb, sLi, c->f_Linv + z0 * sLi,
+                             nz));
+    FISDF_TRY(build_trsm_q(s, c->f_Lp + z0 * nn, nip, nn, c->f_Q + z0 * nn, nz, GEMM_FULL));
+    // L^{-1} by the same block-row substitution applied to the identity (the fit then applies it
+    // as one lower-triangular GEMM over the grid; J/K within 2-3x of the TRSM's rounding,
+    // tests/experiments/explicit_tri_inverse.py)
+    FISDF_TRY(set_identity(s, c->f_Li + z0 * nn, nip, nz));
+    FISDF_TRY(trsm_merged_batched(s, c->f_Q + z0 * nn, nn, nip, c->f_Li + z0 * nn, nip, nn, nip,
+                                   nz, true, c->f_ksw, c->f_ksw_elems));
+    return 0;
+  };
+  // the first fitted slots' operators first (ev_fac_early): their lanes start the fit while the
+  // rest are still being built.  FISDF_FAC_EARLY (slots, read per call; 0 off)
+  const int early = [&] {
+    const char* e = getenv("FISDF_FAC_EARLY");
+    const int v = e ? atoi(e) : 2;
+    return (v > 0 && v < nk) ? v : 0;
+  }();
+  c->f_early = early;
+  if (early) {
+    FISDF_TRY(operators(0, early));
+    FISDF_HIP(hipEventRecord(c->ev_fac_early, s));
+  }
+  FISDF_TRY(operators(early, nk - early));
   return 0;
 }
 
@@ -1848,6 +1874,7 @@ static int ensure_side(fisdf_ctx* c) {
   if (!c->ev_x4) {
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_x4, hipEventDisableTiming));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_fac, hipEventDisableTiming));
+    FISDF_HIP(hipEventCreateWithFlags(&c->ev_fac_early, hipEventDisableTiming));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_chol, hipEventDisableTiming));
   }
   return 0;
@@ -2544,7 +2571,11 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     }
     cplx* Uq = U;  // where L^{-1} Yh lands
     const long ncol = ncols_of(lq);  // grid columns fitted (half for a self-conjugate q)
-    if (c->f_fac_unjoined) FISDF_HIP(hipStreamWaitEvent(st, c->ev_fac, 0));  // L^-1, Q, ...
+    // L^-1, Q, ...: the slots built first need only their own (ev_fac_early); a lane's later q
+    // wait for all of them
+    if (c->f_fac_unjoined)
+      FISDF_HIP(hipStreamWaitEvent(
+          st, (sl < c->f_early && !cod_of(sl)) ? c->ev_fac_early : c->ev_fac, 0));
     {
       // U = L^{-1} Yh   (fit, factored order; (x4_q)_PP = L L^H): one GEMM (timed kernel-exact)
       // on a full-rank q and on a minimum-norm q; the basic solution of a rank-deficient q
