@@ -2417,6 +2417,16 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
   size_t oP[4] = {0, 0, 0, 0};
   if (unpack)
     for (int l = 0; l < (pipe ? 1 : NL); ++l) oP[l] = cv.take(sizeof(cplx) * (size_t)nip * ngrid);
+  // W_PP = L^-H G L^-1 (two upper-triangular nip^3 GEMMs per q) split over K: 100 output tiles
+  // of 64 x 64 at C3 leave most CUs idle for ~180 us per GEMM, in every lane, for every q.  The
+  // split depends on nip only, the same in the lanes and in the batched tail (W_q bitwise equal
+  // between the 1-GPU and the k-sharded builds).  FISDF_WPP_KSPLIT (read per call; 1 = off)
+  const int wks = [&] {
+    const char* e = getenv("FISDF_WPP_KSPLIT");
+    const int v = e ? atoi(e) : 4;
+    return (nip >= 256 && v > 1) ? std::min(v, 16) : 1;
+  }();
+  const size_t oWk = wks > 1 ? cv.take(sizeof(cplx) * (size_t)NL * wks * rr) : 0;
   size_t oG = cv.take(sizeof(cplx) * nq * rr);
   size_t oT = cv.take(sizeof(cplx) * nq * rr);
   size_t oS = cv.take(sizeof(cplx) * nq * rr);
@@ -2644,10 +2654,11 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
     if (lane_wpp) {  // W_PP = L^-H G L^-1 of this q (S = L^-H G, W_PP = L^-H S^H), scattered
       StageTimer tm(c, FISDF_ST_SMALL, st);
       const cplx* Lf = c->f_Li + (long)sl * nn;
+      cplx* wk = wks > 1 ? (cplx*)(b + oWk) + (long)ln * wks * rr : nullptr;
       FISDF_TRY(zgemm(st, OP_C, OP_N, nip, nip, nip, ONE, Lf, nip, 0, G + lq * rr, rmax, 0, ZERO,
-                      S + lq * rr, rmax, 0, 1, 1, nullptr, EPI_NONE, nullptr, GEMM_A_UPPER));
+                      S + lq * rr, rmax, 0, 1, wks, wk, EPI_NONE, nullptr, GEMM_A_UPPER));
       FISDF_TRY(zgemm(st, OP_C, OP_C, nip, nip, nip, ONE, Lf, nip, 0, S + lq * rr, rmax, 0, ZERO,
-                      T + lq * rr, rmax, 0, 1, 1, nullptr, EPI_NONE, nullptr, GEMM_A_UPPER));
+                      T + lq * rr, rmax, 0, 1, wks, wk, EPI_NONE, nullptr, GEMM_A_UPPER));
       FISDF_TRY(scatter_w(st, T + lq * rr, rmax, rr, rmax, c->f_piv + (long)sl * nip,
                           c->f_rank_dev + sl, Wq + lq * nn, nip, 1));
     }
@@ -2680,10 +2691,24 @@ int fisdf_fit_coulomb_qs(fisdf_ctx* c, const int* h_qs, int nq, const void* yTv,
       // M-tile starts its K loop at its own row: half the flops of dense GEMMs):
       //   S = L^{-H} G,  W_PP = L^{-H} S^H  (= L^{-H} G L^{-1}, G Hermitian)
       const cplx* Lf = c->f_Li + (long)s0 * nn;
-      FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nip, nip, nip, ONE, Lf, nip, nn, G, rmax, rr, ZERO,
-                      S, rmax, rr, nq, 1, nullptr, EPI_NONE, nullptr, GEMM_A_UPPER));
-      FISDF_TRY(zgemm(c->stream, OP_C, OP_C, nip, nip, nip, ONE, Lf, nip, nn, S, rmax, rr, ZERO,
-                      T, rmax, rr, nq, 1, nullptr, EPI_NONE, nullptr, GEMM_A_UPPER));
+      if (wks > 1) {
+        // the lanes' split workspace, NL q at a time (per-q arithmetic as in the lanes)
+        cplx* wk = (cplx*)(b + oWk);
+        for (int z0 = 0; z0 < nq; z0 += NL) {
+          const int nz = std::min(NL, nq - z0);
+          FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nip, nip, nip, ONE, Lf + (long)z0 * nn, nip, nn,
+                          G + z0 * rr, rmax, rr, ZERO, S + z0 * rr, rmax, rr, nz, wks, wk, EPI_NONE,
+                          nullptr, GEMM_A_UPPER));
+          FISDF_TRY(zgemm(c->stream, OP_C, OP_C, nip, nip, nip, ONE, Lf + (long)z0 * nn, nip, nn,
+                          S + z0 * rr, rmax, rr, ZERO, T + z0 * rr, rmax, rr, nz, wks, wk, EPI_NONE,
+                          nullptr, GEMM_A_UPPER));
+        }
+      } else {
+        FISDF_TRY(zgemm(c->stream, OP_C, OP_N, nip, nip, nip, ONE, Lf, nip, nn, G, rmax, rr, ZERO,
+                        S, rmax, rr, nq, 1, nullptr, EPI_NONE, nullptr, GEMM_A_UPPER));
+        FISDF_TRY(zgemm(c->stream, OP_C, OP_C, nip, nip, nip, ONE, Lf, nip, nn, S, rmax, rr, ZERO,
+                        T, rmax, rr, nq, 1, nullptr, EPI_NONE, nullptr, GEMM_A_UPPER));
+      }
     } else {
       FISDF_TRY(trsm_blocked(c->stream, 0, Lp0, nip, nn, rmax, Li0, sLi, nb, G, rmax, rr,
                              T, rmax, rr, rmax, nq));

@@ -714,8 +714,10 @@ int zgemm(hipStream_t s, int opA, int opB, int M, int N, int K, cplx alpha, cons
   FISDF_CHECK(mode == GEMM_FULL || mode == GEMM_A_UPPER ||
                   (opB == OP_N && (opA == OP_N || opA == OP_C)),
               "zgemm: real modes are implemented for (N,N) and (C,N) only");
-  FISDF_CHECK(mode != GEMM_A_UPPER || (opA == OP_C && ksplit <= 1),
-              "zgemm: GEMM_A_UPPER is implemented for op(A) = A^H without split-K");
+  // GEMM_A_UPPER with split-K: a split whose K range lies wholly left of an M-tile's first row
+  // runs no K-step and writes a zero partial (the reduce sums every split)
+  FISDF_CHECK(mode != GEMM_A_UPPER || opA == OP_C,
+              "zgemm: GEMM_A_UPPER is implemented for op(A) = A^H");
   FISDF_CHECK(!(mode & GEMM_A_LOWER) || (opA == OP_N && opB == OP_N && !(mode & GEMM_RE_ONLY)),
               "zgemm: GEMM_A_LOWER is implemented for (N,N), optionally with GEMM_A_REAL");
   if (M == 0 || N == 0 || batch == 0) return 0;
