@@ -205,11 +205,12 @@ struct fisdf_ctx {
   std::map<int, std::pair<void*, size_t>> owned;  // role -> library-owned buffer
   std::vector<void*> lent;                        // buffers from alloc_fn not yet returned
   // The y build streamed behind the selection (build_impl, FISDF_Y_STREAM): while the
-  // cooperative selection runs on `stream`, aux[0] forms y in blocks of pivots as the kernel
-  // publishes them (pchol_select_coop's progress word).  ys_dev: {progress, spin error} (device
-  // ints); ws_ypiv: the pivots, context-owned so that no later arena user overwrites them under
-  // the y stream; ws_ystream: XT / FT of the fused kernel.  `ys` is the build's request, armed
-  // around the first selection only; enqueued: the y stream received the work.
+  // cooperative selection runs on `stream`, aux[2] and aux[0] form y in blocks of pivots as the
+  // kernel publishes them (pchol_select_coop's progress word).  ys_dev: {progress, spin error,
+  // gate} (device ints); ws_ypiv: the pivots, context-owned so that no later arena user
+  // overwrites them under the y stream; ws_ystream: XT / FT of the fused kernel.  `ys` is the
+  // build's request, armed around the first selection only; enqueued: the y stream received the
+  // work.
   int* ys_dev = nullptr;
   int* ys_err_pinned = nullptr;
   hipEvent_t ev_yerr = nullptr;
@@ -1118,14 +1119,10 @@ int fisdf_tri_inverse(fisdf_ctx* c, const void* L, int n, int batch, void* Linv)
 }
 
 // ---- A1 ---------------------------------------------------------------------
-// The selection's pivots on the device: the cooperative kernel, the blocked or the generic pivoted
-// Cholesky (in that order of preference), then ONE pinned read-back of {error flag, rank, pivots}
-// and one stream synchronisation (round 2 synchronised twice through pageable copies); a
-// cooperative run that reports a stalled step is redone on the non-cooperative paths.
-// the streamed y build's work on aux[0], enqueued right after the selection kernel (so it never
-// precedes it on any queue): the fused y kernel block by block, each block's XT rows waiting on
-// the kernel's progress word (y_fused_stream).  Ordered after everything on `stream` before the
-// selection (the previous build's readers of the y buffer and workspaces included).
+// The streamed y build's work on aux[2] and aux[0], enqueued right after the selection kernel (so
+// it never precedes it on any queue): the fused y kernel block by block, each block's XT rows
+// waiting on the kernel's progress word (y_fused_stream).  Ordered after everything on `stream`
+// before the selection (the previous build's readers of the y buffer and workspaces included).
 static int ensure_side(fisdf_ctx* c);
 
 static int ystream_enqueue(fisdf_ctx* c, const int* piv) {
@@ -1194,7 +1191,7 @@ static int ystream_enqueue(fisdf_ctx* c, const int* piv) {
 
 // after the selection: whether yT holds the y build of the selected points (the selection gave
 // the cap's points, its first pass did not fail, the q-list is the armed one); the y stream's
-// spin-error flag is queued for read-back (ev_yerr).  The caller joins aux[0] (ystream_join).
+// spin-error flag is queued for read-back (ev_yerr).  The caller joins the y stream (ystream_join).
 static bool ystream_valid(fisdf_ctx* c, int nip, const int* qs, int nq) {
   const fisdf_ctx::YStream& Y = c->ys;
   return Y.enqueued && !Y.stale && nip == Y.nip && (int)Y.qs.size() == nq &&
@@ -1270,6 +1267,10 @@ static int ystream_arm(fisdf_ctx* c, const void* x0, int ng0, const void* f, lon
   return 0;
 }
 
+// The selection's pivots on the device: the cooperative kernel, the blocked or the generic pivoted
+// Cholesky (in that order of preference), then ONE pinned read-back of {error flag, rank, pivots}
+// and one stream synchronisation (round 2 synchronised twice through pageable copies); a
+// cooperative run that reports a stalled step is redone on the non-cooperative paths.
 static int select_pivots_dev(fisdf_ctx* c, const cplx* X2, double scale, int ng0, int nip_max,
                              double tol, cplx* X4, int* piv, int* rank, cplx* L, double* d,
                              int* flags, double* w, int* h_perm, int* h_rank) {
