@@ -1515,12 +1515,9 @@ int fisdf_gather_points(fisdf_ctx* c, const void* x0, int nk, int ng0, int nao, 
 
 // ---- A2 ---------------------------------------------------------------------
 // FISDF_X4_DFT=0: the x4 build through the two dense Phi GEMMs (A/B on one box)
-static bool x4_dft_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("FISDF_X4_DFT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+static bool x4_dft_enabled() {  // read per call (A/B in one process)
+  const char* e = getenv("FISDF_X4_DFT");
+  return !(e && e[0] == '0');
 }
 
 static int build_x4_on(fisdf_ctx* c, hipStream_t st, fisdf_ctx::DevBuf* wsb, const void* Xv,
