@@ -149,8 +149,9 @@ int chol_unpivoted(hipStream_t s, cplx* W, int n, int batch, double tol_rel, int
 // on other streams can start on the first pivots while the selection runs (the streamed y
 // build, api.hip); *publishes tells whether the kernel that ran does so (the other paths
 // publish nothing: their consumers see only the kSelDone the caller writes after the kernel)
-// whether the selection kernels go through hipLaunchCooperativeKernel (FISDF_COOP_LAUNCH=1;
-// default: a plain launch after the occupancy check, pchol.hip launch_coresident)
+// whether the selection kernels go through hipLaunchCooperativeKernel (FISDF_COOP_LAUNCH=0/1;
+// default: cooperative on HIP runtimes >= 7.2, else a plain launch after the occupancy check,
+// pchol.hip coop_launch_enabled / launch_coresident)
 bool coop_launch_enabled();
 constexpr int kSelPublish = 16;
 constexpr int kSelDone = 1 << 30;
