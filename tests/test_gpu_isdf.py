@@ -616,6 +616,39 @@ def test_streamed_y_matches(name):
     assert b[5] == (fused and coop and b[6] == cap)
 
 
+@pytest.mark.parametrize("name", ["toy222", "toy331_fr"])
+@pytest.mark.parametrize("rows,two,gate", [("16", "1", None), ("48", "0", None),
+                                           ("256", "1", None), ("16", "1", "1")])
+def test_streamed_y_variants(name, rows, two, gate):
+    """The streamed y's schedule does not change its result: pivot blocks of 16 / 48 / 256 rows
+    (FISDF_Y_STREAM_ROWS), one stream or two (FISDF_Y_STREAM_2S), and the blocks from the second
+    on held until x4 is done (FISDF_Y_GATE_FROM=1, the gate opened by the build's join) all give
+    the unstreamed build's W_q, W_s and J/K bit for bit."""
+    import os
+    env = {"FISDF_Y_STREAM_ROWS": rows, "FISDF_Y_STREAM_2S": two}
+    if gate is not None:
+        env["FISDF_Y_GATE_FROM"] = gate
+    res = {}
+    for on in ("0", "1"):
+        os.environ["FISDF_Y_STREAM"] = on
+        os.environ.update(env)
+        try:
+            df, o, dm = make_df(name, inject=False)
+            df.build()
+            vj, vk = df.get_jk(dm)
+            st = df._dev_state
+            res[on] = (st["Wq"].cpu().numpy(), st["Ws"].cpu().numpy(), vj, vk, df.y_streamed,
+                       df.nip)
+        finally:
+            for k in ["FISDF_Y_STREAM", *env]:
+                os.environ.pop(k, None)
+    a, b = res["0"], res["1"]
+    print(f"\n{name} rows {rows} 2s {two} gate {gate}: nip {b[5]}, streamed {b[4]}")
+    assert b[4] and not a[4]
+    for i, what in ((0, "W_q"), (1, "W_s"), (2, "J"), (3, "K")):
+        assert np.array_equal(a[i], b[i]), what
+
+
 @pytest.mark.parametrize("name", ["toy222", "toy331_fr", "toy333_fr", "nio_small"])
 def test_get_k_register_transform(name):
     """get_k's k-mesh transform pair (rho_s = Phi rho_k, V_s = W_s Re(rho_s), V_k = Phi^T V_s,
