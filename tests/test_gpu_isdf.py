@@ -649,6 +649,52 @@ def test_streamed_y_variants(name, rows, two, gate):
         assert np.array_equal(a[i], b[i]), what
 
 
+def _build_env(name, env, inject=False):
+    import os
+    os.environ.update(env)
+    try:
+        df, o, dm = make_df(name, inject=inject)
+        df.build()
+        vj, vk = df.get_jk(dm)
+        st = df._dev_state
+        return (st["Wq"].cpu().numpy(), st["Ws"].cpu().numpy(), vj, vk), o, df
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+
+
+@pytest.mark.parametrize("name", ["toy222", "toy331_fr", "nio_small"])
+@pytest.mark.parametrize("env", [{"FISDF_FAC_EARLY": "0"}, {"FISDF_FAC_EARLY": "5"},
+                                 {"FISDF_FACTOR_PRIO": "1"}, {"FISDF_X4_SIDE": "1"}],
+                         ids=["early0", "early5", "prio1", "x4side"])
+def test_schedule_switches_bitwise(name, env):
+    """Round-6 scheduling switches move work between streams or reorder independent launches
+    only: the first fitted slots' factor operators built before the rest (FISDF_FAC_EARLY, 0 =
+    all at once), the factor chain's stream priority (FISDF_FACTOR_PRIO) and x4 on the side
+    stream beside the streamed y (FISDF_X4_SIDE) leave W_q, W_s and J/K bit for bit."""
+    ref, _, _ = _build_env(name, {})
+    got, _, _ = _build_env(name, env)
+    for i, what in enumerate(("W_q", "W_s", "J", "K")):
+        assert np.array_equal(ref[i], got[i]), what
+
+
+@pytest.mark.parametrize("name", ["nio_small", "si_small"])
+def test_wpp_split_k(name):
+    """W_PP = L^-H G L^-1's two upper-triangular GEMMs split 4-way over K (the default from
+    256 points) against the unsplit products (FISDF_WPP_KSPLIT=1): W_q to rounding, J/K vs the
+    oracle within the north-star bar both ways.  (Full-rank cases: a rank-deficient q takes the
+    blocked back-substitutions instead, where the switch has no effect.)"""
+    a, o, df = _build_env(name, {"FISDF_WPP_KSPLIT": "1"}, inject=True)
+    b, _, _ = _build_env(name, {}, inject=True)
+    assert df.nip >= 256 and min(df.ranks) == df.nip, "case does not split"
+    dw = abs(a[0] - b[0]).max() / abs(a[0]).max()
+    e = [max(abs(r[2] - o["vj"]).max(), abs(r[3] - o["vk"]).max()) for r in (a, b)]
+    print(f"\n{name}: nip {df.nip}: rel |dW_q| split vs unsplit {dw:.1e}; |dJK| vs oracle "
+          f"unsplit {e[0]:.2e} split {e[1]:.2e}")
+    assert 0 < dw < 1e-12       # the split ran (another summation order), to rounding
+    assert max(e) < JK_TOL
+
+
 @pytest.mark.parametrize("name", ["toy222", "toy331_fr", "toy333_fr", "nio_small"])
 def test_get_k_register_transform(name):
     """get_k's k-mesh transform pair (rho_s = Phi rho_k, V_s = W_s Re(rho_s), V_k = Phi^T V_s,
