@@ -206,8 +206,8 @@ struct fisdf_ctx {
   std::vector<void*> lent;                        // buffers from alloc_fn not yet returned
   // The y build streamed behind the selection (build_impl, FISDF_Y_STREAM): while the
   // cooperative selection runs on `stream`, aux[2] and aux[0] form y in blocks of pivots as the
-  // kernel publishes them (pchol_select_coop's progress word).  ys_dev: {progress, spin error,
-  // gate} (device ints); ws_ypiv: the pivots, context-owned so that no later arena user
+  // kernel publishes them (pchol_select_coop's progress word).  ys_dev: {progress, spin error}
+  // (device ints); ws_ypiv: the pivots, context-owned so that no later arena user
   // overwrites them under the y stream; ws_ystream: XT / FT of the fused kernel.  `ys` is the
   // build's request, armed around the first selection only; enqueued: the y stream received the
   // work.
@@ -220,7 +220,6 @@ struct fisdf_ctx {
   struct YStream {
     bool armed = false, enqueued = false;
     bool stale = false;  // the kernel it followed failed (a stalled step): its pivots were redone
-    bool gated = false;  // later blocks wait for the gate (ys_dev[2]): someone must open it
     int aux = 2;         // the aux stream it runs on
     const cplx* x0 = nullptr;
     const cplx* f = nullptr;
@@ -1159,24 +1158,18 @@ static int ystream_enqueue(fisdf_ctx* c, const int* piv) {
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_ys2[0], hipEventDisableTiming));
     FISDF_HIP(hipEventCreateWithFlags(&c->ev_ys2[1], hipEventDisableTiming));
   }
-  // FISDF_Y_GATE_FROM=b (experiment, read per build; default -1, off): the blocks from b on also
-  // wait for the gate (ys_dev[2]), which the build opens once x4 is done, so they leave the CU
-  // slots to x4 and the factor chain when the selection ends.  x4 then takes 1.3 ms instead of
-  // 3.0, but the chain after it stretches from 4.1 to 5.2 ms beside the released blocks and the
-  // step is 0.5-1 ms slower (profiles/r06/r06_gate)
-  const int gate_from = [] {
-    const char* e = getenv("FISDF_Y_GATE_FROM");
-    return e ? atoi(e) : -1;
-  }();
-  Y.gated = gate_from >= 0;
+  // (a round-6 experiment held the blocks after the first until x4 was done, on a device flag the
+  // build set: x4 1.3 ms instead of 3.0, but the factor chain after it 5.2 instead of 4.1 ms and
+  // the step 0.5-1 ms slower, profiles/r06/r06_gate.  Removed: a host-side device synchronisation
+  // before the flag was set — a workspace growth, a hipFree — waited for the held blocks until
+  // their bounded wait expired)
   bool handled = false;
   {
     StageTimer tm(c, FISDF_ST_Y, ys);
     FISDF_TRY(y_fused_stream(ys, Y.x0, Y.ng0, Y.nao, piv, c->ys_dev, c->ys_dev + 1, Y.nip, Y.rows,
                              Y.f, Y.fks, (int)Y.m, Y.kmesh, Y.qs.data(), nq, Y.yT,
                              (long)Y.nip * Y.m, Y.m, 0, (cplx*)wb, yw, Y.rmask, &handled,
-                             i2 >= 0 ? c->aux[i2] : nullptr, c->ev_ys2[0], c->ev_ys2[1],
-                             c->ys_dev + 2, gate_from));
+                             i2 >= 0 ? c->aux[i2] : nullptr, c->ev_ys2[0], c->ev_ys2[1]));
   }
   // aux[i2]'s work is ordered before aux[ia]'s last command: joined with it (buffer-return
   // bookkeeping, check_aux_joined)
@@ -1198,18 +1191,9 @@ static bool ystream_valid(fisdf_ctx* c, int nip, const int* qs, int nq) {
          std::equal(Y.qs.begin(), Y.qs.end(), qs);
 }
 
-// open the streamed y's gate on stream st (stream-ordered: after whatever st has enqueued)
-static int ystream_open_gate(fisdf_ctx* c, hipStream_t st) {
-  if (!c->ys.enqueued || !c->ys.gated) return 0;
-  FISDF_HIP(hipMemsetD32Async(c->ys_dev + 2, 1, 1, st));
-  c->ys.gated = false;
-  return 0;
-}
-
 static int ystream_join(fisdf_ctx* c) {
   const int ia = c->ys.aux;
   if (!c->ys.enqueued || c->aux_joined[ia] == c->aux_use[ia]) return 0;
-  FISDF_TRY(ystream_open_gate(c, c->stream));  // nobody opened it: the join would wait forever
   FISDF_TRY(aux_join(c, ia));
   FISDF_HIP(hipMemcpyAsync(c->ys_err_pinned, c->ys_dev + 1, sizeof(int), hipMemcpyDeviceToHost,
                            c->stream));
@@ -1297,7 +1281,7 @@ static int select_pivots_dev(fisdf_ctx* c, const cplx* X2, double scale, int ng0
       FISDF_TRY(devbuf_get(c->ws_ypiv, sizeof(int) * (size_t)nip_max, &pp));
       piv = (int*)pp;
       progress = c->ys_dev;
-      FISDF_HIP(hipMemsetAsync(c->ys_dev, 0, 3 * sizeof(int), c->stream));
+      FISDF_HIP(hipMemsetAsync(c->ys_dev, 0, 2 * sizeof(int), c->stream));
       // the y stream starts from here, beside the kernel (not after it)
       FISDF_HIP(hipEventRecord(c->ev_ysfork, c->stream));
     }
@@ -3496,10 +3480,7 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
   const char* x4e = getenv("FISDF_X4_SIDE");
   const bool x4_side = !comm && (x4e && x4e[0] == '1') && c->ys.enqueued && !c->ys.stale && tr &&
                        nip == c->ys.nip;
-  if (!x4_side) {
-    FISDF_TRY(fisdf_build_x4(c, X, nip, nao, kmesh, a, x4));                       // :38-48
-    FISDF_TRY(ystream_open_gate(c, c->stream));
-  }
+  if (!x4_side) FISDF_TRY(fisdf_build_x4(c, X, nip, nao, kmesh, a, x4));           // :38-48
   std::vector<int> qs, partner;
   std::vector<double> wt;
   tr_classes(kmesh, tr, qs, partner, wt);
@@ -3538,7 +3519,6 @@ int build_impl(fisdf_ctx* c, const fisdf_comm* comm, const void* x0, int ng0, co
     if (x4_side) {  // X gathered (ev_x4) -> x4 -> the factor chain, all on the side stream
       FISDF_HIP(hipStreamWaitEvent(c->side, c->ev_x4, 0));
       FISDF_TRY(build_x4_on(c, c->side, &c->ws_x4, X, nip, nao, kmesh, a, x4));  // :38-48
-      FISDF_TRY(ystream_open_gate(c, c->side));
     }
     void* yT = yT_pre;
     if (!yT) FISDF_TRY(build_alloc(c, BR_Y, sizeof(cplx) * (size_t)nq * nip * ngrid, &yT));

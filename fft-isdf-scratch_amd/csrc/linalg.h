@@ -111,7 +111,7 @@ int y_fused_stream(hipStream_t s, const cplx* x0, int ng0, int nao, const int* p
                    int m, const int kmesh[3], const int* h_qs, int nq, cplx* yT, long qs, long Is,
                    long goff, cplx* work, size_t work_bytes, unsigned long long rmask,
                    bool* handled, hipStream_t s2 = nullptr, hipEvent_t ev_a = nullptr,
-                   hipEvent_t ev_b = nullptr, const int* gate = nullptr, int gate_from = -1);
+                   hipEvent_t ev_b = nullptr);
 int kmesh_rep_runs(const int kmesh[3], std::vector<int>* runs);
 // Bloch AO values (ao.hip): F (nimg, ng, nao) f64 workspace, scratch for the small tables;
 // nkb > 0: at the nkb band k-points h_kband (any k) instead of the k-mesh, F (nT, ng, nao)

@@ -703,15 +703,12 @@ __global__ __launch_bounds__(256) void yf_xt_stream_kernel(const cplx* __restric
                                                            const int* __restrict__ progress,
                                                            int lo, int hi, int nip, YfPlan plan,
                                                            cplx* __restrict__ XT,
-                                                           int* __restrict__ err,
-                                                           const int* __restrict__ gate) {
+                                                           int* __restrict__ err) {
   extern __shared__ cplx tile[];  // [64][nao + 1]
   __shared__ int s_p[64];
   if (threadIdx.x == 0) {
     long spins = 0;
-    // gate (nullable): also wait until another stream has opened it (nonzero)
-    while (__hip_atomic_load(progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hi ||
-           (gate && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)) {
+    while (__hip_atomic_load(progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hi) {
       __builtin_amdgcn_s_sleep(127);
       if (++spins > kXtSpinCap) {
         atomicExch(err, 1);
@@ -1722,8 +1719,7 @@ int y_fused_stream(hipStream_t s, const cplx* x0, int ng0, int nao, const int* p
                    const int* progress, int* err, int nip, int rows, const cplx* F, long fks,
                    int m, const int kmesh[3], const int* h_qs, int nq, cplx* yT, long qs, long Is,
                    long goff, cplx* work, size_t work_bytes, unsigned long long rmask,
-                   bool* handled, hipStream_t s2, hipEvent_t ev_a, hipEvent_t ev_b,
-                   const int* gate, int gate_from) {
+                   bool* handled, hipStream_t s2, hipEvent_t ev_a, hipEvent_t ev_b) {
   *handled = false;
   if (m <= 0 || nip <= 0) return 0;
   FISDF_CHECK(rows >= 16 && rows % 16 == 0 && rows <= 64 * 16, "y_fused_stream: bad row block");
@@ -1755,9 +1751,8 @@ int y_fused_stream(hipStream_t s, const cplx* x0, int ng0, int nao, const int* p
   for (int lo = 0, b = 0; lo < nip; lo += rows, ++b) {
     const int hi = std::min(nip, lo + rows);
     hipStream_t sb = (s2 && (b & 1)) ? s2 : s;
-    const int* gb = (gate && gate_from >= 0 && b >= gate_from) ? gate : nullptr;
     hipLaunchKernelGGL(yf_xt_stream_kernel, dim3((hi - lo + 63) / 64, nsl), dim3(256), tl, sb, x0,
-                       (long)ng0 * nao, ng0, nao, piv, progress, lo, hi, nip, plan, XT, err, gb);
+                       (long)ng0 * nao, ng0, nao, piv, progress, lo, hi, nip, plan, XT, err);
     FISDF_HIP(hipGetLastError());
     bool h = false;
     FISDF_TRY(yf_launch(sb, kmesh, XT, nip, nao, FT, m, lo / 16, (hi - lo + 15) / 16, plan, qmask,

@@ -617,17 +617,13 @@ def test_streamed_y_matches(name):
 
 
 @pytest.mark.parametrize("name", ["toy222", "toy331_fr"])
-@pytest.mark.parametrize("rows,two,gate", [("16", "1", None), ("48", "0", None),
-                                           ("256", "1", None), ("16", "1", "1")])
-def test_streamed_y_variants(name, rows, two, gate):
+@pytest.mark.parametrize("rows,two", [("16", "1"), ("48", "0"), ("256", "1")])
+def test_streamed_y_variants(name, rows, two):
     """The streamed y's schedule does not change its result: pivot blocks of 16 / 48 / 256 rows
-    (FISDF_Y_STREAM_ROWS), one stream or two (FISDF_Y_STREAM_2S), and the blocks from the second
-    on held until x4 is done (FISDF_Y_GATE_FROM=1, the gate opened by the build's join) all give
-    the unstreamed build's W_q, W_s and J/K bit for bit."""
+    (FISDF_Y_STREAM_ROWS) on one stream or two (FISDF_Y_STREAM_2S) give the unstreamed build's
+    W_q, W_s and J/K bit for bit."""
     import os
     env = {"FISDF_Y_STREAM_ROWS": rows, "FISDF_Y_STREAM_2S": two}
-    if gate is not None:
-        env["FISDF_Y_GATE_FROM"] = gate
     res = {}
     for on in ("0", "1"):
         os.environ["FISDF_Y_STREAM"] = on
@@ -643,7 +639,7 @@ def test_streamed_y_variants(name, rows, two, gate):
             for k in ["FISDF_Y_STREAM", *env]:
                 os.environ.pop(k, None)
     a, b = res["0"], res["1"]
-    print(f"\n{name} rows {rows} 2s {two} gate {gate}: nip {b[5]}, streamed {b[4]}")
+    print(f"\n{name} rows {rows} 2s {two}: nip {b[5]}, streamed {b[4]}")
     assert b[4] and not a[4]
     for i, what in ((0, "W_q"), (1, "W_s"), (2, "J"), (3, "K")):
         assert np.array_equal(a[i], b[i]), what
