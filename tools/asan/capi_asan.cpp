@@ -3,9 +3,11 @@
 // What a C caller does, twice over on one context: fisdf_create, fisdf_malloc / memcpy for every
 // buffer, fisdf_build (the reference's ISDF.build(), fftisdf.py:308-325), fisdf_build_get,
 // fisdf_get_jk (fftisdf.py:390-408), fisdf_build_release; then the error paths (get_jk before any
-// build, a bad device id) and teardown.  Every host-side buffer the library touches is checked by
+// build, a bad device id), a fisdf_group of 3 ranks on one device (threads, device-copy
+// collectives) and its failed-creation path, and teardown.  Every host-side buffer the library touches is checked by
 // the sanitizer; the second build must reproduce the first bit for bit.
 //   capi_asan CASE.bin OUT.bin      (the case file: tools/asan/check.py make)
+#include <algorithm>
 #include <complex>
 #include <cstdio>
 #include <cstdlib>
@@ -114,6 +116,62 @@ int main(int argc, char** argv) {
   if (fisdf_create(1 << 20, nullptr, &ctx3) == 0 || !strstr(fisdf_last_error(nullptr), "device id")) {
     fprintf(stderr, "a bad device id did not fail as documented\n");
     return 1;
+  }
+
+  // fisdf_group: 3 ranks on device 0 joined by device copies (one host thread per rank inside
+  // the library, fisdf_build_sharded on each): every rank's all-reduced J/K equal the 1-GPU J/K
+  // to rounding; then a group whose second device does not exist fails cleanly
+  {
+    const int n = 3, devs[3] = {0, 0, 0};
+    fisdf_group* g = nullptr;
+    CHECK(fisdf_group_create(n, devs, FISDF_GROUP_COPY, &g));
+    const void* x0s[3] = {d_x0, d_x0, d_x0};
+    const void* fs[3] = {d_f, d_f, d_f};
+    const void* ds[3] = {d_dms, d_dms, d_dms};
+    void *gvj[3], *gvk[3];
+    for (int r = 0; r < n; ++r) {
+      CHECK(fisdf_malloc(ctx, nd * sizeof(cplx), &gvj[r]));
+      CHECK(fisdf_malloc(ctx, nd * sizeof(cplx), &gvk[r]));
+    }
+    fisdf_build_opts o;
+    fisdf_build_opts_default(&o);
+    o.nip_max = h.nip_max;
+    int gnip = 0;
+    if (fisdf_group_build(g, x0s, h.ng0, fs, h.nao, h.kmesh, h.mesh, h.a, &o, &gnip) != 0 ||
+        fisdf_group_get_jk(g, ds, h.nset, 1, 1, gvj, gvk) != 0) {
+      fprintf(stderr, "group: %s\n", fisdf_group_last_error(g));
+      return 1;
+    }
+    if (gnip != (int)perm.size()) {
+      fprintf(stderr, "group: %d points against %zu\n", gnip, perm.size());
+      return 1;
+    }
+    double vmax = 0, dmax = 0;
+    for (size_t i = 0; i < nd; ++i) vmax = std::max(vmax, std::max(std::abs(vj[0][i]), std::abs(vk[0][i])));
+    std::vector<cplx> t(nd);
+    for (int r = 0; r < n; ++r) {
+      CHECK(fisdf_memcpy_dtoh(ctx, t.data(), gvj[r], nd * sizeof(cplx)));
+      for (size_t i = 0; i < nd; ++i) dmax = std::max(dmax, std::abs(t[i] - vj[0][i]));
+      CHECK(fisdf_memcpy_dtoh(ctx, t.data(), gvk[r], nd * sizeof(cplx)));
+      for (size_t i = 0; i < nd; ++i) dmax = std::max(dmax, std::abs(t[i] - vk[0][i]));
+    }
+    if (!(dmax <= 1e-12 * std::max(1.0, vmax))) {
+      fprintf(stderr, "group J/K differ from the 1-GPU J/K by %.3e\n", dmax);
+      return 1;
+    }
+    printf("capi_asan: fisdf_group of %d ranks: J/K within %.1e of the 1-GPU build\n", n, dmax);
+    CHECK(fisdf_group_destroy(g));
+    for (int r = 0; r < n; ++r) {
+      CHECK(fisdf_free(ctx, gvj[r]));
+      CHECK(fisdf_free(ctx, gvk[r]));
+    }
+    const int bad[2] = {0, 1 << 20};
+    fisdf_group* g2 = nullptr;
+    if (fisdf_group_create(2, bad, FISDF_GROUP_COPY, &g2) == 0 || g2 != nullptr ||
+        !strstr(fisdf_last_error(nullptr), "group_create")) {
+      fprintf(stderr, "a group with a bad device did not fail as documented\n");
+      return 1;
+    }
   }
 
   for (void* p : {d_x0, d_f, d_dms, d_vj, d_vk}) CHECK(fisdf_free(ctx, p));
