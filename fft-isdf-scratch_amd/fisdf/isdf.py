@@ -318,6 +318,60 @@ class InterpolativeSeparableDensityFitting:
         self._dev_state = dict(X=X)
         self.nip = nip
 
+    # ---- checkpoint (the reference keeps _x / _w0 / _wq in memory only) ---------
+    _DUMP_VERSION = 1
+
+    def dump(self, path):
+        """Save what build() left resident — the interpolation points, X (``_x``), the fitted W_q
+        (``_wq`` of the fitted q; the others are their time-reversal partners' conjugates) and
+        W_s — to an ``.npz`` of plain arrays (no pickles), so that another process can call
+        get_jk / get_eri on the same cell without building again (``load``).  A k-sharded build
+        (W_q and the W_s rows distributed over the ranks) is not saved: NotImplementedError."""
+        st = self._dev_state
+        if st is None or "Ws" not in st:
+            raise RuntimeError("ISDF.dump: call build() first")
+        if self.device.sharded(self):
+            raise NotImplementedError("ISDF.dump of a k-sharded build (W_q are distributed)")
+        np.savez(path, version=self._DUMP_VERSION, kmesh=np.asarray(self.kmesh, np.int64),
+                 mesh=np.asarray(self.mesh, np.int64),
+                 a=np.asarray(self.cell.lattice_vectors(), float), nao=self.cell.nao_nr(),
+                 perm=self.perm, fit_qs=self.fit_qs, q_partner=self.q_partner, ranks=self.ranks,
+                 X=st["X"].cpu().numpy(), Wq=st["Wq"].cpu().numpy(), Ws=st["Ws"].cpu().numpy(),
+                 time_reversal_used=bool(self.time_reversal_used),
+                 min_norm_slots=int(self.min_norm_slots),
+                 used_pivoted_fit=bool(self.used_pivoted_fit), tr_deviation=self.tr_deviation)
+
+    def load(self, path):
+        """Restore a ``dump`` into this object (the same lattice, FFT mesh, k-mesh and AO count,
+        checked: ValueError otherwise); afterwards get_jk / get_eri / _x / _w0 / _wq behave as
+        after the build that was saved.  Returns self."""
+        z = np.load(path)                                     # plain arrays: allow_pickle off
+        if int(z["version"]) != self._DUMP_VERSION:
+            raise ValueError(f"ISDF.load: dump version {int(z['version'])}")
+        kmesh = self._kmesh()
+        if (tuple(int(v) for v in z["kmesh"]) != tuple(int(v) for v in kmesh)
+                or tuple(int(v) for v in z["mesh"]) != tuple(int(v) for v in self.mesh)
+                or int(z["nao"]) != self.cell.nao_nr()
+                or not np.allclose(z["a"], np.asarray(self.cell.lattice_vectors(), float),
+                                   rtol=0, atol=1e-12)):
+            raise ValueError("ISDF.load: the dump is of another cell, FFT mesh or k-mesh")
+        if self.device.sharded(self):
+            raise NotImplementedError("ISDF.load into a k-sharded object")
+        d = self.device
+        Wq = d.to_dev(z["Wq"])
+        self._dev_state = dict(X=d.to_dev(z["X"]), Wq=Wq, W0=Wq[0], Ws=d.to_dev(z["Ws"]))
+        self.perm = np.asarray(z["perm"], np.int32)
+        self.fit_qs = np.asarray(z["fit_qs"], np.int32)
+        self.my_qs = self.fit_qs.copy()
+        self.q_partner = np.asarray(z["q_partner"], np.int32)
+        self.ranks = np.asarray(z["ranks"]).copy()
+        self.nip = len(self.perm)
+        self.time_reversal_used = bool(z["time_reversal_used"])
+        self.min_norm_slots = int(z["min_norm_slots"])
+        self.used_pivoted_fit = bool(z["used_pivoted_fit"])
+        self.tr_deviation = float(z["tr_deviation"])
+        return self
+
     def get_jk(self, dm, hermi=1, kpts=None, kpts_band=None, with_j=True, with_k=True,
                omega=None, exxdiv=None):
         """fftisdf.py:390-408."""

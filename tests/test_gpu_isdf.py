@@ -362,6 +362,38 @@ def test_get_eri_partner_q():
             assert abs(wq[df.q_partner[q]] - wq[q].conj()).max() == 0.0
 
 
+@pytest.mark.parametrize("name", ["toy333_fr", "toy222_rank"])
+def test_dump_load(name, tmp_path):
+    """ISDF.dump / ISDF.load (checkpoint): a fresh object on the same cell restored from
+    the .npz gives get_jk, get_eri and _x / _w0 / _wq bit for bit as after the build; a dump of
+    another k-mesh is refused."""
+    from fisdf import ISDF
+    df, o, dm = make_df(name)
+    df.build()
+    vj, vk = df.get_jk(dm)
+    path = tmp_path / "isdf.npz"
+    df.dump(path)
+    cell, kmesh, m0, c0, *_ = inputs(name)
+    df2 = ISDF(cell, cell.get_kpts(kmesh), m0=list(m0), c0=c0).load(path)
+    vj2, vk2 = df2.get_jk(dm)
+    assert np.array_equal(vj, vj2) and np.array_equal(vk, vk2)
+    for a in ("_x", "_w0", "_wq"):
+        assert np.array_equal(getattr(df, a), getattr(df2, a)), a
+    kpts = df.kpts
+    nk = len(kpts)
+    k4 = kpts[[0, min(1, nk - 1), min(2, nk - 1), 0]]
+    try:
+        e1 = df.get_eri(k4)
+    except ValueError:                      # momentum conservation: use a diagonal quartet
+        k4 = kpts[[0, 0, 0, 0]]
+        e1 = df.get_eri(k4)
+    assert np.array_equal(e1, df2.get_eri(k4))
+    other = tuple(int(v) + 1 if i == 0 else int(v) for i, v in enumerate(kmesh))
+    with pytest.raises(ValueError):
+        ISDF(cell, cell.get_kpts(other), m0=list(m0), c0=c0).load(path)
+    print(f"\n{name}: dump {path.stat().st_size / 1e6:.1f} MB, reloaded J/K, ERI, _wq bitwise")
+
+
 def test_get_eri_and_ao2mo():
     """next-2: ISDF ERIs vs the exact FFT ERI (fftdf-with-k-lstsq.py:219-258 harness: fails
     above 1e-4) and vs the oracle's ISDF ERI; ao2mo with MO coefficients == transformed AO ERI."""

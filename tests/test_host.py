@@ -76,6 +76,23 @@ def test_reference_surface():
         df.get_jk(dm[0], kpts=np.zeros(3))         # single k-point (fftisdf.py:399-401)
 
 
+def test_dump_load_checks(tmp_path):
+    """ISDF.dump before a build raises; ISDF.load refuses a dump of another version, k-mesh or
+    lattice before it touches a device (the bitwise round trip is tests/test_gpu_isdf.py)."""
+    from fisdf import ISDF, cell as C
+    cell = C.diamond_cell(mesh=(8, 8, 8))
+    df = ISDF(cell, cell.get_kpts((2, 2, 1)))
+    with pytest.raises(RuntimeError):
+        df.dump(tmp_path / "x.npz")
+    good = dict(version=1, kmesh=np.array([2, 2, 1]), mesh=np.array([8, 8, 8]),
+                a=np.asarray(cell.lattice_vectors(), float), nao=cell.nao_nr())
+    for bad in (dict(version=2), dict(kmesh=np.array([2, 1, 2])), dict(a=good["a"] * 1.01),
+                dict(nao=cell.nao_nr() + 1)):
+        np.savez(tmp_path / "bad.npz", **{**good, **bad})
+        with pytest.raises(ValueError):
+            ISDF(cell, cell.get_kpts((2, 2, 1))).load(tmp_path / "bad.npz")
+
+
 def test_time_reversal_reps():
     from fisdf.kshard import time_reversal_reps
     for kmesh, nrep in [((4, 4, 4), 36), ((2, 2, 2), 8), ((3, 3, 1), 5), ((1, 1, 1), 1),
